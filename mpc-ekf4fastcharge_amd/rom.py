@@ -1,0 +1,446 @@
+"""ROM container, synthetic NMC30-like ROM generator and device packing.
+
+The reference loads ``ROM_NMC30_HRA.mat`` (runMPC.m:4-5).  That file is listed in
+the reference's ``.MISSING_LARGE_BLOBS:1`` and is absent, and it also carries the
+``cellData.function.*`` MATLAB handles the hot path calls (OB_step.m:203-219,
+iterEKF.m:282-283,362-363,392-407, EKFmatsHandler.m:53-92).  This module
+
+* defines :class:`ROM`, a plain-array mirror of the MATLAB ``ROM`` struct
+  (``ROMmdls(T,Z).{A,B,C,D,T,SOC}``, ``tfData.{names,xLoc}``,
+  ``xraData.{T,SOC,Tsamp}``, ``cellData``);
+* defines the *tabulated* ``cellData.function`` semantics this framework uses
+  (piecewise-linear OCP tables, Arrhenius ``k0``, constant ``Rf``/``wDL``/``Cdl``),
+  identical in the numpy oracle, the C oracle and the HIP kernels;
+* generates a deterministic synthetic NMC30-like ROM (3 x 21 set-points, n = 5,
+  nz = 26 outputs) that satisfies every index check of iterEKF.m:692-734 and
+  OB_step.m:140-158;
+* resolves the output-row roles (iterEKF.m:610-735) and packs everything into
+  the flat arrays the C-ABI ``mpcekf_rom`` struct expects (include/mpcekf.h).
+
+A real ROM exported from MATLAB can be loaded with :func:`ROM.load_npz` as long as
+its cellData functions are tabulated in the same format.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+# --------------------------------------------------------------------------
+# tfData name codes (shared with include/mpcekf.h: MPCEKF_TF_*)
+# --------------------------------------------------------------------------
+TF_NAMES = [
+    "negIfdl", "posIfdl", "negIf", "posIf", "negIdl", "posIdl",
+    "negPhis", "posPhis", "negPhise", "posPhise", "negThetass", "posThetass",
+    "negPhie", "sepPhie", "posPhie", "negThetae", "sepThetae", "posThetae",
+]
+TF_CODE = {n: i for i, n in enumerate(TF_NAMES)}
+
+# Role slots: the 11 rows the hot path addresses individually.  The device
+# layout puts them first, in this order (see DESIGN.md "row permutation").
+ROLE_NAMES = ["Ifdl0", "Ifdl3", "If0", "If3", "Thetass0", "Thetass3",
+              "Thetae1", "Thetae_end", "Phie_end", "Phise0", "negPhise2"]
+NROLE = len(ROLE_NAMES)
+
+# per-row group flags (include/mpcekf.h: MPCEKF_G_*)
+G_NEG_THETASS = 1 << 0
+G_POS_THETASS = 1 << 1
+G_NEG_PHISE = 1 << 2
+G_POS_PHISE = 1 << 3
+G_PHIE = 1 << 4          # member of ind.Phie (after the loc==0 drop)
+G_PHIE_LOC0 = 1 << 5     # member of ind.Phie with loc == 0 (iterEKF.m:374-375)
+G_THETAE = 1 << 6
+G_POS_PHIS = 1 << 7
+
+# getChatZ Chat0 kinds (iterEKF.m:540-586), last assignment wins
+C0_ZERO, C0_CHATV0, C0_RES0N, C0_RES0P, C0_DUN_RES0N, C0_DUP_RES0P, C0_MDUN_RES0N = range(7)
+
+EPS = np.finfo(float).eps
+
+
+@dataclass
+class Electrode:
+    theta0: float
+    theta100: float
+    Rf: float
+    k0ref: float
+    Ea_k0: float
+    wDL: float
+    Cdl: float
+    nDL: float
+    U: np.ndarray          # OCP table on a uniform grid over theta in [0, 1]
+    dUdT: np.ndarray       # entropic coefficient table (V/K)
+    dU: np.ndarray         # dUocp/dtheta table
+
+
+def interp_tab(tab: np.ndarray, x: float) -> float:
+    """Piecewise-linear table lookup on a uniform grid over [0, 1].
+
+    NaN in -> NaN out; the abscissa is clamped to [0, 1].  The C oracle
+    (oracle/mpcekf_oracle.c: tab_interp) and the kernels (csrc: tab_interp)
+    evaluate exactly this expression sequence.
+    """
+    if x != x:
+        return float("nan")
+    n = tab.shape[0]
+    xc = min(max(x, 0.0), 1.0)
+    t = xc * (n - 1)
+    i = int(math.floor(t))
+    if i > n - 2:
+        i = n - 2
+    f = t - i
+    return float(tab[i] + f * (tab[i + 1] - tab[i]))
+
+
+class CellFunctions:
+    """Tabulated stand-in for one electrode's ``cellData.function.{neg,pos}``."""
+
+    def __init__(self, e: Electrode, Tref: float, R: float):
+        self.e = e
+        self.Tref = Tref
+        self.R = R
+
+    def soc(self, z, T=None):                 # cellData.function.neg.soc(z,T)
+        e = self.e
+        return e.theta0 + z * (e.theta100 - e.theta0)
+
+    def Uocp(self, theta, T=None):            # 1-arg call == Tref (EKFmatsHandler.m:96)
+        if T is None:
+            T = self.Tref
+        return interp_tab(self.e.U, theta) + (T - self.Tref) * interp_tab(self.e.dUdT, theta)
+
+    def dUocp(self, theta, T=None):
+        return interp_tab(self.e.dU, theta)
+
+    def k0(self, theta, T):
+        e = self.e
+        return e.k0ref * math.exp(e.Ea_k0 / self.R * (1.0 / self.Tref - 1.0 / T))
+
+    def Rf(self, theta, T=None):
+        return self.e.Rf
+
+    def wDL(self, theta=None, T=None):
+        return self.e.wDL
+
+    def Cdl(self, theta=None, T=None):
+        return self.e.Cdl
+
+    def nDL(self):
+        return self.e.nDL
+
+    def theta0(self):
+        return self.e.theta0
+
+    def theta100(self):
+        return self.e.theta100
+
+
+@dataclass
+class ROM:
+    """Plain-array mirror of the MATLAB ROM struct (runMPC.m:5)."""
+    T_degC: np.ndarray         # xraData.T  [nT] (ascending)
+    SOC_pct: np.ndarray        # xraData.SOC [nZ] (ascending)
+    Ts: float                  # xraData.Tsamp
+    A: np.ndarray              # [nT, nZ, n+1] diag(ROMmdls(t,z).A), last == 1
+    C: np.ndarray              # [nT, nZ, nz, n+1]
+    D: np.ndarray              # [nT, nZ, nz]
+    names: list                # tfData.names [nz]
+    xloc: np.ndarray           # tfData.xLoc [nz]
+    F: float
+    R: float
+    Q: float                   # cellData.function.const.Q(), Ah
+    Rc: float
+    Tref: float
+    neg: Electrode
+    pos: Electrode
+    meta: dict = field(default_factory=dict)
+
+    # ---- shapes -------------------------------------------------------
+    @property
+    def nT(self):
+        return self.A.shape[0]
+
+    @property
+    def nZ(self):
+        return self.A.shape[1]
+
+    @property
+    def n(self):
+        return self.A.shape[2] - 1
+
+    @property
+    def nz(self):
+        return self.C.shape[2]
+
+    @property
+    def NM(self):
+        return self.nT * self.nZ
+
+    def fn(self, which):
+        return CellFunctions(self.neg if which == "neg" else self.pos, self.Tref, self.R)
+
+    # ROMmdls(t,z).T / .SOC exactly as initKF.m:57-59 reads them
+    def mdl_T_K(self):
+        return np.array([self.T_degC[t] + 273.15 for t in range(self.nT)])
+
+    def mdl_Z(self):
+        return np.array([self.SOC_pct[z] / 100 for z in range(self.nZ)])
+
+    # ---- index resolution (iterEKF.m:610-735, OB_step.m:86-163) --------
+    def resolve_indices(self):
+        names = list(self.names)
+        loc = np.asarray(self.xloc, dtype=float)
+
+        def find(nm):
+            return [i for i, s in enumerate(names) if s == nm]
+
+        ind = {nm: find(nm) for nm in TF_NAMES}
+        Ifdl = ind["negIfdl"] + ind["posIfdl"]
+        If = ind["negIf"] + ind["posIf"]
+        Thetass = ind["negThetass"] + ind["posThetass"]
+        Phise = ind["negPhise"] + ind["posPhise"]
+        Phie = ind["negPhie"] + ind["sepPhie"] + ind["posPhie"]
+        Thetae = ind["negThetae"] + ind["sepThetae"] + ind["posThetae"]
+
+        def at(lst, x):
+            return [i for i in lst if loc[i] == x]
+
+        r = {}
+        r["Ifdl0"], r["Ifdl3"] = at(Ifdl, 0), at(Ifdl, 3)
+        r["If0"], r["If3"] = at(If, 0), at(If, 3)
+        r["Thetass0"], r["Thetass3"] = at(Thetass, 0), at(Thetass, 3)
+        r["Phise0"] = at(Phise, 0)
+        for k in ("Ifdl0", "Ifdl3", "If0", "If3", "Thetass0", "Thetass3", "Phise0"):
+            if len(r[k]) != 1:
+                raise ValueError(f"ROM must have exactly one {k} output (iterEKF.m:692-725); got {r[k]}")
+        if not Thetae or loc[Thetae[0]] > 0:
+            raise ValueError("Simulation requires thetae at negative-collector! (iterEKF.m:709)")
+        if loc[Thetae[-1]] > 3 + EPS or loc[Thetae[-1]] < 3 - EPS:
+            raise ValueError("Simulation requires thetae at positive-collector! (iterEKF.m:711)")
+        if Phie and loc[Phie[0]] == 0:       # iterEKF.m:728-731 (warning, dropped)
+            Phie = Phie[1:]
+        if not Phie or loc[Phie[-1]] > 3 + EPS or loc[Phie[-1]] < 3 - EPS:
+            raise ValueError("Simulation requires phie at positive-collector! (iterEKF.m:732)")
+        if len(ind["negPhise"]) < 2:
+            raise ValueError("EKFmatsHandler.m:97 needs ind.negPhise(2)")
+        # OB_step's own (stricter) lookups must land on the same rows (OB_step.m:131-137)
+        ob = {
+            "negIfdl0": [i for i in ind["negIfdl"] if loc[i] == 0],
+            "posIfdl3": [i for i in ind["posIfdl"] if loc[i] == 3],
+            "negIf0": [i for i in ind["negIf"] if loc[i] == 0],
+            "posIf3": [i for i in ind["posIf"] if loc[i] == 3],
+            "negThetass0": [i for i in ind["negThetass"] if loc[i] == 0],
+            "posThetass3": [i for i in ind["posThetass"] if loc[i] == 3],
+        }
+        pairs = [("negIfdl0", "Ifdl0"), ("posIfdl3", "Ifdl3"), ("negIf0", "If0"),
+                 ("posIf3", "If3"), ("negThetass0", "Thetass0"), ("posThetass3", "Thetass3")]
+        for a, b in pairs:
+            if ob[a] != r[b]:
+                raise ValueError(f"OB_step {a} and iterEKF {b} resolve to different rows")
+        roles = {k: r[k][0] for k in ("Ifdl0", "Ifdl3", "If0", "If3", "Thetass0", "Thetass3", "Phise0")}
+        roles["Thetae1"] = Thetae[0]
+        roles["Thetae_end"] = Thetae[-1]
+        roles["Phie_end"] = Phie[-1]
+        roles["negPhise2"] = ind["negPhise"][1]
+        rows = [roles[k] for k in ROLE_NAMES]
+        if len(set(rows)) != NROLE:
+            raise ValueError("role rows must be distinct for the device row permutation")
+        return dict(ind=ind, Ifdl=Ifdl, If=If, Thetass=Thetass, Phise=Phise, Phie=Phie,
+                    Thetae=Thetae, roles=roles, loc=loc)
+
+    def validate(self):
+        """initKF.m:66-91 structure checks plus grid ordering."""
+        if np.any(np.diff(self.T_degC) <= 0) or np.any(np.diff(self.SOC_pct) <= 0):
+            raise ValueError("ROM set-points must be strictly ascending")
+        if not np.all(self.A[..., -1] == 1):
+            raise ValueError("A does not have integrator state (initKF.m:74)")
+        self.resolve_indices()
+
+    # ---- device packing -------------------------------------------------
+    def device_layout(self):
+        """Row permutation + per-row flags for the kernels."""
+        info = self.resolve_indices()
+        roles = [info["roles"][k] for k in ROLE_NAMES]
+        perm = roles + [i for i in range(self.nz) if i not in roles]
+        loc = info["loc"]
+        flags = np.zeros(self.nz, dtype=np.int32)
+        c0 = np.zeros(self.nz, dtype=np.int32)
+        ind = info["ind"]
+        for i in ind["negThetass"]:
+            flags[i] |= G_NEG_THETASS
+        for i in ind["posThetass"]:
+            flags[i] |= G_POS_THETASS
+        for i in ind["negPhise"]:
+            flags[i] |= G_NEG_PHISE
+        for i in ind["posPhise"]:
+            flags[i] |= G_POS_PHISE
+        for i in info["Phie"]:
+            flags[i] |= G_PHIE
+            if loc[i] == 0:
+                flags[i] |= G_PHIE_LOC0
+        for i in info["Thetae"]:
+            flags[i] |= G_THETAE
+        for i in ind["posPhis"]:
+            flags[i] |= G_POS_PHIS
+        # Chat0 assignment order of getChatZ (iterEKF.m:553-586)
+        for i in ind["posPhis"]:
+            c0[i] = C0_CHATV0
+        for i in ind["negThetass"]:
+            c0[i] = C0_RES0N
+        for i in ind["posThetass"]:
+            c0[i] = C0_RES0P
+        for i in ind["negPhise"]:
+            c0[i] = C0_DUN_RES0N
+        for i in ind["posPhise"]:
+            c0[i] = C0_DUP_RES0P
+        for i in info["Phie"]:
+            c0[i] = C0_MDUN_RES0N
+        # C row of Phise0 used by the Phie rows in getChatZ is role slot 9
+        return dict(perm=np.array(perm, dtype=np.int32),
+                    flags=flags[perm].astype(np.int32),
+                    c0kind=c0[perm].astype(np.int32))
+
+    # ---- persistence ----------------------------------------------------
+    def to_npz_dict(self):
+        d = dict(T_degC=self.T_degC, SOC_pct=self.SOC_pct, Ts=self.Ts, A=self.A, C=self.C, D=self.D,
+                 names=np.array(self.names), xloc=self.xloc, F=self.F, R=self.R, Q=self.Q, Rc=self.Rc,
+                 Tref=self.Tref)
+        for side, e in (("neg", self.neg), ("pos", self.pos)):
+            for k, v in e.__dict__.items():
+                d[f"{side}_{k}"] = v
+        return d
+
+    def save_npz(self, path):
+        np.savez(path, **self.to_npz_dict())
+
+    @staticmethod
+    def load_npz(path):
+        z = np.load(path, allow_pickle=False)
+
+        def el(side):
+            keys = ["theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL"]
+            kw = {k: float(z[f"{side}_{k}"]) for k in keys}
+            for k in ("U", "dUdT", "dU"):
+                kw[k] = np.array(z[f"{side}_{k}"], dtype=float)
+            return Electrode(**kw)
+
+        return ROM(T_degC=np.array(z["T_degC"], float), SOC_pct=np.array(z["SOC_pct"], float),
+                   Ts=float(z["Ts"]), A=np.array(z["A"], float), C=np.array(z["C"], float),
+                   D=np.array(z["D"], float), names=[str(s) for s in z["names"]],
+                   xloc=np.array(z["xloc"], float), F=float(z["F"]), R=float(z["R"]),
+                   Q=float(z["Q"]), Rc=float(z["Rc"]), Tref=float(z["Tref"]),
+                   neg=el("neg"), pos=el("pos"))
+
+
+# --------------------------------------------------------------------------
+# Synthetic NMC30-like ROM
+# --------------------------------------------------------------------------
+# Output list: (tf name, xLoc, D [V or flux per A], DC gain per mode per A, res0 kind)
+# Sign convention of the reference: Iapp < 0 charges (OB_step.m:7).
+_M = 1.0 / 30.0   # flux normalisation: |i_f| ~ 1 at 1C
+_OUTPUTS = [
+    ("negIfdl", 0.0, +1.40 * _M, [-0.25 * _M, -0.10 * _M, -0.05 * _M, 0, 0], None),
+    ("negIfdl", 1.0, +0.60 * _M, [+0.25 * _M, +0.10 * _M, +0.05 * _M, 0, 0], None),
+    ("posIfdl", 2.0, -0.70 * _M, [-0.20 * _M, -0.10 * _M, 0, 0, 0], None),
+    ("posIfdl", 3.0, -1.30 * _M, [+0.20 * _M, +0.10 * _M, 0, 0, 0], None),
+    ("negIf", 0.0, +1.20 * _M, [-0.05 * _M, -0.10 * _M, -0.05 * _M, 0, 0], None),
+    ("negIf", 1.0, +0.80 * _M, [+0.05 * _M, +0.10 * _M, +0.05 * _M, 0, 0], None),
+    ("posIf", 2.0, -0.90 * _M, [-0.05 * _M, -0.05 * _M, 0, 0, 0], None),
+    ("posIf", 3.0, -1.10 * _M, [+0.05 * _M, +0.05 * _M, 0, 0, 0], None),
+    ("negIdl", 0.0, +0.20 * _M, [-0.20 * _M, 0, 0, 0, 0], None),
+    ("posIdl", 3.0, -0.20 * _M, [+0.20 * _M, 0, 0, 0, 0], None),
+    ("negPhis", 1.0, +2e-5, [1e-5, 0, 0, 0, 0], None),
+    ("posPhis", 2.0, -1e-5, [-1e-5, 0, 0, 0, 0], None),
+    ("posPhis", 3.0, -2e-5, [-1e-5, 0, 0, 0, 0], None),
+    ("negPhise", 0.0, +3.0e-4, [1e-4, 1e-4, 1e-4, 1.5e-4, 5e-5], None),
+    ("negPhise", 1.0, +4.0e-4, [1e-4, 1e-4, 2e-4, 2e-4, 5e-5], None),
+    ("posPhise", 3.0, -3.0e-4, [-1e-4, -1e-4, -1e-4, -1e-4, 0], None),
+    ("negThetass", 0.0, 0.0, [0, 0, -4e-4, -6e-4, -1e-4], "n"),
+    ("negThetass", 1.0, 0.0, [0, 0, -5e-4, -7e-4, -1e-4], "n"),
+    ("posThetass", 2.0, 0.0, [0, 0, 3.5e-4, 4.5e-4, 1e-4], "p"),
+    ("posThetass", 3.0, 0.0, [0, 0, 3.0e-4, 4.0e-4, 1e-4], "p"),
+    ("negPhie", 1.0, -1e-4, [-5e-5, -5e-5, 0, 0, 0], None),
+    ("sepPhie", 1.5, -2e-4, [-1e-4, -1e-4, -5e-5, 0, 0], None),
+    ("posPhie", 3.0, -4e-4, [-1e-4, -2e-4, -2e-4, 0, 0], None),
+    ("negThetae", 0.0, 0.0, [0, 5e-4, 1e-3, 1e-3, 0], None),
+    ("sepThetae", 1.5, 0.0, [0, 2e-4, 3e-4, 0, 0], None),
+    ("posThetae", 3.0, 0.0, [0, -5e-4, -1e-3, -1e-3, 0], None),
+]
+_FLUX = {"negIfdl", "posIfdl", "negIf", "posIf", "negIdl", "posIdl"}
+_TAU_REF = np.array([2.0, 8.0, 30.0, 120.0, 500.0])   # s at 25 degC
+
+
+def _u_neg(th):
+    # graphite-like: ~0.20 V at 10 % SOC, ~0.14 V at 53 %, ~0.09 V at 100 %
+    return (0.088 + 0.1 * np.exp(-8 * th) + 0.03 * (1 - np.tanh((th - 0.55) / 0.12))
+            + 0.4 * np.exp(-60 * th))
+
+
+def _u_pos(th):
+    # NMC-like: OCV(z) ~ 3.56 V at 10 %, ~4.07 V at 95 % with the graphite curve
+    d = th - 0.4965
+    return 4.10 - 1.31 * d + 0.9 * d * d - 0.3 * np.exp(40 * (th - 1.0)) + 0.2 * np.exp(-40 * (th - 0.35))
+
+
+def _deriv(fun, th, h=1e-6):
+    return (fun(th + h) - fun(th - h)) / (2 * h)
+
+
+def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), Ts=1.0,
+                   ntab=201) -> ROM:
+    """Deterministic synthetic NMC30-like xRA ROM.
+
+    Every number is fixed here; nothing random.  Local models differ smoothly with
+    temperature (Arrhenius) and SOC so the bilinear blends of OB_step.m:281-285 and
+    iterEKF.m:312-313 exercise real interpolation.
+    """
+    T_degC = np.asarray(T_degC, dtype=float)
+    SOC_pct = np.asarray(SOC_pct, dtype=float)
+    R = 8.3144621
+    F = 96485.3365
+    Q = 29.86
+    Tref = 298.15
+    n = 5
+    nT, nZ, nz = len(T_degC), len(SOC_pct), len(_OUTPUTS)
+
+    th = np.linspace(0.0, 1.0, ntab)
+    neg = Electrode(theta0=0.01, theta100=0.80, Rf=2.0e-3, k0ref=2.0, Ea_k0=3.0e4,
+                    wDL=5.0, Cdl=150.0, nDL=0.95,
+                    U=_u_neg(th), dUdT=-1.0e-4 * np.exp(-5 * th), dU=_deriv(_u_neg, th))
+    pos = Electrode(theta0=0.93, theta100=0.40, Rf=3.0e-3, k0ref=4.0, Ea_k0=4.0e4,
+                    wDL=5.0, Cdl=120.0, nDL=0.93,
+                    U=_u_pos(th), dUdT=-0.5e-4 * (1 - th), dU=_deriv(_u_pos, th))
+    res0n = -Ts * (neg.theta100 - neg.theta0) / (3600 * Q)
+    res0p = -Ts * (pos.theta100 - pos.theta0) / (3600 * Q)
+
+    A = np.zeros((nT, nZ, n + 1))
+    C = np.zeros((nT, nZ, nz, n + 1))
+    D = np.zeros((nT, nZ, nz))
+    for t in range(nT):
+        TK = T_degC[t] + 273.15
+        f_res = math.exp(2.0e4 / R * (1.0 / TK - 1.0 / Tref))   # resistive gains
+        f_tau = math.exp(1.5e4 / R * (1.0 / TK - 1.0 / Tref))   # slower when cold
+        for z in range(nZ):
+            zz = SOC_pct[z] / 100.0
+            f_soc = 1.0 + 0.3 * (zz - 0.5) ** 2
+            tau = _TAU_REF * f_tau * (1.0 + 0.2 * (zz - 0.5) ** 2) * np.array([1.0, 1.02, 1.05, 1.1, 1.2])
+            a = np.exp(-Ts / tau)
+            A[t, z, :n] = a
+            A[t, z, n] = 1.0
+            for r, (nm, _loc, d, g, r0) in enumerate(_OUTPUTS):
+                if nm in _FLUX:
+                    scale = 1.0 + 0.1 * (zz - 0.5)
+                elif "Thetass" in nm or "Thetae" in nm:
+                    scale = f_tau
+                else:
+                    scale = f_res * f_soc
+                C[t, z, r, :n] = np.asarray(g, dtype=float) * scale * (1.0 - a)
+                D[t, z, r] = d * scale
+                C[t, z, r, n] = res0n if r0 == "n" else (res0p if r0 == "p" else 0.0)
+    rom = ROM(T_degC=T_degC, SOC_pct=SOC_pct, Ts=float(Ts), A=A, C=C, D=D,
+              names=[o[0] for o in _OUTPUTS], xloc=np.array([o[1] for o in _OUTPUTS]),
+              F=F, R=R, Q=Q, Rc=8.0e-4, Tref=Tref, neg=neg, pos=pos,
+              meta={"kind": "synthetic-NMC30-like", "version": 1})
+    rom.validate()
+    return rom

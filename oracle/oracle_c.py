@@ -1,0 +1,177 @@
+"""ctypes front-end of oracle/mpcekf_oracle.c -- TEST INFRASTRUCTURE ONLY.
+
+PARITY UNPINNED (see oracle_np.py).  Used by tests/ as the checker of the HIP
+kernels and by bench.py's ``cpu_baseline`` leg (kind "port").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+TF_CODES = {n: i for i, n in enumerate([
+    "negIfdl", "posIfdl", "negIf", "posIf", "negIdl", "posIdl", "negPhis", "posPhis",
+    "negPhise", "posPhise", "negThetass", "posThetass", "negPhie", "sepPhie", "posPhie",
+    "negThetae", "sepThetae", "posThetae"])}
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class _Electrode(C.Structure):
+    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("Rf", C.c_double),
+                ("k0ref", C.c_double), ("Ea", C.c_double), ("wDL", C.c_double), ("Cdl", C.c_double),
+                ("nDL", C.c_double), ("ntab", C.c_int), ("U", _dp), ("dUdT", _dp), ("dU", _dp)]
+
+
+class _Rom(C.Structure):
+    _fields_ = [("nT", C.c_int), ("nZ", C.c_int), ("n", C.c_int), ("nz", C.c_int),
+                ("T_degC", _dp), ("SOC_pct", _dp), ("Ts", C.c_double), ("A", _dp), ("C", _dp),
+                ("D", _dp), ("tf", _ip), ("xloc", _dp), ("F", C.c_double), ("R", C.c_double),
+                ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double),
+                ("neg", _Electrode), ("pos", _Electrode)]
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("Np", C.c_int), ("Nc", C.c_int), ("ref", C.c_double), ("u_max", C.c_double),
+                ("Crate", C.c_double), ("du_min", C.c_double), ("du_max", C.c_double),
+                ("v_max", C.c_double), ("phise_min", C.c_double), ("z_max", C.c_double),
+                ("z_tol", C.c_double), ("use_cur", C.c_int), ("use_v", C.c_int),
+                ("use_eta", C.c_int), ("maxHild", C.c_int), ("hild_tol", C.c_double),
+                ("SigmaV", C.c_double), ("SigmaW", C.c_double), ("SigmaX0", C.c_double * 6),
+                ("max_warn", C.c_int)]
+
+
+def build(quiet=True):
+    subprocess.run(["make", "-s", "-C", HERE], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_run.restype = C.c_int
+        L.orc_run.argtypes = [C.POINTER(_Rom), C.POINTER(_Cfg), C.c_int, _dp, _dp, C.c_int,
+                              _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, C.c_int]
+        L.orc_predmat.argtypes = [_dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp]
+        L.orc_hildreth.restype = C.c_int
+        L.orc_hildreth.argtypes = [C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_int, C.c_double, _dp]
+        L.orc_sigma_min.restype = C.c_double
+        L.orc_sigma_min.argtypes = [C.c_int, _dp]
+        L.orc_meas_cov.argtypes = [_dp, _dp, C.c_double, C.c_int]
+        L.orc_jacobi.argtypes = [C.c_int, _dp, _dp, _dp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_dp)
+
+
+class PackedRom:
+    """Keeps the numpy buffers alive for the lifetime of the struct."""
+
+    def __init__(self, rom):
+        self.keep = []
+
+        def arr(x, dt=np.float64):
+            a = np.ascontiguousarray(x, dtype=dt)
+            self.keep.append(a)
+            return a
+
+        r = _Rom()
+        r.nT, r.nZ, r.n, r.nz = rom.nT, rom.nZ, rom.n, rom.nz
+        r.T_degC = _p(arr(rom.T_degC))
+        r.SOC_pct = _p(arr(rom.SOC_pct))
+        r.Ts = rom.Ts
+        r.A = _p(arr(rom.A))
+        r.C = _p(arr(rom.C))
+        r.D = _p(arr(rom.D))
+        r.tf = arr([TF_CODES[n] for n in rom.names], np.int32).ctypes.data_as(_ip)
+        r.xloc = _p(arr(rom.xloc))
+        r.F, r.R, r.Q, r.Rc, r.Tref = rom.F, rom.R, rom.Q, rom.Rc, rom.Tref
+        for side in ("neg", "pos"):
+            e = getattr(rom, side)
+            s = getattr(r, side)
+            s.theta0, s.theta100, s.Rf, s.k0ref, s.Ea = e.theta0, e.theta100, e.Rf, e.k0ref, e.Ea_k0
+            s.wDL, s.Cdl, s.nDL, s.ntab = e.wDL, e.Cdl, e.nDL, len(e.U)
+            s.U, s.dUdT, s.dU = _p(arr(e.U)), _p(arr(e.dUdT)), _p(arr(e.dU))
+        self.s = r
+
+
+DEFAULTS = dict(Np=5, Nc=2, ref=95.0, u_max=2.0, Crate=2.0, du_min=-50.0, du_max=50.0, v_max=4.1,
+                phise_min=0.08, z_max=0.95, z_tol=0.0, constraints=(1, 1, 1), maxHild=100,
+                hild_tol=1e-6, SigmaV=1e-3, SigmaW=1e2, SigmaX0=(1, 1, 1, 1, 1, 2e6), max_warn=10)
+
+
+def make_cfg(**kw):
+    d = dict(DEFAULTS)
+    d.update(kw)
+    c = _Cfg()
+    c.Np, c.Nc = d["Np"], d["Nc"]
+    for k in ("ref", "u_max", "Crate", "du_min", "du_max", "v_max", "phise_min", "z_max", "z_tol",
+              "hild_tol", "SigmaV", "SigmaW"):
+        setattr(c, k, float(d[k]))
+    c.use_cur, c.use_v, c.use_eta = (int(x) for x in d["constraints"])
+    c.maxHild = d["maxHild"]
+    c.max_warn = d["max_warn"]
+    for i in range(6):
+        c.SigmaX0[i] = float(d["SigmaX0"][i])
+    return c
+
+
+def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, **cfg):
+    """Batched closed loop on the CPU. Returns dict of [nsteps, ncells] arrays."""
+    soc0 = np.ascontiguousarray(soc0, dtype=np.float64)
+    tc = np.ascontiguousarray(tc, dtype=np.float64)
+    n = soc0.shape[0]
+    pr = PackedRom(rom)
+    c = make_cfg(**cfg)
+    out = {k: np.zeros((nsteps, n)) for k in ("u", "v", "soc", "phise")}
+    out["nexec"] = np.zeros((nsteps, n), dtype=np.int32)
+    out["status"] = np.zeros(n, dtype=np.int32)
+    zk = np.zeros((n, rom.nz + 2)) if want_zk else None
+    zbk = np.zeros((n, rom.nz + 2)) if want_zk else None
+    rc = lib().orc_run(C.byref(pr.s), C.byref(c), n, _p(soc0), _p(tc), nsteps, _p(out["u"]),
+                       _p(out["v"]), _p(out["soc"]), _p(out["phise"]),
+                       out["nexec"].ctypes.data_as(_ip), out["status"].ctypes.data_as(_ip),
+                       _p(zk) if want_zk else None, _p(zbk) if want_zk else None, nthreads)
+    if rc:
+        raise RuntimeError(f"orc_run failed: {rc}")
+    if want_zk:
+        out["zk"], out["zbk"] = zk, zbk
+    return out
+
+
+def predmat(a, Cr, D, Np, Nc):
+    Phi = np.zeros((Np, 7))
+    G = np.zeros((Np, Nc))
+    lib().orc_predmat(_p(np.ascontiguousarray(a, float)), _p(np.ascontiguousarray(Cr, float)),
+                      float(D), Np, Nc, _p(Phi), _p(G))
+    return Phi, G
+
+
+def hildreth(E, F, M, gamma, lam0, maxIter=100, tol=1e-6):
+    E = np.ascontiguousarray(E, float)
+    M = np.ascontiguousarray(M, float)
+    lam = np.array(lam0, dtype=float)
+    DU = np.zeros(E.shape[0])
+    it = lib().orc_hildreth(E.shape[0], M.shape[0], _p(E), _p(np.ascontiguousarray(F, float)), _p(M),
+                            _p(np.ascontiguousarray(gamma, float)), _p(lam), maxIter, tol, _p(DU))
+    return DU, lam, it
+
+
+def sigma_min(G):
+    G = np.ascontiguousarray(G, float)
+    return lib().orc_sigma_min(G.shape[0], _p(G))
