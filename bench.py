@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Benchmark: batched MPC+EKF control steps/s on MI355X (BASELINE.json metric).
+
+One step = one closed-loop pass of runMPC.m:84-111 (OB_step -> iterEKF ->
+EKFmatsHandler -> iterMPC/hildreth) over every cell of the batch.  Workload:
+65 536 cells per GPU (BASELINE.json configs[2], the north_star target config),
+synthetic NMC30-like ROM (3 x 21 set-points), Np=5 / Nc=2, SOC0 ~ U[5,30] %,
+TC ~ U[20,30] degC (seed 0x5EED).  Multi-GPU: one process per GPU, cells sharded
+contiguously with no collective on the data path (weak scaling); the only
+collectives are the timing barrier and the max-over-ranks of the elapsed time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cells-per-gpu C]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
+
+METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
+
+
+def algorithmic_bytes_per_cell(NM, ncon, bounds):
+    """Algorithmic HBM bytes each kernel moves per cell per step (DESIGN.md "Roofline").
+
+    bulk : every local model's EKF record (xhat 5 + packed SigmaX 15 doubles) and
+           plant state (6 doubles) read and written once, + 2 per-cell scalars.
+    cell : the 4 corner EKF records read+written, warm-start lambda read+written,
+           per-cell scalars/constants, trajectory outputs and zk.
+    plant: the 4 corner plant states read, per-cell scalars.
+    """
+    bulk = 2 * 8 * NM * (20 + 6) + 2 * 8
+    cell = 4 * 2 * 8 * 20 + 2 * 8 * ncon + 20 * 8 + 4 * 8 + 4 + 28 * 8 + (28 * 8 if bounds else 0)
+    plant = 4 * 6 * 8 + 12 * 8 + 8
+    return dict(bulk=bulk, cell=cell, plant=plant)
+
+
+def batch_inputs(n, seed=0x5EED):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return rng.uniform(5, 30, n), rng.uniform(20, 30, n)
+
+
+def cpu_baseline(rom, soc0, tc, cells, steps, threads):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c
+    t0 = time.perf_counter()
+    oracle_c.run(rom, soc0[:cells], tc[:cells], steps, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=cells * steps / dt, unit="cell-steps/s", cores=threads, kind="port",
+                sample=f"C oracle (oracle/mpcekf_oracle.c, -O3 fp64, OpenMP) on the first {cells} cells "
+                       f"of the workload x {steps} steps from init, {threads} host threads, {dt:.1f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--cells-per-gpu", type=int, default=65536)
+    ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
+    ap.add_argument("--cpu-cells", type=int, default=8192)
+    ap.add_argument("--cpu-steps", type=int, default=300)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
+    rom = P.make_synth_rom()
+    cpg = args.cells_per_gpu
+    total = cpg * world
+    soc0_all, tc_all = batch_inputs(total)
+    sl = slice(rank * cpg, (rank + 1) * cpg)
+    cfg = M.make_config(bounds=bool(args.bounds))
+    ctx = M.Context(rom, cpg, cfg, device=local)
+    ctx.init_cells(soc0_all[sl], tc_all[sl])
+    dev = torch.device("cuda", local)
+    K, W = args.steps, args.warmup
+    outs = [torch.empty((max(K, W), cpg), dtype=torch.float64, device=dev) for _ in range(4)]
+    nex = torch.empty((max(K, W), cpg), dtype=torch.int32, device=dev)
+    ptrs = [t.data_ptr() for t in outs] + [nex.data_ptr()]
+    if W:
+        ctx.step_device(W, *ptrs)
+    ctx.set_timing(True)
+    ctx.get_timing()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ctx.step_device(K, *ptrs)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    tim = ctx.get_timing()
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    status = ctx.get_state()["status"]
+    nerr = int((status & 1).sum())
+    u_last = outs[0][K - 1].double().cpu().numpy() if K else np.zeros(0)
+    mean_nexec = float(nex[:K].float().mean().item()) if K else 0.0
+    ctx.close()
+
+    if rank == 0:
+        cell_steps = total * K
+        value = cell_steps / dt if dt > 0 else 0.0
+        bpc = algorithmic_bytes_per_cell(rom.NM, 23, bool(args.bounds))
+        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1]) for k in tim}
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_launch"])
+        ms = per_kernel[dom]["ms_per_launch"]
+        achieved = bpc[dom] * cpg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        traffic = None
+        if os.path.exists(args.pmc):
+            try:
+                traffic = json.load(open(args.pmc)).get("per_launch_bytes", {}).get(dom)
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps, args.cpu_threads)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "cell-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": dt / K * 1e3 if K else 0.0,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (synthetic NMC30-like ROM; SOC0~U[5,30]%, TC~U[20,30]C, seed 0x5EED)",
+            "config": {
+                "workload": f"{cpg} cells per GPU ({total} total), Np=5 Nc=2, closed loop runMPC.m:84-111 "
+                            f"incl. plant, boundzk={'on' if args.bounds else 'off'}",
+                "cells_per_gpu": cpg, "total_cells": total, "Np": 5, "Nc": 2, "models_per_cell": rom.NM,
+                "rom_outputs": rom.nz, "parallelism": f"cell-shard x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "algorithmic_bytes_per_cell": bpc[dom],
+            },
+            "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
+                                gbs_algorithmic=round(bpc[k] * cpg / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
+                                if v["ms_per_launch"] > 0 else None)
+                        for k, v in per_kernel.items()},
+            "cpu_baseline": cpu,
+            "checks": {"cells_in_error": nerr, "mean_nexec": round(mean_nexec, 3),
+                       "u_last_mean": float(np.nanmean(u_last)) if u_last.size else None},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,214 @@
+/*
+ * mpcekf.h -- C-ABI of the MI355X batched MPC+EKF fast-charge control step.
+ *
+ * Drop-in boundary for the per-timestep loop of Rodrigops27/MPC-EKF4FastCharge
+ * (runMPC.m:83-112).  The reference has no FFI of its own: its public surface
+ * is the set of MATLAB functions runMPC.m calls by name.  Each entry point below
+ * replaces one of them, batched over independent cells:
+ *
+ *   mpcekf_plant_step   <- [Vcell,obs,cellState] = OB_step(Iapp,Tc,cellState,ROM)  OB_step.m:1
+ *   mpcekf_ekf_step     <- [zk,boundzk,ekfData,Xind] = iterEKF(vk,ik,Tk,ekfData)    iterEKF.m:30
+ *   mpcekf_linearize    <- [MPC,xhat] = EKFmatsHandler(ekfData,Xind,zk,Tk)         EKFmatsHandler.m:1
+ *   mpcekf_predmat      <- [Phi,G,aug] = predMat(A,B,C,D,Np,Nc)                    predMat.m:1
+ *   mpcekf_constraints  <- [M,gamma] = constraintsMPC(x_aug_k,cellState,mpcData)   constraintsMPC.m:1
+ *   mpcekf_mpc_step     <- [uk,mpcData] = iterMPC(xk,cellState,mpcData)            iterMPC.m:1
+ *   mpcekf_hildreth     <- [DU,lambda,nexec] = hildreth(E,F,M,gamma,lambda0,maxIter) hildreth.m:1
+ *   mpcekf_init_cells   <- initKF.m:30, initMPC.m:29, first OB_step call (runMPC.m:20,52,74)
+ *   mpcekf_step         <- the fused loop body runMPC.m:84-111, nsteps times
+ *
+ * Conventions
+ *  - Plain C types only; no exceptions cross the ABI.  Every function returns an
+ *    int status (MPCEKF_OK == 0); on failure mpcekf_last_error() returns a
+ *    thread-local message.
+ *  - Batched arrays are cell-major ("[ncells][k]") unless stated; trajectories
+ *    are step-major "[nsteps][ncells]".  All floating point is IEEE fp64.
+ *  - Host pointers unless the argument is documented as "device".  Every call
+ *    synchronises its HIP stream before returning.
+ *  - Per-cell soft failures never fail a call: they set bits in the per-cell
+ *    status word (MPCEKF_ST_*), after which that cell's outputs are NaN.  This
+ *    replaces the MATLAB errors/NaN lock-out of iterEKF.m:55-59,384-389.
+ *  - One context = one GPU + one HIP stream; use one host thread per context.
+ *    Multi-GPU runs create one context per device on disjoint cell ranges.
+ */
+#ifndef MPCEKF_H
+#define MPCEKF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCEKF_ABI_VERSION 1
+
+/* return codes */
+#define MPCEKF_OK 0
+#define MPCEKF_E_ARG -1         /* bad argument / size                                  */
+#define MPCEKF_E_ROM -2         /* ROM fails the initKF/iterEKF/OB_step structure checks */
+#define MPCEKF_E_HIP -3         /* HIP runtime error                                     */
+#define MPCEKF_E_UNSUPPORTED -4 /* configuration not built into this library             */
+#define MPCEKF_E_STATE -5       /* call order (e.g. step before init_cells)              */
+
+/* per-cell status bits */
+#define MPCEKF_ST_ERROR 1      /* cell stopped; outputs NaN from here on                       */
+#define MPCEKF_ST_LOCKOUT 2    /* warnCount > max_warn at iterEKF entry (iterEKF.m:55-59)      */
+#define MPCEKF_ST_THETAE_NEG 4 /* thetae < 0 in getVariables; MATLAB errors (iterEKF.m:384-389) */
+
+/* tfData.names codes (tf_code[] of mpcekf_rom) */
+enum {
+  MPCEKF_TF_negIfdl = 0, MPCEKF_TF_posIfdl, MPCEKF_TF_negIf, MPCEKF_TF_posIf, MPCEKF_TF_negIdl,
+  MPCEKF_TF_posIdl, MPCEKF_TF_negPhis, MPCEKF_TF_posPhis, MPCEKF_TF_negPhise, MPCEKF_TF_posPhise,
+  MPCEKF_TF_negThetass, MPCEKF_TF_posThetass, MPCEKF_TF_negPhie, MPCEKF_TF_sepPhie,
+  MPCEKF_TF_posPhie, MPCEKF_TF_negThetae, MPCEKF_TF_sepThetae, MPCEKF_TF_posThetae,
+  MPCEKF_TF_COUNT
+};
+
+/* One electrode of cellData.function.* in tabulated form (see DESIGN.md "ROM").
+ *   soc(z)       = theta0 + z*(theta100-theta0)
+ *   Uocp(th,T)   = interp(U,th) + (T-Tref)*interp(dUdT,th)   (1-arg call: T = Tref)
+ *   dUocp(th)    = interp(dU,th)
+ *   k0(th,T)     = k0ref*exp(Ea_k0/R*(1/Tref-1/T))
+ *   Rf, wDL, Cdl, nDL constants; interp = piecewise linear on a uniform grid over [0,1]. */
+typedef struct {
+  double theta0, theta100, Rf, k0ref, Ea_k0, wDL, Cdl, nDL;
+  int32_t ntab;
+  const double *U, *dUdT, *dU; /* [ntab] each */
+} mpcekf_electrode;
+
+/* The ROM struct of runMPC.m:5 as plain arrays.  Set-points ascending. */
+typedef struct {
+  int32_t nT, nZ;          /* ROMmdls is nT x nZ                                  */
+  int32_t n;               /* transient states per model (must be 5)               */
+  int32_t nz;              /* outputs per model                                    */
+  const double *T_degC;    /* xraData.T   [nT]                                     */
+  const double *SOC_pct;   /* xraData.SOC [nZ]                                     */
+  double Ts;               /* xraData.Tsamp                                        */
+  const double *A;         /* [nT][nZ][n+1]      diag(ROMmdls(t,z).A), last == 1   */
+  const double *C;         /* [nT][nZ][nz][n+1]  ROMmdls(t,z).C (with res0 column) */
+  const double *D;         /* [nT][nZ][nz]       ROMmdls(t,z).D                    */
+  const int32_t *tf_code;  /* [nz] MPCEKF_TF_*   tfData.names                      */
+  const double *tf_xloc;   /* [nz]               tfData.xLoc                       */
+  double F, R, Q, Rc, Tref;
+  mpcekf_electrode neg, pos;
+} mpcekf_rom;
+
+#define MPCEKF_CF_BOUNDS 1 /* also compute boundzk (iterEKF.m:186-205) */
+
+/* Controller/estimator configuration (runMPC.m:8-50, initMPC.m). */
+typedef struct {
+  int32_t Np, Nc;          /* horizons (runMPC.m:28-29)                          */
+  double target_soc;       /* mpcData.ref, percent (runMPC.m:30)                 */
+  double Crate;            /* u_min = -Q*Crate (initMPC.m:66-67)                 */
+  double u_max, du_min, du_max, v_min, v_max, phise_min, z_max, z_tol;
+  int32_t use_current, use_voltage, use_eta; /* constraint switches (runMPC.m:33) */
+  int32_t max_hild;        /* mpcData.maxHild (initMPC.m:47)                     */
+  double hild_tol;         /* hildreth.m:39 (1e-6)                               */
+  double SigmaV, SigmaW;   /* runMPC.m:18-19                                     */
+  double SigmaX0[6];       /* diagonal of SigmaX0 (runMPC.m:17)                  */
+  int32_t max_warn;        /* lock-out threshold (iterEKF.m:55: > 10)            */
+  int32_t flags;           /* MPCEKF_CF_*                                        */
+} mpcekf_config;
+
+/* Layout of one linearisation record (EKFmatsHandler outputs), doubles: */
+#define MPCEKF_LIN_A 0     /* [6] diag(A)              */
+#define MPCEKF_LIN_CSOC 6  /* [6] Csoc                 */
+#define MPCEKF_LIN_DSOC 12 /* Dsoc                     */
+#define MPCEKF_LIN_CV 13   /* [6] [Cv 0]               */
+#define MPCEKF_LIN_DV 19   /* Dv                       */
+#define MPCEKF_LIN_CPHI 20 /* [6] [Cphi 0]             */
+#define MPCEKF_LIN_DPHI 26 /* Dphi                     */
+#define MPCEKF_LIN_BV 27   /* bv                       */
+#define MPCEKF_LIN_BPHI 28 /* bphi                     */
+#define MPCEKF_LIN_XHAT 29 /* [6] xhat (model + 0)     */
+#define MPCEKF_LIN_SIZE 35
+
+typedef struct mpcekf_ctx mpcekf_ctx;
+
+int mpcekf_abi_version(void);
+const char *mpcekf_last_error(void);
+void mpcekf_config_defaults(mpcekf_config *cfg); /* the runMPC.m values */
+
+/* Context: owns the device copy of the ROM and the per-cell state (SoA/AoS in HBM). */
+int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int device, int64_t ncells,
+                      mpcekf_ctx **out);
+int mpcekf_ctx_destroy(mpcekf_ctx *ctx);
+int mpcekf_ctx_info(const mpcekf_ctx *ctx, int64_t *ncells, int32_t *nmodels, int32_t *nz, int32_t *ncon);
+
+/* initKF + initMPC + OB_step first call for every cell: SOC0 in percent, Tc in degC. */
+int mpcekf_init_cells(mpcekf_ctx *ctx, const double *soc0_pct, const double *tc_degC);
+
+/* nsteps fused closed-loop steps.  Each output may be NULL; non-NULL outputs are
+ * [nsteps][ncells] host arrays (or device arrays when outputs_on_device != 0):
+ *   traj_u = u_store (MPC command), traj_v = voltage_store, traj_soc = SOC_store
+ *   (zk(end)), traj_phise = phise_store, traj_nexec = mpcData.cost.nexec. */
+int mpcekf_step(mpcekf_ctx *ctx, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
+                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device);
+
+/* Optional per-step EKF output of the LAST mpcekf_step call: zk and boundzk
+ * ([ncells][nz+2], boundzk only with MPCEKF_CF_BOUNDS). */
+int mpcekf_get_zk(mpcekf_ctx *ctx, double *zk, double *boundzk);
+
+/* ---- stage entry points (one MATLAB function each; all batched over cells) ---- */
+/* OB_step: applies iapp[c] to the plant state, returns vcell[c]. */
+int mpcekf_plant_step(mpcekf_ctx *ctx, const double *iapp, double *vcell);
+/* iterEKF: zk/boundzk [ncells][nz+2] (boundzk may be NULL), xind_model [ncells][4]
+ * (model index t*nZ+z of Xind.theT/theZ), xind_gamma [ncells][4]. */
+int mpcekf_ekf_step(mpcekf_ctx *ctx, const double *vk, const double *ik, double *zk, double *boundzk,
+                    int32_t *xind_model, double *xind_gamma);
+/* EKFmatsHandler: lin [ncells][MPCEKF_LIN_SIZE]. */
+int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                     double *lin);
+/* iterMPC (uses and updates the context's uk_1 and lambda warm start):
+ * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec. */
+int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
+
+/* Context-free batched kernels (device chosen by `device`).
+ * predMat with A = diag(a), B = ones: a,C [n][6], D [n] -> Phi [n][Np][7], G [n][Np][Nc]. */
+int mpcekf_predmat(int device, int64_t n, int32_t Np, int32_t Nc, const double *a, const double *C,
+                   const double *D, double *Phi, double *G);
+/* constraintsMPC: lin [n][LIN], uk_1/soc_k1 [n] -> M [n][ncon][Nc], gamma [n][ncon]. */
+int mpcekf_constraints(int device, const mpcekf_config *cfg, double Q, int64_t n, const double *lin,
+                       const double *uk_1, const double *soc_k1, double *M, double *gamma);
+/* hildreth: E [n][Nc][Nc], F [n][Nc], M [n][ncon][Nc], gamma/lambda [n][ncon]; lambda is
+ * the warm start in and the multipliers out; DU [n][Nc]; nexec [n]. */
+int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const double *E, const double *F,
+                    const double *M, const double *gamma, double *lambda, int32_t max_iter, double tol,
+                    double *DU, int32_t *nexec);
+
+/* ---- instrumentation (not part of the reference interface) ---- */
+/* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
+ * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch
+ * counts of [plant, bulk, cell] since the last call and resets them. */
+#define MPCEKF_K_PLANT 0
+#define MPCEKF_K_BULK 1
+#define MPCEKF_K_CELL 2
+int mpcekf_set_timing(mpcekf_ctx *ctx, int32_t enable);
+int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
+
+/* ---- state access (open-loop parity, checkpoint/restore) ---- */
+typedef struct {
+  double *bigX;    /* [ncells][NM][6]   OB_step cellState.bigX (column per model)     */
+  double *ekf;     /* [ncells][NM][20]  per model: xhat[5], SigmaX packed upper [15] */
+  double *scal;    /* [ncells][MPCEKF_NSCAL] scalars, see MPCEKF_S_*                 */
+  double *lambda;  /* [ncells][ncon]    mpcData.lambda                               */
+  int32_t *warn;   /* [ncells]          iterEKF warnCount                            */
+  int32_t *status; /* [ncells]          MPCEKF_ST_*                                   */
+} mpcekf_state;
+
+#define MPCEKF_S_SOCNAVG 0 /* cellState.SOCnAvg          */
+#define MPCEKF_S_SOCPAVG 1 /* cellState.SOCpAvg          */
+#define MPCEKF_S_X0 2      /* ekfData.x0                 */
+#define MPCEKF_S_SIGMAX0 3 /* ekfData.SigmaX0            */
+#define MPCEKF_S_PRIORI 4  /* ekfData.priorI             */
+#define MPCEKF_S_UK_1 5    /* mpcData.uk_1               */
+#define MPCEKF_S_UK 6      /* command applied next step  */
+#define MPCEKF_S_VK 7      /* last plant voltage         */
+#define MPCEKF_NSCAL 8
+
+int mpcekf_get_state(mpcekf_ctx *ctx, mpcekf_state *st);
+int mpcekf_set_state(mpcekf_ctx *ctx, const mpcekf_state *st);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCEKF_H */

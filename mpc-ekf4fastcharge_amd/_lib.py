@@ -1,0 +1,121 @@
+"""ctypes binding of the C-ABI in include/mpcekf.h (libmpcekf.so, built in-tree).
+
+The product path is this library and nothing else: if it is missing the import
+fails loudly (there is no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libmpcekf.so")
+
+MPCEKF_OK = 0
+ST_ERROR, ST_LOCKOUT, ST_THETAE_NEG = 1, 2, 4
+CF_BOUNDS = 1
+LIN_SIZE = 35
+NSCAL = 8
+S_SOCNAVG, S_SOCPAVG, S_X0, S_SIGMAX0, S_PRIORI, S_UK_1, S_UK, S_VK = range(8)
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class Electrode(C.Structure):
+    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("Rf", C.c_double),
+                ("k0ref", C.c_double), ("Ea_k0", C.c_double), ("wDL", C.c_double), ("Cdl", C.c_double),
+                ("nDL", C.c_double), ("ntab", C.c_int32), ("U", _dp), ("dUdT", _dp), ("dU", _dp)]
+
+
+class Rom(C.Structure):
+    _fields_ = [("nT", C.c_int32), ("nZ", C.c_int32), ("n", C.c_int32), ("nz", C.c_int32),
+                ("T_degC", _dp), ("SOC_pct", _dp), ("Ts", C.c_double), ("A", _dp), ("C", _dp),
+                ("D", _dp), ("tf_code", _ip), ("tf_xloc", _dp), ("F", C.c_double), ("R", C.c_double),
+                ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double), ("neg", Electrode),
+                ("pos", Electrode)]
+
+
+class Config(C.Structure):
+    _fields_ = [("Np", C.c_int32), ("Nc", C.c_int32), ("target_soc", C.c_double), ("Crate", C.c_double),
+                ("u_max", C.c_double), ("du_min", C.c_double), ("du_max", C.c_double),
+                ("v_min", C.c_double), ("v_max", C.c_double), ("phise_min", C.c_double),
+                ("z_max", C.c_double), ("z_tol", C.c_double), ("use_current", C.c_int32),
+                ("use_voltage", C.c_int32), ("use_eta", C.c_int32), ("max_hild", C.c_int32),
+                ("hild_tol", C.c_double), ("SigmaV", C.c_double), ("SigmaW", C.c_double),
+                ("SigmaX0", C.c_double * 6), ("max_warn", C.c_int32), ("flags", C.c_int32)]
+
+
+class State(C.Structure):
+    _fields_ = [("bigX", _dp), ("ekf", _dp), ("scal", _dp), ("lam", _dp), ("warn", _ip), ("status", _ip)]
+
+
+class MpcekfError(RuntimeError):
+    pass
+
+
+EXPORTS = [
+    "mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_ctx_create",
+    "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_get_zk",
+    "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
+    "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
+    "mpcekf_set_timing", "mpcekf_get_timing",
+]
+
+_lib = None
+
+
+def load():
+    """Load libmpcekf.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpcekfError(f"{LIB_PATH} not found: run __graft_entry__.build() (hipcc gfx950)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.mpcekf_abi_version.restype = C.c_int
+    L.mpcekf_last_error.restype = C.c_char_p
+    L.mpcekf_config_defaults.argtypes = [C.POINTER(Config)]
+    L.mpcekf_config_defaults.restype = None
+    L.mpcekf_ctx_create.argtypes = [C.POINTER(Rom), C.POINTER(Config), C.c_int, C.c_int64, C.POINTER(vp)]
+    L.mpcekf_ctx_destroy.argtypes = [vp]
+    L.mpcekf_ctx_info.argtypes = [vp, C.POINTER(C.c_int64), _ip, _ip, _ip]
+    L.mpcekf_init_cells.argtypes = [vp, _dp, _dp]
+    L.mpcekf_step.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32]
+    L.mpcekf_get_zk.argtypes = [vp, _dp, _dp]
+    L.mpcekf_plant_step.argtypes = [vp, _dp, _dp]
+    L.mpcekf_ekf_step.argtypes = [vp, _dp, _dp, _dp, _dp, _ip, _dp]
+    L.mpcekf_linearize.argtypes = [vp, _dp, _ip, _dp, _dp]
+    L.mpcekf_mpc_step.argtypes = [vp, _dp, _dp, _dp, _ip]
+    L.mpcekf_predmat.argtypes = [C.c_int, C.c_int64, C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp]
+    L.mpcekf_constraints.argtypes = [C.c_int, C.POINTER(Config), C.c_double, C.c_int64, _dp, _dp, _dp,
+                                     _dp, _dp]
+    L.mpcekf_hildreth.argtypes = [C.c_int, C.c_int64, C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp,
+                                  C.c_int32, C.c_double, _dp, _ip]
+    L.mpcekf_get_state.argtypes = [vp, C.POINTER(State)]
+    L.mpcekf_set_state.argtypes = [vp, C.POINTER(State)]
+    L.mpcekf_set_timing.argtypes = [vp, C.c_int32]
+    L.mpcekf_get_timing.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
+    for nm in EXPORTS:
+        if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults"):
+            getattr(L, nm).restype = C.c_int
+    if L.mpcekf_abi_version() != 1:
+        raise MpcekfError("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != MPCEKF_OK:
+        raise MpcekfError(f"mpcekf error {rc}: {_lib.mpcekf_last_error().decode()}")
+
+
+def dptr(a):
+    return a.ctypes.data_as(_dp) if a is not None else None
+
+
+def iptr(a):
+    return a.ctypes.data_as(_ip) if a is not None else None

@@ -1,0 +1,62 @@
+"""Builds libmpcekf.so in-tree with hipcc for gfx950 (no JIT cache, no CPU fallback).
+
+Flags: ``-ffp-contract=off`` (no FMA contraction: the kernels reproduce the
+oracle's defined evaluation order) and never ``-ffast-math`` (IEEE NaN/inf
+semantics are part of the reference behaviour, SURVEY.md §7 hard part 3).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_build")
+LIB = os.path.join(OUT, "libmpcekf.so")
+ARCH = os.environ.get("MPCEKF_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
+          "-Wno-unused-result"]
+SOURCES = ["mpcekf_kernels.hip", "mpcekf_host.cpp"]
+DEPS = ["mpcekf_kernels.hpp", os.path.join("..", "..", "include", "mpcekf.h")]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else -1.0
+
+
+def _stale(obj, src):
+    newest = max([_mtime(src)] + [_mtime(os.path.join(SRC, d)) for d in DEPS])
+    return _mtime(obj) < newest
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OUT, exist_ok=True)
+    jobs = []
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(SRC, s)
+        obj = os.path.join(OUT, os.path.splitext(s)[0] + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src):
+            jobs.append([HIPCC, *CFLAGS, "-c", src, "-o", obj])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+    if jobs:
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            list(ex.map(run, jobs))
+    if jobs or force or not os.path.exists(LIB) or any(_mtime(o) > _mtime(LIB) for o in objs):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,822 @@
+// mpcekf_host.cpp -- C-ABI (include/mpcekf.h) over the gfx950 kernels.
+//
+// Owns: ROM validation (initKF.m:66-91, iterEKF.m:692-734, OB_step.m:140-158),
+// the output-row permutation and LDS blobs, device state allocation, per-cell
+// initialisation (initKF/initMPC/first OB_step), the fused step loop and the
+// stage entry points.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcekf.h"
+#include "mpcekf_kernels.hpp"
+
+using namespace mk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(MPCEKF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int NCON_BUILT = 4 * 2 + 3 * 5;  // Np = 5, Nc = 2 compiled into the kernels
+
+template <class T>
+int dalloc(T **p, size_t n) {
+  *p = nullptr;
+  if (n == 0) return MPCEKF_OK;
+  HIPCHK(hipMalloc((void **)p, n * sizeof(T)));
+  return MPCEKF_OK;
+}
+
+}  // namespace
+
+struct mpcekf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t n = 0;
+  int NM = 0, nz = 0, nzp = 0, ncon = 0;
+  bool initialized = false;
+  KRom r{};
+  KCfg k{};
+  KState s{};
+  mpcekf_config cfg{};
+  // device buffers owned by the context
+  double *d_cell_blob = nullptr, *d_plant_blob = nullptr, *d_bulk = nullptr;
+  double *d_const = nullptr;  // 8 per-cell constant arrays
+  double *d_scal = nullptr;   // 8 scalar state arrays + J_unc, J_fin
+  int *d_int = nullptr;       // warn, status, nviol
+  double *d_zk = nullptr, *d_zbk = nullptr;
+  // staging for host trajectories / stage IO (grown on demand)
+  double *d_tmp = nullptr;
+  size_t tmp_bytes = 0;
+  // per-kernel HIP-event timing (mpcekf_set_timing)
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  double t_ms[3] = {0, 0, 0};
+  int64_t t_n[3] = {0, 0, 0};
+  // electrode constants kept for per-cell initialisation (k0(T), Cdleff)
+  double Tref = 0, Rgas = 0, th0[2] = {0, 0}, th100[2] = {0, 0}, k0ref[2] = {0, 0}, Ea[2] = {0, 0};
+  double Cdl[2] = {0, 0}, wDL[2] = {0, 0}, nDL[2] = {0, 0};
+
+  int tmp(size_t bytes) {
+    if (bytes <= tmp_bytes) return MPCEKF_OK;
+    if (d_tmp) (void)hipFree(d_tmp);
+    d_tmp = nullptr;
+    tmp_bytes = 0;
+    HIPCHK(hipMalloc((void **)&d_tmp, bytes));
+    tmp_bytes = bytes;
+    return MPCEKF_OK;
+  }
+};
+
+extern "C" {
+
+int mpcekf_abi_version(void) { return MPCEKF_ABI_VERSION; }
+
+const char *mpcekf_last_error(void) { return g_err.c_str(); }
+
+void mpcekf_config_defaults(mpcekf_config *c) {
+  std::memset(c, 0, sizeof(*c));
+  c->Np = 5;                  // runMPC.m:28
+  c->Nc = 2;                  // runMPC.m:29
+  c->target_soc = 95;         // runMPC.m:30
+  c->Crate = 2;               // runMPC.m:36
+  c->u_max = 2;               // runMPC.m:37
+  c->du_min = -50;            // runMPC.m:38
+  c->du_max = 50;             // runMPC.m:39
+  c->v_min = 3.4;             // runMPC.m:40 (not enforced by constraintsMPC.m)
+  c->v_max = 4.1;             // runMPC.m:41
+  c->phise_min = 0.08;        // runMPC.m:42
+  c->z_max = 95.0 / 100;      // runMPC.m:43
+  c->z_tol = 0 * 5.0 / 100;   // runMPC.m:44
+  c->use_current = c->use_voltage = c->use_eta = 1;  // runMPC.m:33
+  c->max_hild = 100;          // initMPC.m:47
+  c->hild_tol = 1e-6;         // hildreth.m:39
+  c->SigmaV = 1e-3;           // runMPC.m:19
+  c->SigmaW = 1e2;            // runMPC.m:18
+  for (int i = 0; i < 5; ++i) c->SigmaX0[i] = 1;
+  c->SigmaX0[5] = 2e6;        // runMPC.m:17
+  c->max_warn = 10;           // iterEKF.m:55
+  c->flags = 0;
+}
+
+// ---------------------------------------------------------------------------
+// ROM validation and packing
+// ---------------------------------------------------------------------------
+static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
+  if (!R || !R->T_degC || !R->SOC_pct || !R->A || !R->C || !R->D || !R->tf_code || !R->tf_xloc)
+    return fail(MPCEKF_E_ARG, "rom: null array");
+  if (R->n != NX) return fail(MPCEKF_E_UNSUPPORTED, "rom: n = %d transient states, kernels are built for 5", R->n);
+  if (R->nT < 1 || R->nT > MAXT || R->nZ < 1 || R->nZ > MAXZ)
+    return fail(MPCEKF_E_UNSUPPORTED, "rom: grid %dx%d exceeds %dx%d", R->nT, R->nZ, MAXT, MAXZ);
+  if (R->nz < NROLE || R->nz > MAXROWS) return fail(MPCEKF_E_UNSUPPORTED, "rom: nz = %d outside [11, 64]", R->nz);
+  if (R->neg.ntab < 2 || R->neg.ntab != R->pos.ntab || !R->neg.U || !R->pos.U || !R->neg.dU || !R->pos.dU ||
+      !R->neg.dUdT || !R->pos.dUdT)
+    return fail(MPCEKF_E_ROM, "rom: OCP tables missing or of different lengths");
+  for (int i = 1; i < R->nT; ++i)
+    if (!(R->T_degC[i] > R->T_degC[i - 1])) return fail(MPCEKF_E_ROM, "rom: T set-points not ascending");
+  for (int i = 1; i < R->nZ; ++i)
+    if (!(R->SOC_pct[i] > R->SOC_pct[i - 1])) return fail(MPCEKF_E_ROM, "rom: SOC set-points not ascending");
+  const int nT = R->nT, nZ = R->nZ, NM = nT * nZ, nz = R->nz, n1 = NX + 1;
+  for (int m = 0; m < NM; ++m)
+    if (R->A[(size_t)m * n1 + NX] != 1.0) return fail(MPCEKF_E_ROM, "A for model %d has no integrator state (initKF.m:74)", m);
+  for (int q = 0; q < nz; ++q)
+    if (R->tf_code[q] < 0 || R->tf_code[q] >= MPCEKF_TF_COUNT) return fail(MPCEKF_E_ROM, "rom: bad tf code at row %d", q);
+
+  // --- index resolution (iterEKF.m:610-735) ---
+  auto rows_of = [&](int code) {
+    std::vector<int> v;
+    for (int q = 0; q < nz; ++q)
+      if (R->tf_code[q] == code) v.push_back(q);
+    return v;
+  };
+  auto cat = [](std::vector<int> a, const std::vector<int> &b) {
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+  };
+  const double *loc = R->tf_xloc;
+  auto at = [&](const std::vector<int> &v, double x) {
+    std::vector<int> o;
+    for (int q : v)
+      if (loc[q] == x) o.push_back(q);
+    return o;
+  };
+  std::vector<int> Ifdl = cat(rows_of(MPCEKF_TF_negIfdl), rows_of(MPCEKF_TF_posIfdl));
+  std::vector<int> If = cat(rows_of(MPCEKF_TF_negIf), rows_of(MPCEKF_TF_posIf));
+  std::vector<int> Thss = cat(rows_of(MPCEKF_TF_negThetass), rows_of(MPCEKF_TF_posThetass));
+  std::vector<int> Phise = cat(rows_of(MPCEKF_TF_negPhise), rows_of(MPCEKF_TF_posPhise));
+  std::vector<int> Phie = cat(cat(rows_of(MPCEKF_TF_negPhie), rows_of(MPCEKF_TF_sepPhie)), rows_of(MPCEKF_TF_posPhie));
+  std::vector<int> Thetae =
+      cat(cat(rows_of(MPCEKF_TF_negThetae), rows_of(MPCEKF_TF_sepThetae)), rows_of(MPCEKF_TF_posThetae));
+  struct {
+    const char *name;
+    std::vector<int> v;
+  } singles[] = {{"ifdl at negative-collector", at(Ifdl, 0)}, {"ifdl at positive-collector", at(Ifdl, 3)},
+                 {"if at negative-collector", at(If, 0)},     {"if at positive-collector", at(If, 3)},
+                 {"thetass at negative-collector", at(Thss, 0)}, {"thetass at positive-collector", at(Thss, 3)},
+                 {"phise at negative-collector", at(Phise, 0)}};
+  for (auto &s : singles)
+    if (s.v.size() != 1) return fail(MPCEKF_E_ROM, "Simulation requires exactly one %s (iterEKF.m:692-725)", s.name);
+  const double eps = 2.220446049250313e-16;
+  if (Thetae.empty() || loc[Thetae.front()] > 0) return fail(MPCEKF_E_ROM, "Simulation requires thetae at negative-collector!");
+  if (loc[Thetae.back()] > 3 + eps || loc[Thetae.back()] < 3 - eps)
+    return fail(MPCEKF_E_ROM, "Simulation requires thetae at positive-collector!");
+  if (!Phie.empty() && loc[Phie.front()] == 0) Phie.erase(Phie.begin());  // iterEKF.m:728-731
+  if (Phie.empty() || loc[Phie.back()] > 3 + eps || loc[Phie.back()] < 3 - eps)
+    return fail(MPCEKF_E_ROM, "Simulation requires phie at positive-collector!");
+  std::vector<int> negPhise = rows_of(MPCEKF_TF_negPhise);
+  if (negPhise.size() < 2) return fail(MPCEKF_E_ROM, "EKFmatsHandler.m:97 needs ind.negPhise(2)");
+  // OB_step's own lookups (OB_step.m:131-137) must agree
+  auto negat = [&](int code, double x) { return at(rows_of(code), x); };
+  if (negat(MPCEKF_TF_negIfdl, 0) != singles[0].v || negat(MPCEKF_TF_posIfdl, 3) != singles[1].v ||
+      negat(MPCEKF_TF_negIf, 0) != singles[2].v || negat(MPCEKF_TF_posIf, 3) != singles[3].v ||
+      negat(MPCEKF_TF_negThetass, 0) != singles[4].v || negat(MPCEKF_TF_posThetass, 3) != singles[5].v)
+    return fail(MPCEKF_E_ROM, "OB_step and iterEKF resolve collector rows differently");
+  int role[NROLE];
+  role[R_IFDL0] = singles[0].v[0];
+  role[R_IFDL3] = singles[1].v[0];
+  role[R_IF0] = singles[2].v[0];
+  role[R_IF3] = singles[3].v[0];
+  role[R_TH0] = singles[4].v[0];
+  role[R_TH3] = singles[5].v[0];
+  role[R_TE1] = Thetae.front();
+  role[R_TEE] = Thetae.back();
+  role[R_PHIE] = Phie.back();
+  role[R_PHISE0] = singles[6].v[0];
+  role[R_NPHISE2] = negPhise[1];
+  for (int a = 0; a < NROLE; ++a)
+    for (int b = a + 1; b < NROLE; ++b)
+      if (role[a] == role[b]) return fail(MPCEKF_E_UNSUPPORTED, "rom: role rows %d and %d coincide", a, b);
+  std::vector<int> perm(role, role + NROLE);
+  for (int q = 0; q < nz; ++q)
+    if (std::find(perm.begin(), perm.end(), q) == perm.end()) perm.push_back(q);
+  int nzp = 0;
+  for (int cand : {26, 32})
+    if (nz <= cand && cell_kernel_supported(cand)) { nzp = cand; break; }
+  if (!nzp) return fail(MPCEKF_E_UNSUPPORTED, "rom: nz = %d not built (kernels: 26, 32)", nz);
+
+  unsigned char flags[MAXROWS] = {0}, c0k[MAXROWS] = {0};
+  std::vector<unsigned> fl(nz, 0u);
+  std::vector<int> c0(nz, C0_ZERO);
+  for (int q : rows_of(MPCEKF_TF_negThetass)) fl[q] |= G_NTH;
+  for (int q : rows_of(MPCEKF_TF_posThetass)) fl[q] |= G_PTH;
+  for (int q : rows_of(MPCEKF_TF_negPhise)) fl[q] |= G_NPHISE;
+  for (int q : rows_of(MPCEKF_TF_posPhise)) fl[q] |= G_PPHISE;
+  for (int q : Phie) fl[q] |= G_PHIE | (loc[q] == 0 ? G_PHIE0 : 0u);
+  for (int q : Thetae) fl[q] |= G_THETAE;
+  for (int q : rows_of(MPCEKF_TF_posPhis)) fl[q] |= G_PPHIS;
+  for (int q : rows_of(MPCEKF_TF_posPhis)) c0[q] = C0_CHATV0;  // iterEKF.m:553-586 order
+  for (int q : rows_of(MPCEKF_TF_negThetass)) c0[q] = C0_RES0N;
+  for (int q : rows_of(MPCEKF_TF_posThetass)) c0[q] = C0_RES0P;
+  for (int q : rows_of(MPCEKF_TF_negPhise)) c0[q] = C0_DUN;
+  for (int q : rows_of(MPCEKF_TF_posPhise)) c0[q] = C0_DUP;
+  for (int q : Phie) c0[q] = C0_MDUN;
+  KRom &r = X->r;
+  std::memset(&r, 0, sizeof(r));
+  for (int q = 0; q < nz; ++q) {
+    flags[q] = (unsigned char)fl[perm[q]];
+    c0k[q] = (unsigned char)c0[perm[q]];
+    r.perm[q] = (short)perm[q];
+  }
+  std::memcpy(r.flags, flags, sizeof flags);
+  std::memcpy(r.c0k, c0k, sizeof c0k);
+  r.NM = NM; r.nT = nT; r.nZ = nZ; r.nz = nz; r.nzp = nzp; r.ntab = R->neg.ntab;
+  r.Ts = R->Ts; r.Q = R->Q; r.F = R->F; r.R = R->R; r.Rc = R->Rc; r.Tref = R->Tref;
+  r.th0n = R->neg.theta0; r.th100n = R->neg.theta100; r.th0p = R->pos.theta0; r.th100p = R->pos.theta100;
+  r.Rfn = R->neg.Rf; r.Rfp = R->pos.Rf;
+
+  // --- blobs ---
+  const int nt = r.ntab;
+  std::vector<double> tabs;
+  for (const mpcekf_electrode *e : {&R->neg, &R->pos}) {
+    tabs.insert(tabs.end(), e->U, e->U + nt);
+    tabs.insert(tabs.end(), e->dUdT, e->dUdT + nt);
+    tabs.insert(tabs.end(), e->dU, e->dU + nt);
+  }
+  std::vector<double> pts(MAXT + MAXZ, 0.0);
+  for (int t = 0; t < nT; ++t) pts[t] = R->T_degC[t] + 273.15;  // ROMmdls(t,z).T (initKF.m:58)
+  for (int z = 0; z < nZ; ++z) pts[MAXT + z] = R->SOC_pct[z] / 100;  // ROMmdls(t,z).SOC
+  auto Cval = [&](int m, int q, int k) { return R->C[((size_t)m * nz + q) * n1 + k]; };
+  auto Dval = [&](int m, int q) { return R->D[(size_t)m * nz + q]; };
+  // cell blob: per model [C nzp x 5][D nzp][a 5]
+  r.cell_stride = nzp * NX + nzp + NX;
+  std::vector<double> cb((size_t)NM * r.cell_stride, 0.0);
+  for (int m = 0; m < NM; ++m) {
+    double *b = cb.data() + (size_t)m * r.cell_stride;
+    for (int q = 0; q < nz; ++q) {
+      for (int k = 0; k < NX; ++k) b[q * NX + k] = Cval(m, perm[q], k);  // initKF.m:91 strips res0
+      b[nzp * NX + q] = Dval(m, perm[q]);
+    }
+    for (int k = 0; k < NX; ++k) b[nzp * NX + nzp + k] = R->A[(size_t)m * n1 + k];
+  }
+  r.cell_tab = (int)cb.size();
+  cb.insert(cb.end(), tabs.begin(), tabs.end());
+  cb.insert(cb.end(), pts.begin(), pts.end());
+  r.cell_len = (int)cb.size();
+  // plant blob: per model [C 9 x 5][res0 9][D 9] over role rows 0..8
+  std::vector<double> pb((size_t)NM * PREC, 0.0);
+  for (int m = 0; m < NM; ++m) {
+    double *b = pb.data() + (size_t)m * PREC;
+    for (int q = 0; q < NPLANT; ++q) {
+      for (int k = 0; k < NX; ++k) b[q * NX + k] = Cval(m, perm[q], k);
+      b[NPLANT * NX + q] = Cval(m, perm[q], NX);  // res0 column (Phise rows are not among these)
+      b[NPLANT * NX + NPLANT + q] = Dval(m, perm[q]);
+    }
+  }
+  r.plant_tab = (int)pb.size();
+  pb.insert(pb.end(), tabs.begin(), tabs.end());
+  pb.insert(pb.end(), pts.begin(), pts.end());
+  r.plant_len = (int)pb.size();
+  // bulk tables: cA/cB per EKF record element, cP per plant state
+  std::vector<double> bt((size_t)NM * (2 * REC + 6));
+  double *cA = bt.data(), *cB = cA + (size_t)NM * REC, *cP = cB + (size_t)NM * REC;
+  int pr[NPK], pc[NPK];
+  for (int p = 0, i = 0; p < NX; ++p)
+    for (int q = p; q < NX; ++q, ++i) { pr[i] = p; pc[i] = q; }
+  for (int m = 0; m < NM; ++m) {
+    const double *a = R->A + (size_t)m * n1;
+    for (int e = 0; e < NX; ++e) { cA[m * REC + e] = a[e]; cB[m * REC + e] = 1.0; }
+    for (int i = 0; i < NPK; ++i) { cA[m * REC + NX + i] = a[pr[i]]; cB[m * REC + NX + i] = a[pc[i]]; }
+    for (int e = 0; e < 6; ++e) cP[m * 6 + e] = a[e];
+  }
+  if (cell_lds_bytes(r) > 160 * 1024)
+    return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of ROM tables exceed the 160 KiB LDS", cell_lds_bytes(r));
+  int rc;
+  if ((rc = dalloc(&X->d_cell_blob, cb.size()))) return rc;
+  if ((rc = dalloc(&X->d_plant_blob, pb.size()))) return rc;
+  if ((rc = dalloc(&X->d_bulk, bt.size()))) return rc;
+  HIPCHK(hipMemcpy(X->d_cell_blob, cb.data(), cb.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(X->d_plant_blob, pb.data(), pb.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(X->d_bulk, bt.data(), bt.size() * 8, hipMemcpyHostToDevice));
+  r.cell_blob = X->d_cell_blob;
+  r.plant_blob = X->d_plant_blob;
+  r.bulk_tab = X->d_bulk;
+  X->NM = NM;
+  X->nz = nz;
+  X->nzp = nzp;
+  return MPCEKF_OK;
+}
+
+static int check_cfg(const mpcekf_config *c) {
+  if (c->Np != 5 || c->Nc != 2)
+    return fail(MPCEKF_E_UNSUPPORTED, "Np=%d Nc=%d: this build compiles the GPU step for Np=5, Nc=2", c->Np, c->Nc);
+  if (!c->use_current || !c->use_voltage || !c->use_eta)
+    return fail(MPCEKF_E_UNSUPPORTED, "constraint switches must all be on (runMPC.m:33) in this build");
+  if (c->max_hild < 1) return fail(MPCEKF_E_ARG, "max_hild < 1");
+  return MPCEKF_OK;
+}
+
+static void fill_kcfg(const mpcekf_config *c, double Q, KCfg &k) {
+  k.SigmaV = c->SigmaV;
+  k.SigmaW = c->SigmaW;
+  k.ref = c->target_soc;
+  k.u_max = c->u_max;
+  k.u_min = -Q * c->Crate;  // initMPC.m:66-67
+  k.du_min = c->du_min;
+  k.du_max = c->du_max;
+  k.v_max = c->v_max;
+  k.phise_min = c->phise_min;
+  k.zmax = c->z_max + c->z_tol;  // constraintsMPC.m:90-91
+  k.hild_tol = c->hild_tol;
+  k.max_warn = c->max_warn;
+  k.max_hild = c->max_hild;
+  k.flags = c->flags;
+}
+
+int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int device, int64_t ncells,
+                      mpcekf_ctx **out) {
+  if (!out || !cfg || ncells < 0) return fail(MPCEKF_E_ARG, "ctx_create: bad argument");
+  *out = nullptr;
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MPCEKF_E_ARG, "device %d of %d", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  mpcekf_ctx *X = new (std::nothrow) mpcekf_ctx();
+  if (!X) return fail(MPCEKF_E_ARG, "out of host memory");
+  X->device = device;
+  X->n = ncells;
+  X->cfg = *cfg;
+  X->ncon = NCON_BUILT;
+  if ((rc = build_rom(X, rom))) { mpcekf_ctx_destroy(X); return rc; }
+  fill_kcfg(cfg, rom->Q, X->k);
+  X->Tref = rom->Tref;
+  X->Rgas = rom->R;
+  const mpcekf_electrode *el[2] = {&rom->neg, &rom->pos};
+  for (int i = 0; i < 2; ++i) {
+    X->th0[i] = el[i]->theta0; X->th100[i] = el[i]->theta100; X->k0ref[i] = el[i]->k0ref; X->Ea[i] = el[i]->Ea_k0;
+    X->Cdl[i] = el[i]->Cdl; X->wDL[i] = el[i]->wDL; X->nDL[i] = el[i]->nDL;
+  }
+  hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
+  const size_t n = (size_t)ncells, NM = (size_t)X->NM;
+  KState &s = X->s;
+  s.n = ncells;
+  if ((rc = dalloc(&s.bigx, n * NM * 6)) || (rc = dalloc(&s.ekf, n * NM * REC)) ||
+      (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
+      (rc = dalloc(&X->d_int, n * 3)) || (rc = dalloc(&X->d_const, n * 8)) ||
+      (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2)))) {
+    mpcekf_ctx_destroy(X);
+    return rc;
+  }
+  double *sc = X->d_scal;
+  s.SOCn = sc; s.SOCp = sc + n; s.x0 = sc + 2 * n; s.S0 = sc + 3 * n; s.priorI = sc + 4 * n;
+  s.uk_1 = sc + 5 * n; s.uk = sc + 6 * n; s.vk = sc + 7 * n; s.J_unc = sc + 8 * n; s.J_fin = sc + 9 * n;
+  s.warn = X->d_int; s.status = X->d_int + n; s.nviol = X->d_int + 2 * n;
+  double *cs = X->d_const;
+  s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
+  s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
+  *out = X;
+  return MPCEKF_OK;
+}
+
+int mpcekf_ctx_destroy(mpcekf_ctx *X) {
+  if (!X) return MPCEKF_OK;
+  (void)hipSetDevice(X->device);
+  if (X->stream) (void)hipStreamSynchronize(X->stream);
+  for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
+  void *ptrs[] = {X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam};
+  for (void *p : ptrs)
+    if (p) (void)hipFree(p);
+  if (X->stream) (void)hipStreamDestroy(X->stream);
+  delete X;
+  return MPCEKF_OK;
+}
+
+int mpcekf_ctx_info(const mpcekf_ctx *X, int64_t *ncells, int32_t *nmodels, int32_t *nz, int32_t *ncon) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  if (ncells) *ncells = X->n;
+  if (nmodels) *nmodels = X->NM;
+  if (nz) *nz = X->nz;
+  if (ncon) *ncon = X->ncon;
+  return MPCEKF_OK;
+}
+
+// initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.  The
+// T-only cellData functions are evaluated here once per cell with the host libm
+// (bit-identical to evaluating them at every call, since Tc is constant).
+int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_degC) {
+  if (!X || ((!soc0_pct || !tc_degC) && X->n)) return fail(MPCEKF_E_ARG, "init_cells: null argument");
+  HIPCHK(hipSetDevice(X->device));
+  const size_t n = (size_t)X->n;
+  std::vector<double> cst(n * 8), sc(n * 10, 0.0);
+  for (size_t c = 0; c < n; ++c) {
+    double tc = tc_degC[c], soc0 = soc0_pct[c];
+    if (!(tc <= 100)) return fail(MPCEKF_E_ARG, "cell %zu: Tc = %g; Tc must be in degC (iterEKF.m:62)", c, tc);
+    double T = tc + 273.15;  // OB_step.m:63,75
+    double z = soc0 / 100;
+    cst[0 * n + c] = tc;
+    cst[1 * n + c] = z;                                          // ekfData.SOC0 (initKF.m:133)
+    cst[2 * n + c] = X->th0[0] + z * (X->th100[0] - X->th0[0]);  // SOC0n (OB_step.m:64)
+    cst[3 * n + c] = X->th0[1] + z * (X->th100[1] - X->th0[1]);  // SOC0p
+    for (int e = 0; e < 2; ++e) {
+      cst[(4 + e) * n + c] = X->k0ref[e] * std::exp(X->Ea[e] / X->Rgas * (1.0 / X->Tref - 1.0 / T));
+      cst[(6 + e) * n + c] = std::pow(X->Cdl[e], 2 - X->nDL[e]) * std::pow(X->wDL[e], X->nDL[e] - 1);  // OB_step.m:218
+    }
+    sc[0 * n + c] = cst[2 * n + c];  // SOCnAvg
+    sc[1 * n + c] = cst[3 * n + c];  // SOCpAvg
+    sc[3 * n + c] = X->cfg.SigmaX0[5];  // ekfData.SigmaX0 (initKF.m:99)
+  }
+  HIPCHK(hipMemcpyAsync(X->d_const, cst.data(), cst.size() * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemsetAsync(X->s.lam, 0, n * X->ncon * 8, X->stream));
+  HIPCHK(hipMemsetAsync(X->d_int, 0, n * 3 * sizeof(int), X->stream));
+  int rc = launch_init_state(X->n, X->NM, X->s.ekf, X->s.bigx, X->cfg.SigmaX0, X->stream);
+  if (rc) return fail(MPCEKF_E_HIP, "init kernel: %s", hipGetErrorString((hipError_t)rc));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  X->initialized = true;
+  return MPCEKF_OK;
+}
+
+static int need_init(mpcekf_ctx *X) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  if (!X->initialized) return fail(MPCEKF_E_STATE, "call mpcekf_init_cells first");
+  HIPCHK(hipSetDevice(X->device));
+  return MPCEKF_OK;
+}
+
+static int lerr(int rc, const char *what) {
+  if (rc) return fail(MPCEKF_E_HIP, "%s launch: %s", what, hipGetErrorString((hipError_t)rc));
+  return MPCEKF_OK;
+}
+
+// runMPC.m:84-111, nsteps times: OB_step -> (all-model advance + EKF time
+// update) -> iterEKF measurement update -> EKFmatsHandler -> iterMPC.
+int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
+                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (nsteps < 0) return fail(MPCEKF_E_ARG, "nsteps < 0");
+  const size_t n = (size_t)X->n, per = n * (size_t)nsteps;
+  double *outs[4] = {traj_u, traj_v, traj_soc, traj_phise};
+  double *dev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int *dnex = nullptr;
+  if (outputs_on_device) {
+    for (int i = 0; i < 4; ++i) dev[i] = outs[i];
+    dnex = traj_nexec;
+  } else {
+    size_t need = 0;
+    for (int i = 0; i < 4; ++i) need += outs[i] ? per * 8 : 0;
+    need += traj_nexec ? per * 4 + 16 : 0;
+    if ((rc = X->tmp(need))) return rc;
+    char *p = (char *)X->d_tmp;
+    for (int i = 0; i < 4; ++i)
+      if (outs[i]) { dev[i] = (double *)p; p += per * 8; }
+    if (traj_nexec) dnex = (int *)p;
+  }
+  const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
+  if (X->timing && X->ev.size() < (size_t)nsteps * 4) {
+    size_t old = X->ev.size();
+    X->ev.resize((size_t)nsteps * 4);
+    for (size_t i = old; i < X->ev.size(); ++i) HIPCHK(hipEventCreate(&X->ev[i]));
+  }
+  for (int k = 0; k < nsteps; ++k) {
+    const size_t o = (size_t)k * n;
+    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * 4] : nullptr;
+    if (E) HIPCHK(hipEventRecord(E[0], X->stream));
+    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, X->stream), "plant"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[1], X->stream));
+    if ((rc = lerr(launch_bulk(X->r, X->k, X->s, X->s.uk, 1, 1, X->stream), "bulk"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[2], X->stream));
+    KIO io{};
+    io.mode = MODE_FUSED;
+    io.u = dev[0] ? dev[0] + o : nullptr;
+    io.v = dev[1] ? dev[1] + o : nullptr;
+    io.soc = dev[2] ? dev[2] + o : nullptr;
+    io.phise = dev[3] ? dev[3] + o : nullptr;
+    io.nexec = dnex ? dnex + o : nullptr;
+    io.zk = X->d_zk;
+    io.zbk = bounds ? X->d_zbk : nullptr;
+    if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+  }
+  if (!outputs_on_device) {
+    for (int i = 0; i < 4; ++i)
+      if (outs[i]) HIPCHK(hipMemcpyAsync(outs[i], dev[i], per * 8, hipMemcpyDeviceToHost, X->stream));
+    if (traj_nexec) HIPCHK(hipMemcpyAsync(traj_nexec, dnex, per * 4, hipMemcpyDeviceToHost, X->stream));
+  }
+  HIPCHK(hipStreamSynchronize(X->stream));
+  if (X->timing)
+    for (int k = 0; k < nsteps; ++k)
+      for (int j = 0; j < 3; ++j) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * 4 + j], X->ev[(size_t)k * 4 + j + 1]));
+        X->t_ms[j] += ms;
+        X->t_n[j] += 1;
+      }
+  return MPCEKF_OK;
+}
+
+int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  X->timing = enable != 0;
+  return MPCEKF_OK;
+}
+
+int mpcekf_get_timing(mpcekf_ctx *X, double *ms_sum, int64_t *launches) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  for (int j = 0; j < 3; ++j) {
+    if (ms_sum) ms_sum[j] = X->t_ms[j];
+    if (launches) launches[j] = X->t_n[j];
+    X->t_ms[j] = 0;
+    X->t_n[j] = 0;
+  }
+  return MPCEKF_OK;
+}
+
+int mpcekf_get_zk(mpcekf_ctx *X, double *zk, double *boundzk) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  size_t bytes = (size_t)X->n * (X->nz + 2) * 8;
+  if (zk) HIPCHK(hipMemcpyAsync(zk, X->d_zk, bytes, hipMemcpyDeviceToHost, X->stream));
+  if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, X->d_zbk, bytes, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+// ---- stage entry points ----------------------------------------------------
+}  // extern "C"
+// Host arrays are staged through one device scratch slab.
+struct Slab {
+  char *base;
+  size_t off = 0;
+  template <class T>
+  T *take(size_t count) {
+    T *p = (T *)(base + off);
+    off += (count * sizeof(T) + 255) & ~(size_t)255;
+    return p;
+  }
+};
+extern "C" {
+
+int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, double *vcell) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!iapp || !vcell) return fail(MPCEKF_E_ARG, "plant_step: null argument");
+  size_t n = (size_t)X->n;
+  if ((rc = X->tmp(2 * n * 8 + 512))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *di = sl.take<double>(n), *dv = sl.take<double>(n);
+  HIPCHK(hipMemcpyAsync(di, iapp, n * 8, hipMemcpyHostToDevice, X->stream));
+  if ((rc = lerr(launch_plant(X->r, X->s, di, dv, X->stream), "plant"))) return rc;
+  if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
+  HIPCHK(hipMemcpyAsync(vcell, dv, n * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, double *zk, double *boundzk,
+                    int32_t *xind_model, double *xind_gamma) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!vk || !ik || !zk || !xind_model || !xind_gamma) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
+  size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
+  if ((rc = X->tmp((2 * n + 2 * n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dvk = sl.take<double>(n), *dik = sl.take<double>(n), *dzk = sl.take<double>(n * nzz);
+  double *dzb = sl.take<double>(n * nzz), *dxg = sl.take<double>(4 * n);
+  int *dxm = sl.take<int>(4 * n);
+  HIPCHK(hipMemcpyAsync(dvk, vk, n * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(dik, ik, n * 8, hipMemcpyHostToDevice, X->stream));
+  // iterEKF.m:55 lock-out must see the state before the time update: the bulk
+  // update of a locked-out cell is harmless because the cell is stopped.
+  if ((rc = lerr(launch_bulk(X->r, X->k, X->s, nullptr, 0, 1, X->stream), "bulk"))) return rc;
+  KIO io{};
+  io.mode = MODE_EKF;
+  io.vk_in = dvk;
+  io.ik_in = dik;
+  io.zk = dzk;
+  io.zbk = boundzk ? dzb : nullptr;
+  io.xm_out = dxm;
+  io.xg_out = dxg;
+  if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+  HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
+  if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(xind_gamma, dxg, 4 * n * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                     double *lin) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!zk || !xind_model || !xind_gamma || !lin) return fail(MPCEKF_E_ARG, "linearize: null argument");
+  size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
+  if ((rc = X->tmp((n * nzz + 4 * n + n * MPCEKF_LIN_SIZE) * 8 + 4 * n * 4 + 2048))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dzk = sl.take<double>(n * nzz), *dxg = sl.take<double>(4 * n), *dl = sl.take<double>(n * MPCEKF_LIN_SIZE);
+  int *dxm = sl.take<int>(4 * n);
+  HIPCHK(hipMemcpyAsync(dzk, zk, n * nzz * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(dxm, xind_model, 4 * n * 4, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(dxg, xind_gamma, 4 * n * 8, hipMemcpyHostToDevice, X->stream));
+  KIO io{};
+  io.mode = MODE_LIN;
+  io.zk_in = dzk;
+  io.xm_in = dxm;
+  io.xg_in = dxg;
+  io.lin_out = dl;
+  if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+  HIPCHK(hipMemcpyAsync(lin, dl, n * MPCEKF_LIN_SIZE * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!lin || !soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
+  size_t n = (size_t)X->n;
+  if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + 2 * n) * 8 + n * 4 + 2048))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *ds = sl.take<double>(n), *du = sl.take<double>(n);
+  int *dn = sl.take<int>(n);
+  HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, X->stream));
+  KIO io{};
+  io.mode = MODE_MPC;
+  io.lin_in = dl;
+  io.soc_k1_in = ds;
+  io.uk_out = du;
+  io.nexec = dn;
+  if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+  HIPCHK(hipMemcpyAsync(uk, du, n * 8, hipMemcpyDeviceToHost, X->stream));
+  if (nexec) HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+// ---- context-free kernels ----------------------------------------------------
+}  // extern "C"
+namespace {
+struct DevScope {
+  hipStream_t st = nullptr;
+  char *buf = nullptr;
+  ~DevScope() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (buf) (void)hipFree(buf);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+}  // namespace
+extern "C" {
+
+int mpcekf_predmat(int device, int64_t n, int32_t Np, int32_t Nc, const double *a, const double *C, const double *D,
+                   double *Phi, double *G) {
+  if (n < 0 || (n && (!a || !C || !D || !Phi || !G))) return fail(MPCEKF_E_ARG, "predmat: bad argument");
+  if (Np != 5 || Nc != 2) return fail(MPCEKF_E_UNSUPPORTED, "predmat: built for Np=5, Nc=2");
+  if (n == 0) return MPCEKF_OK;
+  HIPCHK(hipSetDevice(device));
+  DevScope d;
+  HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
+  size_t b_in = (size_t)n * 13 * 8, b_out = (size_t)n * (Np * 7 + Np * Nc) * 8;
+  HIPCHK(hipMalloc((void **)&d.buf, b_in + b_out + 1024));
+  double *da = (double *)d.buf, *dC = da + n * 6, *dD = dC + n * 6, *dP = dD + n, *dG = dP + n * Np * 7;
+  HIPCHK(hipMemcpyAsync(da, a, n * 6 * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dC, C, n * 6 * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dD, D, n * 8, hipMemcpyHostToDevice, d.st));
+  int rc = lerr(launch_predmat(n, Np, Nc, da, dC, dD, dP, dG, d.st), "predmat");
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(Phi, dP, n * Np * 7 * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(G, dG, n * Np * Nc * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipStreamSynchronize(d.st));
+  return MPCEKF_OK;
+}
+
+int mpcekf_constraints(int device, const mpcekf_config *cfg, double Q, int64_t n, const double *lin,
+                       const double *uk_1, const double *soc_k1, double *M, double *gamma) {
+  if (!cfg || n < 0 || (n && (!lin || !uk_1 || !soc_k1 || !M || !gamma)))
+    return fail(MPCEKF_E_ARG, "constraints: bad argument");
+  int rc = check_cfg(cfg);
+  if (rc) return rc;
+  if (n == 0) return MPCEKF_OK;
+  KCfg k{};
+  fill_kcfg(cfg, Q, k);
+  HIPCHK(hipSetDevice(device));
+  DevScope d;
+  HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
+  const int ncon = NCON_BUILT;
+  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * (MPCEKF_LIN_SIZE + 2 + ncon * 2 + ncon) * 8 + 1024));
+  double *dl = (double *)d.buf, *du = dl + n * MPCEKF_LIN_SIZE, *ds = du + n, *dM = ds + n, *dg = dM + n * ncon * 2;
+  HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(du, uk_1, n * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, d.st));
+  if ((rc = lerr(launch_constraints(k, n, dl, du, ds, dM, dg, d.st), "constraints"))) return rc;
+  HIPCHK(hipMemcpyAsync(M, dM, n * ncon * 2 * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(gamma, dg, n * ncon * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipStreamSynchronize(d.st));
+  return MPCEKF_OK;
+}
+
+int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const double *E, const double *F,
+                    const double *M, const double *gamma, double *lambda, int32_t max_iter, double tol, double *DU,
+                    int32_t *nexec) {
+  if (n < 0 || (n && (!E || !F || !M || !gamma || !lambda || !DU || !nexec)))
+    return fail(MPCEKF_E_ARG, "hildreth: bad argument");
+  if (Nc != 2 || ncon != NCON_BUILT)
+    return fail(MPCEKF_E_UNSUPPORTED, "hildreth: built for Nc=2, %d constraints", NCON_BUILT);
+  if (max_iter < 1) return fail(MPCEKF_E_ARG, "hildreth: max_iter < 1");
+  if (n == 0) return MPCEKF_OK;
+  HIPCHK(hipSetDevice(device));
+  DevScope d;
+  HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
+  size_t per = (size_t)(Nc * Nc + Nc + ncon * Nc + ncon + ncon + Nc);
+  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * per * 8 + (size_t)n * 4 + 1024));
+  double *dE = (double *)d.buf, *dF = dE + n * Nc * Nc, *dM = dF + n * Nc, *dg = dM + n * ncon * Nc,
+         *dl = dg + n * ncon, *dD = dl + n * ncon;
+  int *dn = (int *)(dD + n * Nc);
+  HIPCHK(hipMemcpyAsync(dE, E, n * Nc * Nc * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dF, F, n * Nc * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dM, M, n * ncon * Nc * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dg, gamma, n * ncon * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dl, lambda, n * ncon * 8, hipMemcpyHostToDevice, d.st));
+  int rc = lerr(launch_hildreth(n, Nc, ncon, dE, dF, dM, dg, dl, max_iter, tol, dD, dn, d.st), "hildreth");
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(lambda, dl, n * ncon * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(DU, dD, n * Nc * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipStreamSynchronize(d.st));
+  return MPCEKF_OK;
+}
+
+// ---- state access ------------------------------------------------------------
+static const int kScalMap[MPCEKF_NSCAL] = {0, 1, 2, 3, 4, 5, 6, 7};  // MPCEKF_S_* -> d_scal slot
+
+int mpcekf_get_state(mpcekf_ctx *X, mpcekf_state *st) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!st) return fail(MPCEKF_E_ARG, "get_state: null");
+  const size_t n = (size_t)X->n, NM = (size_t)X->NM, nc = (size_t)X->ncon;
+  if (st->bigX) HIPCHK(hipMemcpyAsync(st->bigX, X->s.bigx, n * NM * 6 * 8, hipMemcpyDeviceToHost, X->stream));
+  if (st->ekf) HIPCHK(hipMemcpyAsync(st->ekf, X->s.ekf, n * NM * REC * 8, hipMemcpyDeviceToHost, X->stream));
+  std::vector<double> sc(n * 8), lam(n * nc);
+  std::vector<int> iv(n * 2);
+  HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(lam.data(), X->s.lam, n * nc * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  for (size_t c = 0; c < n; ++c) {
+    if (st->scal)
+      for (int k = 0; k < MPCEKF_NSCAL; ++k) st->scal[c * MPCEKF_NSCAL + k] = sc[kScalMap[k] * n + c];
+    if (st->lambda)
+      for (size_t i = 0; i < nc; ++i) st->lambda[c * nc + i] = lam[i * n + c];
+    if (st->warn) st->warn[c] = iv[c];
+    if (st->status) st->status[c] = iv[n + c];
+  }
+  return MPCEKF_OK;
+}
+
+int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!st) return fail(MPCEKF_E_ARG, "set_state: null");
+  const size_t n = (size_t)X->n, NM = (size_t)X->NM, nc = (size_t)X->ncon;
+  if (st->bigX) HIPCHK(hipMemcpyAsync(X->s.bigx, st->bigX, n * NM * 6 * 8, hipMemcpyHostToDevice, X->stream));
+  if (st->ekf) HIPCHK(hipMemcpyAsync(X->s.ekf, st->ekf, n * NM * REC * 8, hipMemcpyHostToDevice, X->stream));
+  std::vector<double> sc(n * 8), lam(n * nc);
+  std::vector<int> iv(n * 2);
+  HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(lam.data(), X->s.lam, n * nc * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  for (size_t c = 0; c < n; ++c) {
+    if (st->scal)
+      for (int k = 0; k < MPCEKF_NSCAL; ++k) sc[kScalMap[k] * n + c] = st->scal[c * MPCEKF_NSCAL + k];
+    if (st->lambda)
+      for (size_t i = 0; i < nc; ++i) lam[i * n + c] = st->lambda[c * nc + i];
+    if (st->warn) iv[c] = st->warn[c];
+    if (st->status) iv[n + c] = st->status[c];
+  }
+  HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), n * 8 * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(X->s.lam, lam.data(), n * nc * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipMemcpyAsync(X->d_int, iv.data(), n * 2 * 4, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+}  // extern "C"

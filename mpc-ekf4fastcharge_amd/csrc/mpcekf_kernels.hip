@@ -1,0 +1,1515 @@
+// mpcekf_kernels.hip -- gfx950 kernels of the batched MPC+EKF control step.
+//
+// Work mapping (DESIGN.md "Kernels"):
+//   k_plant  lane-per-cell   OB_step.m:188-357 minus the all-model advance
+//   k_bulk   block-streaming OB_step.m:278 (bigX = bigA.*bigX + Iapp) and the
+//                            all-model EKF time update iterEKF.m:73-84, over the
+//                            whole cell batch: the HBM-bound part
+//   k_cell   lane-per-cell   iterEKF.m:85-210 (4-corner measurement update),
+//                            EKFmatsHandler.m, predMat.m, constraintsMPC.m,
+//                            iterMPC.m and hildreth.m for one cell per lane
+// The ROM (C/D rows, diag(A), OCP tables) is staged once per workgroup in LDS.
+// Arithmetic follows the defined order of oracle/mpcekf_oracle.c (sequential
+// sums from +0.0, no contraction), so results match it bit-for-bit apart from
+// asinh (device libm vs glibc).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "mpcekf_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+namespace mk {
+
+constexpr int NP = 5;                  // compiled horizon (runMPC.m:28)
+constexpr int NC = 2;                  // compiled control horizon (runMPC.m:29)
+constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
+
+// Keep a value opaque to the optimiser (no code emitted).  Used to pin where a
+// value is materialised (bounding register live ranges) and to stop the
+// loop-invariant products of the Hildreth sweep from being hoisted into 529
+// live registers.
+__device__ __forceinline__ void launder(double &x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ int pk(int r, int c) {
+  // packed upper-triangular index, row-major over r <= c
+  return r <= c ? r * NX - (r * (r - 1)) / 2 + (c - r) : c * NX - (c * (c - 1)) / 2 + (r - c);
+}
+
+__device__ __forceinline__ double tabi(const double *t, int n, double x) {
+  if (x != x) return __builtin_nan("");
+  double xc = fmin(fmax(x, 0.0), 1.0);
+  double tt = xc * (double)(n - 1);
+  int i = (int)floor(tt);
+  if (i > n - 2) i = n - 2;
+  double f = tt - (double)i;
+  return t[i] + f * (t[i + 1] - t[i]);
+}
+// tables: [U_n, dUdT_n, dU_n, U_p, dUdT_p, dU_p], each ntab long
+__device__ __forceinline__ double uocp(const double *tb, int n, int side, double th, double dT) {
+  const double *b = tb + side * 3 * n;
+  return tabi(b, n, th) + dT * tabi(b + n, n, th);
+}
+__device__ __forceinline__ double duocp(const double *tb, int n, int side, double th) {
+  return tabi(tb + side * 3 * n + 2 * n, n, th);
+}
+
+__device__ __forceinline__ void two_nearest(const double *pts, int n, double x, int &i1, int &i2) {
+  int b1 = -1, b2 = -1;
+  double d1 = 0.0, d2 = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double d = fabs(x - pts[i]);
+    bool better1 = b1 < 0 || (d < d1) || (d1 != d1 && d == d);
+    if (better1) {
+      b2 = b1; d2 = d1; b1 = i; d1 = d;
+      continue;
+    }
+    bool better2 = b2 < 0 || (d < d2) || (d2 != d2 && d == d);
+    if (better2) { b2 = i; d2 = d; }
+  }
+  i1 = b1;
+  i2 = b2 < 0 ? b1 : b2;
+}
+
+struct XI {
+  double g[4];
+  int m[4];
+};
+
+// iterEKF.m:219-255
+__device__ __forceinline__ void get_xind(int nT, int nZ, const double *Tp, const double *Zp, double Tk, double SOC,
+                                         XI &xi) {
+  int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
+  if (nZ > 1) {
+    int a, b;
+    two_nearest(Zp, nZ, SOC, a, b);
+    iZu = a; iZl = b;
+    if (Zp[iZu] < Zp[iZl]) { iZu = b; iZl = a; }
+  }
+  if (nT > 1) {
+    int a, b;
+    two_nearest(Tp, nT, Tk, a, b);
+    iTu = a; iTl = b;
+    if (Tp[iTu] < Tp[iTl]) { iTu = b; iTl = a; }
+  }
+  double aZ = 0.0, aT = 0.0;
+  if (nZ > 1) aZ = (SOC - Zp[iZl]) / (Zp[iZu] - Zp[iZl]);
+  if (nT > 1) aT = (Tk - Tp[iTl]) / (Tp[iTu] - Tp[iTl]);
+  xi.g[0] = (1 - aT) * (1 - aZ);
+  xi.g[1] = (1 - aT) * aZ;
+  xi.g[2] = aT * (1 - aZ);
+  xi.g[3] = aT * aZ;
+  xi.m[0] = iTl * nZ + iZl;
+  xi.m[1] = iTl * nZ + iZu;
+  xi.m[2] = iTu * nZ + iZl;
+  xi.m[3] = iTu * nZ + iZu;
+}
+
+__device__ __forceinline__ void load_x(const double *rec, double x[NX]) {
+  const double2 *p = reinterpret_cast<const double2 *>(rec);
+  double2 a = p[0], b = p[1];
+  x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+  x[4] = rec[4];
+}
+__device__ __forceinline__ void load_rec(const double *rec, double x[NX], double S[NPK]) {
+  const double2 *p = reinterpret_cast<const double2 *>(rec);
+  double v[REC];
+#pragma unroll
+  for (int i = 0; i < REC / 2; ++i) {
+    double2 t = p[i];
+    v[2 * i] = t.x;
+    v[2 * i + 1] = t.y;
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) x[i] = v[i];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) S[i] = v[NX + i];
+}
+__device__ __forceinline__ void store_rec(double *rec, const double x[NX], const double S[NPK]) {
+  double2 *p = reinterpret_cast<double2 *>(rec);
+  double v[REC];
+#pragma unroll
+  for (int i = 0; i < NX; ++i) v[i] = x[i];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) v[NX + i] = S[i];
+#pragma unroll
+  for (int i = 0; i < REC / 2; ++i) p[i] = make_double2(v[2 * i], v[2 * i + 1]);
+}
+__device__ __forceinline__ void load_S(const double *rec, double S[NPK]) {
+  S[0] = rec[NX];
+  const double2 *p = reinterpret_cast<const double2 *>(rec + NX + 1);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    double2 t = p[i];
+    S[1 + 2 * i] = t.x;
+    S[2 + 2 * i] = t.y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cyclic Jacobi on a packed symmetric 5x5 (orc_jacobi), V row-major 5x5.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void jacobi5(double a[NPK], double V[NX * NX]) {
+#pragma unroll
+  for (int i = 0; i < NX * NX; ++i) V[i] = (i % (NX + 1)) == 0 ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    double off = 0.0, dg = 0.0;
+#pragma unroll
+    for (int p = 0; p < NX; ++p) {
+      dg = dg + a[pk(p, p)] * a[pk(p, p)];
+#pragma unroll
+      for (int q = p + 1; q < NX; ++q) off = off + a[pk(p, q)] * a[pk(p, q)];
+    }
+    if (!(off > 1e-36 * dg)) break;
+#pragma unroll
+    for (int p = 0; p < NX - 1; ++p) {
+#pragma unroll
+      for (int q = p + 1; q < NX; ++q) {
+        double apq = a[pk(p, q)];
+        if (apq != 0.0) {
+          double theta = (a[pk(q, q)] - a[pk(p, p)]) / (2.0 * apq);
+          double t;
+          if (fabs(theta) > 1e150) {
+            t = 0.5 / theta;
+          } else {
+            t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0) t = -t;
+          }
+          double c = 1.0 / sqrt(t * t + 1.0), s = t * c, tau = s / (1.0 + c);
+          a[pk(p, p)] = a[pk(p, p)] - t * apq;
+          a[pk(q, q)] = a[pk(q, q)] + t * apq;
+          a[pk(p, q)] = 0.0;
+#pragma unroll
+          for (int r = 0; r < NX; ++r) {
+            if (r == p || r == q) continue;
+            double g = a[pk(r, p)], h = a[pk(r, q)];
+            a[pk(r, p)] = g - s * (h + g * tau);
+            a[pk(r, q)] = h + s * (g - h * tau);
+          }
+#pragma unroll
+          for (int r = 0; r < NX; ++r) {
+            double g = V[r * NX + p], h = V[r * NX + q];
+            V[r * NX + p] = g - s * (h + g * tau);
+            V[r * NX + q] = h + s * (g - h * tau);
+          }
+        }
+      }
+    }
+  }
+}
+
+// iterEKF.m:137-153 on one corner record (orc_meas_cov + state update).
+// P = Sigma - (L*St)*L' is only ever used as P + P', so only that sum is kept.
+__device__ __forceinline__ void meas_update(double *rec, const double L[NX], double St, double res) {
+  double x[NX], S[NPK];
+  load_rec(rec, x, S);
+#pragma unroll
+  for (int k = 0; k < NX; ++k) x[k] = x[k] + L[k] * res;
+  double LS[NX];
+#pragma unroll
+  for (int r = 0; r < NX; ++r) LS[r] = L[r] * St;
+  double Ps[NPK], a[NPK];
+#pragma unroll
+  for (int r = 0; r < NX; ++r)
+#pragma unroll
+    for (int c = r; c < NX; ++c) {
+      double prc = S[pk(r, c)] - LS[r] * L[c];
+      double pcr = S[pk(r, c)] - LS[c] * L[r];
+      Ps[pk(r, c)] = prc + pcr;
+      a[pk(r, c)] = (prc + pcr) * 0.5;
+    }
+  double V[NX * NX];
+  jacobi5(a, V);
+  double w[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) w[k] = fabs(a[pk(k, k)]);
+  bool bump = res * res > 9 * St;
+#pragma unroll
+  for (int r = 0; r < NX; ++r)
+#pragma unroll
+    for (int c = r; c < NX; ++c) {
+      double hrc = 0.0, hcr = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) {
+        hrc = hrc + (V[r * NX + k] * w[k]) * V[c * NX + k];
+        hcr = hcr + (V[c * NX + k] * w[k]) * V[r * NX + k];
+      }
+      double v = ((Ps[pk(r, c)] + hrc) + hcr) / 4.0;
+      if (bump) v = v * 2.0;
+      S[pk(r, c)] = v;
+    }
+  store_rec(rec, x, S);
+}
+
+// ---------------------------------------------------------------------------
+// Per-lane context for one cell
+// ---------------------------------------------------------------------------
+struct CellCtx {
+  const double *L;   // LDS: model blob base
+  const double *tb;  // LDS: tables
+  const double *Tp, *Zp;  // LDS set-points
+  double *erec;      // this cell's EKF records in HBM
+  int ntab, stride;
+  double T, dT, k0n, k0p;
+};
+
+// getVariables (iterEKF.m:259-417).  Z is the permuted output vector.
+template <int NZ>
+__device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, const XI &xi, double ik, double x0,
+                                           double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc) {
+  double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+  double SOCnAvg = r.th0n + xSOC * (r.th100n - r.th0n);
+  double SOCpAvg = r.th0p + xSOC * (r.th100p - r.th0p);
+  if (SOCnAvg < 0) { warn++; SOCnAvg = 1e-6; }
+  if (SOCnAvg > 1) { warn++; SOCnAvg = 1 - 1e-6; }
+  if (SOCpAvg < 0) { warn++; SOCpAvg = 1e-6; }
+  if (SOCpAvg > 0.998) { warn++; SOCpAvg = 0.998; }
+#pragma unroll
+  for (int q = 0; q < NZ; ++q) Z[q] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double x[NX];
+    load_x(cc.erec + (size_t)xi.m[j] * REC, x);
+    const double *Cm = cc.L + xi.m[j] * cc.stride;
+    const double *Dm = Cm + NZ * NX;
+    double g = xi.g[j];
+#pragma unroll
+    for (int q = 0; q < NZ; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) acc = acc + Cm[q * NX + k] * x[k];
+      double zj = acc + Dm[q] * ik;
+      Z[q] = Z[q] + zj * g;
+      launder(Z[q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double If0 = Z[R_IF0], If3 = Z[R_IF3];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_NTH) { Z[q] = Z[q] + SOCnAvg; any |= Z[q] < 0; }
+  if (any) {
+    warn++;
+#pragma unroll
+    for (int q = 0; q < NZ; ++q)
+      if ((r.flags[q] & G_NTH) && Z[q] < 0) Z[q] = 1e-6;
+  }
+  any = false;
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_NTH) any |= Z[q] > 1;
+  if (any) {
+    warn++;
+#pragma unroll
+    for (int q = 0; q < NZ; ++q)
+      if ((r.flags[q] & G_NTH) && Z[q] > 1) Z[q] = 1 - 1e-6;
+  }
+  any = false;
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_PTH) { Z[q] = Z[q] + SOCpAvg; any |= Z[q] < 0; }
+  if (any) {
+    warn++;
+#pragma unroll
+    for (int q = 0; q < NZ; ++q)
+      if ((r.flags[q] & G_PTH) && Z[q] < 0) Z[q] = 1e-6;
+  }
+  any = false;
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_PTH) any |= Z[q] > 0.998;
+  if (any) {
+    warn++;
+#pragma unroll
+    for (int q = 0; q < NZ; ++q)
+      if ((r.flags[q] & G_PTH) && Z[q] > 0.998) Z[q] = 0.998;
+  }
+  double Un = uocp(cc.tb, cc.ntab, 0, SOCnAvg, cc.dT), Up = uocp(cc.tb, cc.ntab, 1, SOCpAvg, cc.dT);
+#pragma unroll
+  for (int q = 0; q < NZ; ++q) {
+    if (r.flags[q] & G_NPHISE) Z[q] = Z[q] + Un;
+    if (r.flags[q] & G_PPHISE) Z[q] = Z[q] + Up;
+  }
+  double PhieTilde3 = Z[R_PHIE];
+  double Phise0 = Z[R_PHISE0];
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_PHIE) {
+      if (r.flags[q] & G_PHIE0) Z[q] = 0 - Phise0;
+      else Z[q] = Z[q] - Phise0;
+    }
+  any = false;
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_THETAE) { Z[q] = Z[q] + 1; any |= Z[q] < 0; }
+  if (any) {  // iterEKF.m:384-389 would raise a MATLAB error
+    warn++;
+    st |= ST_ERROR | ST_THETAE_NEG;
+    return __builtin_nan("");
+  }
+  double i0n = cc.k0n * sqrt(Z[R_TE1] * (1 - Z[R_TH0]) * Z[R_TH0]);
+  double i0p = cc.k0p * sqrt(Z[R_TEE] * (1 - Z[R_TH3]) * Z[R_TH3]);
+  double negEta0 = 2 * r.R * cc.T / r.F * asinh(If0 / (2 * i0n));
+  double posEta3 = 2 * r.R * cc.T / r.F * asinh(If3 / (2 * i0p));
+  double Uocpn0 = uocp(cc.tb, cc.ntab, 0, Z[R_TH0], cc.dT), Uocpp3 = uocp(cc.tb, cc.ntab, 1, Z[R_TH3], cc.dT);
+  double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (r.Rfp * Z[R_IFDL3] - r.Rfn * Z[R_IFDL0]);
+#pragma unroll
+  for (int q = 0; q < NZ; ++q)
+    if (r.flags[q] & G_PPHIS) Z[q] = Z[q] + V;
+  Zsoc = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+  return V;
+}
+
+// getChatV (iterEKF.m:421-519): voltage Jacobian rows of the 4 corners.
+template <int NZ>
+__device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, const XI &xi, double zTE1, double zTH0,
+                                          double zTEE, double zTH3, double Chat[4][NX], double &Chat0) {
+  double i0n = cc.k0n * sqrt(zTE1 * (1 - zTH0) * zTH0);
+  double i0p = cc.k0p * sqrt(zTEE * (1 - zTH3) * zTH3);
+  double Rctn = r.R * cc.T / (r.F * i0n), Rctp = r.R * cc.T / (r.F * i0p);
+  double dUn0 = duocp(cc.tb, cc.ntab, 0, zTH0), dUp3 = duocp(cc.tb, cc.ntab, 1, zTH3);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double g = xi.g[j];
+    const double *Cm = cc.L + xi.m[j] * cc.stride;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      double v = r.Rfp * (g * Cm[R_IFDL3 * NX + k]) - r.Rfn * (g * Cm[R_IFDL0 * NX + k]);
+      v = v + Rctp * (g * Cm[R_IF3 * NX + k]) - Rctn * (g * Cm[R_IF0 * NX + k]);
+      v = v + g * Cm[R_PHIE * NX + k];
+      v = v + (dUp3 * (g * Cm[R_TH3 * NX + k]) - dUn0 * (g * Cm[R_TH0 * NX + k]));
+      Chat[j][k] = v;
+    }
+  }
+  double dn = (r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n));
+  double dp = (r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p));
+  double res0n = -dUn0 * r.Ts * dn / (3600 * r.Q);
+  double res0p = -dUp3 * r.Ts * dp / (3600 * r.Q);
+  Chat0 = res0p - res0n;
+}
+
+// ---------------------------------------------------------------------------
+// MPC pieces (compiled for NP x NC)
+// ---------------------------------------------------------------------------
+// predMat.m with A = diag(a), B = ones, evaluated on the structure of Abar:
+// identical nonzero arithmetic to the dense products of orc_predmat.
+__device__ __forceinline__ void predmat_s(const double a[6], const double Cb[7], double Phi[NP][NA], double H[NP]) {
+  double S[6], P[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; }
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc = acc + Cb[j] * S[j];
+    acc = acc + Cb[6] * 1.0;
+    H[k] = acc;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      S[j] = a[j] * S[j] + 1.0;
+      P[j] = a[j] * P[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) Phi[k][j] = 0.0 + Cb[j] * P[j];
+    double acc2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc2 = acc2 + Cb[j] * S[j];
+    acc2 = acc2 + Cb[6] * 1.0;
+    Phi[k][6] = acc2;
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void lu_solve_n(const double Ain[N][N], const double b[N], double x[N]) {
+  double A[N][N], y[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    y[i] = b[i];
+#pragma unroll
+    for (int j = 0; j < N; ++j) A[i][j] = Ain[i][j];
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    int p = k;
+#pragma unroll
+    for (int i = k + 1; i < N; ++i)
+      if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+    // row swap k <-> p with compile-time indices only
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      if (i == p) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) { double t = A[k][j]; A[k][j] = A[i][j]; A[i][j] = t; }
+        double t = y[k]; y[k] = y[i]; y[i] = t;
+      }
+    }
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      double l = A[i][k] / A[k][k];
+      A[i][k] = l;
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) A[i][j] = A[i][j] - l * A[k][j];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int k = 0; k < i; ++k) y[i] = y[i] - A[i][k] * y[k];
+#pragma unroll
+  for (int i = N - 1; i >= 0; --i) {
+    double t = y[i];
+#pragma unroll
+    for (int k = i + 1; k < N; ++k) t = t - A[i][k] * x[k];
+    x[i] = t / A[i][i];
+  }
+}
+
+// Cholesky of an SPD N x N (upper R); returns false on a non-positive pivot.
+template <int N>
+__device__ __forceinline__ bool chol_n(const double E[N][N], double R[N][N]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double s = E[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s = s - R[k][j] * R[k][j];
+    if (!(s > 0)) ok = false;
+    R[j][j] = sqrt(s);
+#pragma unroll
+    for (int i = j + 1; i < N; ++i) {
+      double t = E[j][i];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t = t - R[k][j] * R[k][i];
+      R[j][i] = t / R[j][j];
+    }
+  }
+  return ok;
+}
+template <int N>
+__device__ __forceinline__ void chol_apply(const double R[N][N], const double b[N], double x[N]) {
+  double y[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t = t - R[k][i] * y[k];
+    y[i] = t / R[i][i];
+  }
+#pragma unroll
+  for (int i = N - 1; i >= 0; --i) {
+    double t = y[i];
+#pragma unroll
+    for (int k = i + 1; k < N; ++k) t = t - R[i][k] * x[k];
+    x[i] = t / R[i][i];
+  }
+}
+// MATLAB E\b for symmetric E with positive diagonal: Cholesky, else LU.
+template <int N>
+__device__ __forceinline__ void mldiv_spd(const double E[N][N], const double R[N][N], bool ok, const double b[N],
+                                          double x[N]) {
+  if (ok) chol_apply<N>(R, b, x);
+  else lu_solve_n<N>(E, b, x);
+}
+
+// sigma_min of a symmetric PSD N x N via cyclic Jacobi (orc_sigma_min)
+template <int N>
+__device__ __forceinline__ double sigma_min_n(const double G[N][N]) {
+  double a[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[i][j] = G[i][j];
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    double off = 0.0, dg = 0.0;
+#pragma unroll
+    for (int p = 0; p < N; ++p) {
+      dg = dg + a[p][p] * a[p][p];
+#pragma unroll
+      for (int q = p + 1; q < N; ++q) off = off + a[p][q] * a[p][q];
+    }
+    if (!(off > 1e-36 * dg)) break;
+#pragma unroll
+    for (int p = 0; p < N - 1; ++p)
+#pragma unroll
+      for (int q = p + 1; q < N; ++q) {
+        double apq = a[p][q];
+        if (apq != 0.0) {
+          double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+          double t;
+          if (fabs(theta) > 1e150) {
+            t = 0.5 / theta;
+          } else {
+            t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0) t = -t;
+          }
+          double c = 1.0 / sqrt(t * t + 1.0), s = t * c, tau = s / (1.0 + c);
+          a[p][p] = a[p][p] - t * apq;
+          a[q][q] = a[q][q] + t * apq;
+          a[p][q] = 0.0;
+          a[q][p] = 0.0;
+#pragma unroll
+          for (int r = 0; r < N; ++r) {
+            if (r == p || r == q) continue;
+            double g = a[r][p], h = a[r][q];
+            double gn = g - s * (h + g * tau), hn = h + s * (g - h * tau);
+            a[r][p] = gn; a[p][r] = gn;
+            a[r][q] = hn; a[q][r] = hn;
+          }
+        }
+      }
+  }
+  double m = fabs(a[0][0]);
+#pragma unroll
+  for (int i = 1; i < N; ++i)
+    if (fabs(a[i][i]) < m) m = fabs(a[i][i]);
+  return m;
+}
+
+// Linearisation record (EKFmatsHandler outputs)
+struct Lin {
+  double a[6], Csoc[6], Dsoc, Cv[6], Dv, Cphi[6], Dphi, bv, bphi, xhat[6];
+};
+
+__device__ __forceinline__ void lin_store(double *o, const Lin &L) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    o[0 + k] = L.a[k];
+    o[6 + k] = L.Csoc[k];
+    o[13 + k] = L.Cv[k];
+    o[20 + k] = L.Cphi[k];
+    o[29 + k] = L.xhat[k];
+  }
+  o[12] = L.Dsoc; o[19] = L.Dv; o[26] = L.Dphi; o[27] = L.bv; o[28] = L.bphi;
+}
+__device__ __forceinline__ void lin_load(const double *o, Lin &L) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    L.a[k] = o[0 + k];
+    L.Csoc[k] = o[6 + k];
+    L.Cv[k] = o[13 + k];
+    L.Cphi[k] = o[20 + k];
+    L.xhat[k] = o[29 + k];
+  }
+  L.Dsoc = o[12]; L.Dv = o[19]; L.Dphi = o[26]; L.bv = o[27]; L.bphi = o[28];
+}
+
+// EKFmatsHandler.m:26-114.  zTE1.. are the role rows of zk, Zsoc = zk(end).
+template <int NZ>
+__device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
+                                             double Zsoc, double TK, Lin &L) {
+  int imax = 0;
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+    if (xi.g[j] > xi.g[imax] || (xi.g[imax] != xi.g[imax] && xi.g[j] == xi.g[j])) imax = j;
+  int m = xi.m[0];
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+    if (imax == j) m = xi.m[j];
+  const double *Cm = cc.L + m * cc.stride;
+  const double *Dm = Cm + NZ * NX;
+  const double *am = Dm + NZ;
+  double x[NX];
+  load_x(cc.erec + (size_t)m * REC, x);
+#pragma unroll
+  for (int k = 0; k < NX; ++k) { L.xhat[k] = x[k]; L.a[k] = am[k]; }
+  L.xhat[NX] = 0.0;
+  L.a[NX] = 1.0;
+  double rr = -r.Ts / (3600 * r.Q);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) L.Csoc[k] = 0.0;
+  L.Csoc[NX] = rr;
+  L.Dsoc = 0.0;
+  double SOCnAvg = r.th0n + Zsoc * (r.th100n - r.th0n);
+  double i0n = cc.k0n * sqrt(zr[R_TE1] * (1 - zr[R_TH0]) * zr[R_TH0]);
+  double i0p = cc.k0p * sqrt(zr[R_TEE] * (1 - zr[R_TH3]) * zr[R_TH3]);
+#pragma unroll
+  for (int k = 0; k < NX; ++k)
+    L.Cv[k] = r.Rfp * Cm[R_IFDL3 * NX + k] - r.Rfn * Cm[R_IFDL0 * NX + k] + Cm[R_PHIE * NX + k];
+  L.Cv[NX] = 0.0;
+  L.Dv = r.Rfp * Dm[R_IFDL3] - r.Rfn * Dm[R_IFDL0] + Dm[R_PHIE];
+  double dT = TK - r.Tref;
+  double Upos = uocp(cc.tb, cc.ntab, 1, zr[R_TH3], dT), Uneg = uocp(cc.tb, cc.ntab, 0, zr[R_TH0], dT);
+  double negEta0 = 2 * r.R * TK / r.F * asinh(zr[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * TK / r.F * asinh(zr[R_IF3] / (2 * i0p));
+  double b_phi = 0.01 * 0;
+  L.bv = (Upos - Uneg) + (posEta3 - negEta0) + b_phi;
+  L.bphi = uocp(cc.tb, cc.ntab, 0, SOCnAvg, r.Tref - r.Tref);
+#pragma unroll
+  for (int k = 0; k < NX; ++k) L.Cphi[k] = Cm[R_NPHISE2 * NX + k];
+  L.Cphi[NX] = 0.0;
+  L.Dphi = Dm[R_NPHISE2];
+}
+
+// The constraint matrix of constraintsMPC.m (all switches on) has a fixed
+// pattern: rows [Cu; -Cu; I; -I] are constants and the voltage / eta / SOC rows
+// are lower-triangular Toeplitz in the impulse responses Hv, He, Hs.  Only those
+// 3*NP numbers are kept; mval() reproduces every entry (with the same signed
+// zeros) at compile-time indices.
+struct Cons {
+  double Hv[NP], He[NP], Hs[NP];
+  double gam[NCON];
+};
+
+__device__ __forceinline__ double mval(const Cons &C, int i, int k) {
+  if (i < NC) return k <= i ? 1.0 : 0.0;                              // Cu
+  if (i < 2 * NC) return -((k <= i - NC) ? 1.0 : 0.0);                // -Cu
+  if (i < 3 * NC) return (i - 2 * NC) == k ? 1.0 : 0.0;               // I
+  if (i < 4 * NC) return -((i - 3 * NC) == k ? 1.0 : 0.0);            // -I
+  if (i < 4 * NC + NP) { int r = i - 4 * NC; return k <= r ? C.Hv[r - k] : 0.0; }          // G_v
+  if (i < 4 * NC + 2 * NP) { int r = i - 4 * NC - NP; return -(k <= r ? C.He[r - k] : 0.0); }  // -G_e
+  int r = i - 4 * NC - 2 * NP;
+  return k <= r ? C.Hs[r - k] : 0.0;                                   // G_soc
+}
+
+// constraintsMPC.m:11-112 for NP x NC (terminal row off, as runMPC)
+__device__ __forceinline__ void constraints_s(const KCfg &cf, const Lin &L, const double dx[NA], double uk_1,
+                                              double SOCk_1, const double Phis[NP][NA], const double Hs[NP],
+                                              Cons &C) {
+  int nr = 0;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) C.gam[nr + i] = (cf.u_max - uk_1) * 1.0;
+  nr += NC;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) C.gam[nr + i] = -(cf.u_min - uk_1) * 1.0;
+  nr += NC;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) C.gam[nr + i] = cf.du_max * 1.0;
+  nr += NC;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) C.gam[nr + i] = -cf.du_min * 1.0;
+  nr += NC;
+  double Phi[NP][NA], Cb[7];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Cb[k] = L.Cv[k];
+  Cb[6] = L.Dv;
+  predmat_s(L.a, Cb, Phi, C.Hv);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc = acc + Phi[i][k] * dx[k];
+    double rhs = acc + L.bv * 1.0;
+    C.gam[nr + i] = cf.v_max - rhs;
+  }
+  nr += NP;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Cb[k] = L.Cphi[k];
+  Cb[6] = L.Dphi;
+  predmat_s(L.a, Cb, Phi, C.He);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc = acc + Phi[i][k] * dx[k];
+    double rhs = acc + L.bphi * 1.0;
+    C.gam[nr + i] = -cf.phise_min + rhs;
+  }
+  nr += NP;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    C.Hs[i] = Hs[i];
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc = acc + Phis[i][k] * dx[k];
+    double rhs = acc + SOCk_1 * 1.0;
+    C.gam[nr + i] = cf.zmax * 1.0 - rhs;
+  }
+}
+
+// hildreth.m:17-46.  H = M*(E\M') is re-formed entry by entry in the exact
+// summation order of the dense product (orc_hildreth), never stored.
+template <class MV>
+__device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC], const double F[NC],
+                                             const double gam[NCON], double lam[NCON], int maxIter, double tol,
+                                             double DU[NC]) {
+  double R[NC][NC];
+  bool ok = chol_n<NC>(E, R);
+  double X[NCON][NC];
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    double b[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) b[k] = Mf(i, k);
+    mldiv_spd<NC>(E, R, ok, b, X[i]);
+  }
+  double y[NC];
+  mldiv_spd<NC>(E, R, ok, F, y);
+  double K[NCON];
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s = s + Mf(i, k) * y[k];
+    K[i] = s + gam[i];
+  }
+  int it;
+  for (it = 1; it <= maxIter; ++it) {
+#pragma unroll
+    for (int i = 0; i < NCON; ++i)
+#pragma unroll
+      for (int k = 0; k < NC; ++k) launder(X[i][k]);
+    bool conv = true;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) {
+      double s = 0.0, hii = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCON; ++j) {
+        double h = 0.0;
+#pragma unroll
+        for (int k = 0; k < NC; ++k) h = h + Mf(i, k) * X[j][k];
+        if (j == i) hii = h;
+        s = s + h * lam[j];
+      }
+      double w = -((K[i] + s) - hii * lam[i]) / hii;
+      double nl = w > 0 ? w : 0.0;
+      double d = nl - lam[i];
+      if (!(fabs(d) < tol)) conv = false;
+      lam[i] = nl;
+    }
+    if (conv) break;
+  }
+  if (it > maxIter) it = maxIter;
+  double rhs[NC], mE[NC][NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) s = s + Mf(i, k) * lam[i];
+    rhs[k] = F[k] + s;
+  }
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) mE[a][b] = -E[a][b];
+  lu_solve_n<NC>(mE, rhs, DU);
+  return it;
+}
+
+struct ConsM {
+  const Cons &C;
+  __device__ __forceinline__ double operator()(int i, int k) const { return mval(C, i, k); }
+};
+struct DenseM {
+  const double (&M)[NCON][NC];
+  __device__ __forceinline__ double operator()(int i, int k) const { return M[i][k]; }
+};
+
+struct MpcOut {
+  double uk, J_unc, J_fin;
+  int nexec, nviol;
+};
+
+// iterMPC.m:17-95 (poles/sv diagnostics of :54-60 are out of scope)
+__device__ __forceinline__ void mpc_step(const KCfg &cf, const Lin &L, double &uk_1, double SOCk_1, double lam[NCON],
+                                         MpcOut &o) {
+  double dx[NA];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dx[k] = L.xhat[k];
+  dx[6] = uk_1;
+  double Phis[NP][NA], Hs[NP], Cb[7];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Cb[k] = L.Csoc[k];
+  Cb[6] = L.Dsoc;
+  predmat_s(L.a, Cb, Phis, Hs);
+  double Gs[NP][NC];
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+#pragma unroll
+    for (int j = 0; j < NC; ++j) Gs[i][j] = j <= i ? Hs[i - j] : 0.0;
+  double e[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) acc = acc + Phis[i][k] * dx[k];
+    e[i] = cf.ref * 1.0 - acc;
+  }
+  double F[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) acc = acc + (-2 * Gs[i][j]) * e[i];
+    F[j] = acc;
+  }
+  double GtG[NC][NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) acc = acc + Gs[i][a] * Gs[i][b];
+      GtG[a][b] = acc;
+    }
+  double smin = sigma_min_n<NC>(GtG);
+  double nF = 0.0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) nF = nF + F[j] * F[j];
+  nF = sqrt(nF);
+  double Ru = (nF / (2 * cf.du_max * sqrt((double)NC))) - smin;
+  double E[NC][NC], mE[NC][NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+      E[a][b] = 2 * (GtG[a][b] + Ru * (a == b ? 1.0 : 0.0));
+      mE[a][b] = -E[a][b];
+    }
+  double DU[NC];
+  lu_solve_n<NC>(mE, F, DU);
+  auto cost = [&](const double du[NC]) {
+    double J = 0.0, Jq = 0.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc = acc + Gs[i][j] * du[j];
+      double rr = e[i] - acc;
+      J = J + rr * rr;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) acc = acc + (Ru * (c == k ? 1.0 : 0.0)) * du[k];
+      Jq = Jq + acc * du[c];
+    }
+    return J + Jq;
+  };
+  o.J_unc = cost(DU);
+  Cons Cn;
+  constraints_s(cf, L, dx, uk_1, SOCk_1, Phis, Hs, Cn);
+  ConsM Mf{Cn};
+  int nv = 0;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc = acc + Mf(i, j) * DU[j];
+    if (acc - Cn.gam[i] > 0) nv++;
+  }
+  o.nexec = 0;
+  if (nv > 0) o.nexec = hildreth_core(Mf, E, F, Cn.gam, lam, cf.max_hild, cf.hild_tol, DU);
+  double uk = DU[0] + uk_1;
+  uk_1 = uk;
+  o.uk = uk;
+  int nviol = 0;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc = acc + Mf(i, j) * DU[j];
+    if (acc - Cn.gam[i] > 1e-9) nviol++;
+  }
+  o.nviol = nviol;
+  o.J_fin = cost(DU);
+}
+
+// ---------------------------------------------------------------------------
+// LDS staging
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void stage_lds(double *dst, const double *src, int len) {
+  int n2 = len / 2;
+  const double2 *s2 = reinterpret_cast<const double2 *>(src);
+  double2 *d2 = reinterpret_cast<double2 *>(dst);
+  for (int i = threadIdx.x; i < n2; i += blockDim.x) d2[i] = s2[i];
+  if ((len & 1) && threadIdx.x == 0) dst[len - 1] = src[len - 1];
+}
+
+// ---------------------------------------------------------------------------
+// k_plant: OB_step simStep outputs for every cell (lane per cell)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout) {
+  extern __shared__ double lds[];
+  stage_lds(lds, r.plant_blob, r.plant_len);
+  __syncthreads();
+  const double *Tp = lds + r.plant_tab + 6 * r.ntab;
+  const double *Zp = Tp + MAXT;
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  if (s.status[c] & ST_ERROR) {
+    vout[c] = __builtin_nan("");
+    return;
+  }
+  const double *tb = lds + r.plant_tab;
+  int nt = r.ntab;
+  double Iapp = iapp[c];
+  double T = s.Tc[c] + 273.15;
+  double dT = T - r.Tref;
+  double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
+  double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
+  double dUn = duocp(tb, nt, 0, SOCnAvg), dUp = duocp(tb, nt, 1, SOCpAvg);
+  double dQn = fabs(r.th100n - r.th0n), dQp = fabs(r.th100p - r.th0p);
+  double res0n = -dQn / (3600 * r.Q - s.Cdlen[c] * dQn * dUn);
+  double res0p = dQp / (3600 * r.Q - s.Cdlep[c] * dQp * dUp);
+  SOCnAvg = SOCnAvg + res0n * Iapp * r.Ts;
+  SOCpAvg = SOCpAvg + res0p * Iapp * r.Ts;
+  if (SOCnAvg < 0) SOCnAvg = 0;
+  if (SOCnAvg > 1) SOCnAvg = 1;
+  if (SOCpAvg < 0) SOCpAvg = 0;
+  if (SOCpAvg > 1) SOCpAvg = 1;
+  int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
+  if (r.nZ > 1) {
+    int a, b;
+    two_nearest(Zp, r.nZ, cellSOC, a, b);
+    iZu = a > b ? a : b; iZl = a < b ? a : b;
+  }
+  if (r.nT > 1) {
+    int a, b;
+    two_nearest(Tp, r.nT, T, a, b);
+    iTu = a > b ? a : b; iTl = a < b ? a : b;
+  }
+  double Zu = Zp[iZu], Zl = Zp[iZl], Tu = Tp[iTu], Tl = Tp[iTl];
+  int mm[4] = {iTl * r.nZ + iZl, iTl * r.nZ + iZu, iTu * r.nZ + iZl, iTu * r.nZ + iZu};
+  double y[4][NPLANT];
+  const double *bx = s.bigx + (size_t)c * r.NM * 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double2 *p = reinterpret_cast<const double2 *>(bx + (size_t)mm[j] * 6);
+    double2 q0 = p[0], q1 = p[1], q2 = p[2];
+    double x[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+    const double *B = lds + mm[j] * PREC;
+#pragma unroll
+    for (int q = 0; q < NPLANT; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) acc = acc + B[q * NX + k] * x[k];
+      acc = acc + B[NPLANT * NX + q] * x[5];
+      y[j][q] = acc + B[NPLANT * NX + NPLANT + q] * Iapp;
+      launder(y[j][q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double aZ = 0.0, aT = 0.0;
+  if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
+  if (Tu != Tl) aT = (T - Tl) / (Tu - Tl);
+  double yk[NPLANT];
+#pragma unroll
+  for (int q = 0; q < NPLANT; ++q)
+    yk[q] = (1 - aT) * ((1 - aZ) * y[0][q] + aZ * y[1][q]) + aT * ((1 - aZ) * y[2][q] + aZ * y[3][q]);
+  double th0 = fmin(fmax(yk[R_TH0] + s.SOC0n[c], 1e-6), 1 - 1e-6);
+  double th3 = fmin(fmax(yk[R_TH3] + s.SOC0p[c], 1e-6), 1 - 1e-6);
+  double te1 = fmax(yk[R_TE1] + 1, 1e-6);
+  double teE = fmax(yk[R_TEE] + 1, 1e-6);
+  double i0n = s.k0n[c] * sqrt(te1 * (1 - th0) * th0);
+  double i0p = s.k0p[c] * sqrt(teE * (1 - th3) * th3);
+  double negEta0 = 2 * r.R * T / r.F * asinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * T / r.F * asinh(yk[R_IF3] / (2 * i0p));
+  double Uocpn0 = uocp(tb, nt, 0, th0, dT), Uocpp3 = uocp(tb, nt, 1, th3, dT);
+  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (r.Rfp * yk[R_IFDL3] - r.Rfn * yk[R_IFDL0]);
+  V = V - r.Rc * Iapp;
+  s.SOCn[c] = SOCnAvg;
+  s.SOCp[c] = SOCpAvg;
+  vout[c] = V;
+}
+
+// ---------------------------------------------------------------------------
+// k_bulk: all-model plant advance and EKF time update (HBM streaming)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const KState s, const double *iapp,
+                                              int do_plant, int do_ekf) {
+  extern __shared__ double lds[];
+  const int NM = r.NM;
+  const int ne = NM * REC, np = NM * 6;
+  stage_lds(lds, r.bulk_tab, 2 * ne + np);
+  __syncthreads();
+  const double *cA = lds, *cB = lds + ne, *cP = lds + 2 * ne;
+  const double W = cf.SigmaW;
+  for (int64_t c = blockIdx.x; c < s.n; c += gridDim.x) {
+    if (do_ekf) {
+      double pri = s.priorI[c];
+      double2 *base = reinterpret_cast<double2 *>(s.ekf + (size_t)c * ne);
+      for (int j = threadIdx.x; j < ne / 2; j += blockDim.x) {
+        int e0 = (2 * j) % REC;
+        double2 v = base[j];
+        double add0 = e0 < NX ? pri : W;
+        double add1 = e0 + 1 < NX ? pri : W;
+        v.x = (cA[2 * j] * v.x) * cB[2 * j] + add0;
+        v.y = (cA[2 * j + 1] * v.y) * cB[2 * j + 1] + add1;
+        base[j] = v;
+      }
+    }
+    if (do_plant) {
+      double u = iapp[c];
+      double2 *base = reinterpret_cast<double2 *>(s.bigx + (size_t)c * np);
+      for (int j = threadIdx.x; j < np / 2; j += blockDim.x) {
+        double2 v = base[j];
+        v.x = cP[2 * j] * v.x + u;
+        v.y = cP[2 * j + 1] * v.y + u;
+        base[j] = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_cell: iterEKF measurement update + EKFmatsHandler + iterMPC (lane per cell)
+// ---------------------------------------------------------------------------
+template <int NZ>
+__global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
+  extern __shared__ double lds[];
+  stage_lds(lds, r.cell_blob, r.cell_len);
+  __syncthreads();
+  const double *Tp = lds + r.cell_tab + 6 * r.ntab;
+  const double *Zp = Tp + MAXT;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  const int nz = r.nz;
+  const double NaN = __builtin_nan("");
+  CellCtx cc;
+  cc.L = lds;
+  cc.tb = lds + r.cell_tab;
+  cc.Tp = Tp;
+  cc.Zp = Zp;
+  cc.erec = s.ekf + (size_t)c * r.NM * REC;
+  cc.ntab = r.ntab;
+  cc.stride = r.cell_stride;
+  const double Tc = s.Tc[c];
+  cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
+  cc.dT = cc.T - r.Tref;
+  cc.k0n = s.k0n[c];
+  cc.k0p = s.k0p[c];
+  int st = s.status[c];
+  const bool fused = io.mode & MODE_FUSED;
+
+  auto fail_outputs = [&]() {
+    if (io.u) io.u[c] = NaN;
+    if (io.v) io.v[c] = NaN;
+    if (io.soc) io.soc[c] = NaN;
+    if (io.phise) io.phise[c] = NaN;
+    if (io.nexec) io.nexec[c] = 0;
+    if (io.zk)
+      for (int q = 0; q < nz + 2; ++q) io.zk[c * (nz + 2) + q] = NaN;
+    if (io.zbk)
+      for (int q = 0; q < nz + 2; ++q) io.zbk[c * (nz + 2) + q] = NaN;
+    if (io.uk_out) io.uk_out[c] = NaN;
+    if (io.lin_out)
+      for (int q = 0; q < 35; ++q) io.lin_out[c * 35 + q] = NaN;
+    if (io.xm_out)
+      for (int q = 0; q < 4; ++q) { io.xm_out[c * 4 + q] = -1; io.xg_out[c * 4 + q] = NaN; }
+  };
+
+  double Z[NZ];
+  double vhat = 0.0, Zsoc = 0.0;
+  XI xi;
+  double ik = 0.0, vk = 0.0;
+  if (io.mode & (MODE_EKF | MODE_FUSED)) {
+    if (st & ST_ERROR) {
+      fail_outputs();
+      return;
+    }
+    ik = fused ? s.uk[c] : io.ik_in[c];
+    vk = fused ? s.vk[c] : io.vk_in[c];
+    int warn = s.warn[c];
+    if (warn > cf.max_warn) {  // iterEKF.m:55-59
+      st |= ST_LOCKOUT | ST_ERROR;
+      s.status[c] = st;
+      if (fused) s.uk[c] = NaN;
+      fail_outputs();
+      return;
+    }
+    double x0 = s.x0[c] + s.priorI[c];  // iterEKF.m:85-86 (models: k_bulk)
+    double S0 = s.S0[c] + cf.SigmaW;
+    const double SOC0 = s.SOC0[c];
+    double SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
+    if (st & ST_ERROR) {
+      s.status[c] = st;
+      s.warn[c] = warn;
+      if (fused) s.uk[c] = NaN;
+      fail_outputs();
+      return;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double ChatV[4][NX], C0;
+    get_chatv<NZ>(r, cc, xi, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
+    double S1[NPK];
+    load_S(cc.erec + (size_t)xi.m[0] * REC, S1);
+    double St[4], Lg[4][NX];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double row[NX];
+#pragma unroll
+      for (int cI = 0; cI < NX; ++cI) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) acc = acc + S1[pk(k, cI)] * ChatV[j][k];
+        row[cI] = acc;
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int cI = 0; cI < NX; ++cI) acc = acc + row[cI] * ChatV[j][cI];
+      St[j] = acc + cf.SigmaV;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) Lg[j][k] = row[k] / St[j];
+    }
+    double St0 = C0 * S0 * C0 + cf.SigmaV;
+    double L0 = S0 * C0 / St0;
+    double res = vk - vhat;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      launder(St[j]);
+#pragma unroll
+      for (int k = 0; k < NX; ++k) launder(Lg[j][k]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      meas_update(cc.erec + (size_t)xi.m[j] * REC, Lg[j], St[j], res);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    x0 = x0 + L0 * res;
+    S0 = S0 - L0 * St0 * L0;
+    SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
+    __builtin_amdgcn_sched_barrier(0);
+    s.warn[c] = warn;
+    if (st & ST_ERROR) {
+      s.status[c] = st;
+      s.x0[c] = x0;
+      s.S0[c] = S0;
+      if (fused) s.uk[c] = NaN;
+      fail_outputs();
+      return;
+    }
+#ifndef PROBE_NO_BOUNDS
+    if (io.zbk) {
+      // getChatZ + boundzk (iterEKF.m:186-205, 523-602), diagonal only
+      double ChV[4][NX], ChV0;
+      get_chatv<NZ>(r, cc, xi, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChV, ChV0);
+      double res0n = -r.Ts * ((r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n))) / (3600 * r.Q);
+      double res0p = -r.Ts * ((r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p))) / (3600 * r.Q);
+      double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+      double dUn = duocp(cc.tb, cc.ntab, 0, r.th0n + xSOC * (r.th100n - r.th0n));
+      double dUp = duocp(cc.tb, cc.ntab, 1, r.th0p + xSOC * (r.th100p - r.th0p));
+      double S1b[NPK];
+      load_S(cc.erec + (size_t)xi.m[0] * REC, S1b);
+      double SigV = 0.0;
+      double SigZ[NZ];
+#pragma unroll
+      for (int q = 0; q < NZ; ++q) SigZ[q] = 0.0;
+      const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double g = xi.g[j];
+        const double *Cm = cc.L + xi.m[j] * cc.stride;
+        double cph0[NX];
+#pragma unroll
+        for (int k = 0; k < NX; ++k) {
+          double v = g * Cm[R_PHISE0 * NX + k];
+          if (ph0pp) v = v + ChV[j][k];
+          cph0[k] = v;
+        }
+#pragma unroll
+        for (int q = 0; q < NZ; ++q) {
+          double row[NX];
+          unsigned f = r.flags[q];
+#pragma unroll
+          for (int k = 0; k < NX; ++k) {
+            double v = g * Cm[q * NX + k];
+            if (f & G_PPHIS) v = v + ChV[j][k];
+            if (f & G_PHIE) v = v - cph0[k];
+            row[k] = v;
+          }
+          double qf = 0.0;
+#pragma unroll
+          for (int cI = 0; cI < NX; ++cI) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < NX; ++k) acc = acc + row[k] * S1b[pk(k, cI)];
+            qf = qf + acc * row[cI];
+          }
+          SigZ[q] = SigZ[q] + qf;
+          launder(SigZ[q]);
+        }
+        double row2[NX];
+#pragma unroll
+        for (int cI = 0; cI < NX; ++cI) {
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < NX; ++k) acc = acc + S1b[pk(k, cI)] * ChV[j][k];
+          row2[cI] = acc;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int cI = 0; cI < NX; ++cI) acc = acc + row2[cI] * ChV[j][cI];
+        SigV = SigV + acc;
+        launder(SigV);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int q = 0; q < NZ; ++q) {
+        double c0 = 0.0;
+        switch (r.c0k[q]) {
+          case C0_CHATV0: c0 = ChV0; break;
+          case C0_RES0N: c0 = res0n; break;
+          case C0_RES0P: c0 = res0p; break;
+          case C0_DUN: c0 = dUn * res0n; break;
+          case C0_DUP: c0 = dUp * res0p; break;
+          case C0_MDUN: c0 = -dUn * res0n; break;
+          default: break;
+        }
+        SigZ[q] = SigZ[q] + (c0 * S0) * c0;
+        if (q < nz) io.zbk[c * (nz + 2) + r.perm[q]] = 3 * sqrt(SigZ[q]);
+      }
+      SigV = SigV + ChV0 * S0 * ChV0;
+      double rr = -r.Ts / (3600 * r.Q);
+      double SigSOC = rr * S0 * rr;
+      io.zbk[c * (nz + 2) + nz] = 3 * sqrt(SigV);
+      io.zbk[c * (nz + 2) + nz + 1] = 3 * sqrt(SigSOC);
+    }
+#endif
+    s.x0[c] = x0;
+    s.S0[c] = S0;
+    s.priorI[c] = ik;  // iterEKF.m:210
+    if (io.zk) {
+#pragma unroll
+      for (int q = 0; q < NZ; ++q)
+        if (q < nz) io.zk[c * (nz + 2) + r.perm[q]] = Z[q];
+      io.zk[c * (nz + 2) + nz] = vhat;
+      io.zk[c * (nz + 2) + nz + 1] = Zsoc;
+    }
+    if (io.xm_out) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
+    }
+  }
+
+  Lin L;
+  if (io.mode & (MODE_LIN | MODE_FUSED)) {
+    double zr[NROLE];
+    if (fused) {
+#pragma unroll
+      for (int q = 0; q < NROLE; ++q) zr[q] = Z[q];
+    } else {
+      if (st & ST_ERROR) { fail_outputs(); return; }
+#pragma unroll
+      for (int q = 0; q < NROLE; ++q) zr[q] = io.zk_in[c * (nz + 2) + r.perm[q]];
+      Zsoc = io.zk_in[c * (nz + 2) + nz + 1];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { xi.m[j] = io.xm_in[c * 4 + j]; xi.g[j] = io.xg_in[c * 4 + j]; }
+    }
+    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L);
+    if (io.lin_out) lin_store(io.lin_out + c * 35, L);
+  }
+
+#ifndef PROBE_NO_MPC
+  if (io.mode & (MODE_MPC | MODE_FUSED)) {
+    if (!fused) {
+      if (st & ST_ERROR) { fail_outputs(); return; }
+      lin_load(io.lin_in + c * 35, L);
+      Zsoc = io.soc_k1_in[c];
+    }
+    double lam[NCON];
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * s.n + c];
+    double uk_1 = s.uk_1[c];
+    double ukin = fused ? s.uk[c] : 0.0;
+    double phise = 0.0;
+    if (fused) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc = acc + L.Cphi[k] * L.xhat[k];
+      phise = acc + ukin * L.Dphi + L.bphi;  // runMPC.m:94-95
+    }
+    MpcOut o;
+    mpc_step(cf, L, uk_1, Zsoc, lam, o);
+    s.uk_1[c] = uk_1;
+    if (o.nexec > 0) {
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * s.n + c] = lam[i];  // iterMPC.m:68
+    }
+    if (s.J_unc) { s.J_unc[c] = o.J_unc; s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
+    if (io.uk_out) io.uk_out[c] = o.uk;
+    if (io.nexec) io.nexec[c] = o.nexec;
+    if (fused) {
+      s.uk[c] = o.uk;
+      if (io.u) io.u[c] = o.uk;
+      if (io.v) io.v[c] = vk;
+      if (io.soc) io.soc[c] = Zsoc;
+      if (io.phise) io.phise[c] = phise;
+    }
+  }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// context-free batched kernels
+// ---------------------------------------------------------------------------
+__global__ void k_predmat(int64_t n, const double *a, const double *C, const double *D, double *Phi, double *G) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  double av[6], Cb[7], P[NP][NA], H[NP];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { av[k] = a[c * 6 + k]; Cb[k] = C[c * 6 + k]; }
+  Cb[6] = D[c];
+  predmat_s(av, Cb, P, H);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) Phi[(c * NP + i) * NA + k] = P[i][k];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) G[(c * NP + i) * NC + j] = j <= i ? H[i - j] : 0.0;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_constraints(const KCfg cf, int64_t n, const double *lin,
+                                                    const double *uk_1, const double *soc_k1, double *Mo,
+                                                    double *go) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  Lin L;
+  lin_load(lin + c * 35, L);
+  double dx[NA];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dx[k] = L.xhat[k];
+  dx[6] = uk_1[c];
+  double Phis[NP][NA], Hs[NP], Cb[7];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Cb[k] = L.Csoc[k];
+  Cb[6] = L.Dsoc;
+  predmat_s(L.a, Cb, Phis, Hs);
+  Cons Cn;
+  constraints_s(cf, L, dx, uk_1[c], soc_k1[c], Phis, Hs, Cn);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    go[c * NCON + i] = Cn.gam[i];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) Mo[(c * NCON + i) * NC + j] = mval(Cn, i, j);
+  }
+}
+
+// hildreth.m for an arbitrary (E, F, M, gamma): M is data, not the pattern.
+__global__ void __launch_bounds__(64) k_hildreth(int64_t n, const double *Ei, const double *Fi, const double *Mi,
+                                                 const double *gi, double *lami, int maxIter, double tol,
+                                                 double *DUo, int *nexec) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  double E[NC][NC], F[NC], M[NCON][NC], gam[NCON], lam[NCON], DU[NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) {
+    F[a] = Fi[c * NC + a];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) E[a][b] = Ei[(c * NC + a) * NC + b];
+  }
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    gam[i] = gi[c * NCON + i];
+    lam[i] = lami[c * NCON + i];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) M[i][j] = Mi[(c * NCON + i) * NC + j];
+  }
+  DenseM Mf{M};
+  int it = hildreth_core(Mf, E, F, gam, lam, maxIter, tol, DU);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) lami[c * NCON + i] = lam[i];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) DUo[c * NC + a] = DU[a];
+  nexec[c] = it;
+}
+
+// initKF.m:94-95 / OB_step.m:185: xhat = 0, SigmaX = SigmaX0(1:5,1:5), bigX = 0
+__global__ void k_init_state(int64_t n, int NM, double *ekf, double *bigx, double s0, double s1, double s2, double s3,
+                             double s4) {
+  const double d[NX] = {s0, s1, s2, s3, s4};
+  int64_t total = n * NM;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    double *rec = ekf + i * REC;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) rec[k] = 0.0;
+#pragma unroll
+    for (int p = 0; p < NX; ++p)
+#pragma unroll
+      for (int q = p; q < NX; ++q) rec[NX + pk(p, q)] = p == q ? d[p] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) bigx[i * 6 + k] = 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_init_state, dim3(2048), dim3(256), 0, (hipStream_t)stream, n, NM, ekf, bigx, sx0[0], sx0[1],
+                     sx0[2], sx0[3], sx0[4]);
+  return (int)hipGetLastError();
+}
+static int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
+
+int cell_lds_bytes(const KRom &r) { return (int)((r.cell_len + 1) * sizeof(double)); }
+int plant_lds_bytes(const KRom &r) { return (int)((r.plant_len + 1) * sizeof(double)); }
+
+bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
+
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, void *stream) {
+  if (s.n == 0) return 0;
+  hipLaunchKernelGGL(k_plant, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r, s,
+                     iapp, vout);
+  return (int)hipGetLastError();
+}
+
+int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
+                void *stream) {
+  if (s.n == 0) return 0;
+  int lds = (int)((2 * r.NM * REC + r.NM * 6) * sizeof(double));
+  int grid = (int)(s.n < 2048 ? s.n : 2048);
+  hipLaunchKernelGGL(k_bulk, dim3(grid), dim3(256), lds, (hipStream_t)stream, r, c, s, iapp, do_plant, do_ekf);
+  return (int)hipGetLastError();
+}
+
+template <int NZ>
+static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  static bool attr = false;
+  int lds = cell_lds_bytes(r);
+  if (!attr) {
+    hipFuncSetAttribute((const void *)k_cell<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_cell<NZ>, dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+}
+
+int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream) {
+  if (s.n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (r.nzp) {
+    case 26: launch_cell_t<26>(r, c, s, io, st); break;
+    case 32: launch_cell_t<32>(r, c, s, io, st); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_predmat(int64_t n, int Np, int Nc, const double *a, const double *C, const double *D, double *Phi,
+                   double *G, void *stream) {
+  if (Np != NP || Nc != NC) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_predmat, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, a, C, D, Phi, G);
+  return (int)hipGetLastError();
+}
+
+int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double *uk_1, const double *soc_k1,
+                       double *M, double *gam, void *stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_constraints, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, c, n, lin, uk_1,
+                     soc_k1, M, gam);
+  return (int)hipGetLastError();
+}
+
+int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *F, const double *M,
+                    const double *gam, double *lam, int max_iter, double tol, double *DU, int *nexec,
+                    void *stream) {
+  if (Nc != NC || ncon != NCON) return -1;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_hildreth, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, E, F, M, gam, lam,
+                     max_iter, tol, DU, nexec);
+  return (int)hipGetLastError();
+}
+
+}  // namespace mk

@@ -1,0 +1,97 @@
+// mpcekf_kernels.hpp -- shared declarations between the C-ABI host code and the
+// gfx950 kernels (mpcekf_kernels.hip).  Plain structs passed by value as kernel
+// arguments; every pointer is a device pointer.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace mk {
+
+constexpr int NX = 5;      // transient states per local model (initKF.m:60)
+constexpr int NPK = 15;    // packed upper-triangular 5x5 covariance
+constexpr int NA = 7;      // x_aug = [x(6); u] (predMat.m:20-22)
+constexpr int REC = 20;    // per-model EKF record: xhat[5] + SigmaX packed[15]
+constexpr int MAXT = 8;    // max temperature set-points
+constexpr int MAXZ = 40;   // max SOC set-points
+constexpr int MAXROWS = 64;
+constexpr int NPLANT = 9;  // role rows the plant needs (OB_step.m:289-344)
+constexpr int PREC = NPLANT * NX + NPLANT + NPLANT;  // plant blob record per model: C[9][5], res0[9], D[9]
+
+// role slots = the first rows of the permuted output vector (rom.py ROLE_NAMES)
+enum { R_IFDL0 = 0, R_IFDL3, R_IF0, R_IF3, R_TH0, R_TH3, R_TE1, R_TEE, R_PHIE, R_PHISE0, R_NPHISE2, NROLE };
+// per-row group flags (rom.py G_*)
+enum : unsigned { G_NTH = 1, G_PTH = 2, G_NPHISE = 4, G_PPHISE = 8, G_PHIE = 16, G_PHIE0 = 32, G_THETAE = 64,
+                  G_PPHIS = 128 };
+enum { C0_ZERO = 0, C0_CHATV0, C0_RES0N, C0_RES0P, C0_DUN, C0_DUP, C0_MDUN };
+enum { ST_ERROR = 1, ST_LOCKOUT = 2, ST_THETAE_NEG = 4 };
+
+struct KRom {
+  int NM, nT, nZ, nz, nzp, ntab;  // nzp = padded row count the kernel was built for
+  double Ts, Q, F, R, Rc, Tref;
+  double th0n, th100n, th0p, th100p, Rfn, Rfp;
+  unsigned char flags[MAXROWS];   // per permuted row
+  unsigned char c0k[MAXROWS];     // getChatZ Chat0 kind per permuted row
+  short perm[MAXROWS];            // permuted row -> ROM row
+  // blobs end with: tables [6][ntab], Tpts [MAXT] (K), Zpts [MAXZ] (fraction)
+  const double *cell_blob;        // per model [C nzp*5][D nzp][a 5] ... then tables
+  int cell_stride, cell_tab, cell_len;
+  const double *plant_blob;       // per model [C 9*5][res0 9][D 9] ... then tables
+  int plant_tab, plant_len;
+  const double *bulk_tab;         // cA[NM*20], cB[NM*20], cP[NM*6]
+};
+
+struct KCfg {
+  double SigmaV, SigmaW, ref, u_max, u_min, du_min, du_max, v_max, phise_min, zmax, hild_tol;
+  int max_warn, max_hild, flags;
+};
+
+struct KState {
+  int64_t n;
+  double *bigx;   // [n][NM][6]
+  double *ekf;    // [n][NM][20]
+  double *SOCn, *SOCp, *x0, *S0, *priorI, *uk_1, *uk, *vk;  // [n]
+  double *lam;    // [ncon][n]
+  int *warn, *status;
+  // per-cell constants (set at init)
+  const double *Tc, *SOC0, *SOC0n, *SOC0p, *k0n, *k0p, *Cdlen, *Cdlep;
+  // diagnostics of the last MPC step
+  double *J_unc, *J_fin;
+  int *nviol;
+};
+
+// Inputs/outputs of one cell-kernel launch.  Any pointer may be null.
+struct KIO {
+  int mode;               // MODE_* bits
+  int64_t step_stride;    // unused (reserved)
+  // fused trajectories, already offset to this step ([ncells])
+  double *u, *v, *soc, *phise;
+  int *nexec;
+  double *zk, *zbk;       // [n][nz+2] (un-permuted)
+  // stage entry points
+  const double *vk_in, *ik_in;          // ekf stage
+  int *xm_out; double *xg_out;          // [n][4]
+  const double *zk_in; const int *xm_in; const double *xg_in;  // linearize stage
+  double *lin_out; const double *lin_in;                        // [n][35]
+  const double *soc_k1_in; double *uk_out;                      // mpc stage
+};
+
+enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
+
+// host-side launchers (defined in mpcekf_kernels.hip)
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, void *stream);
+int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
+                void *stream);
+int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream);
+int launch_predmat(int64_t n, int Np, int Nc, const double *a, const double *C, const double *D, double *Phi,
+                   double *G, void *stream);
+int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double *uk_1, const double *soc_k1,
+                       double *M, double *gam, void *stream);
+int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *F, const double *M,
+                    const double *gam, double *lam, int max_iter, double tol, double *DU, int *nexec,
+                    void *stream);
+int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream);
+bool cell_kernel_supported(int nzp);
+int cell_lds_bytes(const KRom &r);
+int plant_lds_bytes(const KRom &r);
+
+}  // namespace mk

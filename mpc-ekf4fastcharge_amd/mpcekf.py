@@ -1,0 +1,285 @@
+"""Host-side mirror of the reference's operator interface, over the C-ABI.
+
+The reference exposes MATLAB functions called by name from runMPC.m; this
+module keeps those names and argument meanings, batched over cells:
+
+  Context.OB_step(Iapp)              <- OB_step.m:1        (cellState lives in the context)
+  Context.iterEKF(vk, ik)            <- iterEKF.m:30       (ekfData lives in the context)
+  Context.EKFmatsHandler(zk, Xind)   <- EKFmatsHandler.m:1
+  Context.iterMPC(lin, SOCk_1)       <- iterMPC.m:1        (mpcData lives in the context)
+  predMat(a, C, D, Np, Nc)           <- predMat.m:1        (A = diag(a), B = ones)
+  constraintsMPC(lin, uk_1, SOCk_1)  <- constraintsMPC.m:1
+  hildreth(E, F, M, gamma, lambda0, maxIter) <- hildreth.m:1
+  runMPC(rom, SOC0, TC, nsteps)      <- runMPC.m:72-112    (fused, batched)
+
+Errors: MATLAB ``error()`` becomes :class:`MpcekfError`; per-cell soft failures
+(EKF lock-out, thetae < 0) set ``status`` bits and make that cell's outputs NaN.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import LIN_SIZE, MpcekfError, check, dptr, iptr
+from .rom import ROM, TF_CODE
+
+__all__ = ["Context", "make_config", "predMat", "constraintsMPC", "hildreth", "runMPC", "MpcekfError",
+           "LIN_SIZE"]
+
+LIN_FIELDS = dict(A=slice(0, 6), Csoc=slice(6, 12), Dsoc=12, Cv=slice(13, 19), Dv=19,
+                  Cphi=slice(20, 26), Dphi=26, bv=27, bphi=28, xhat=slice(29, 35))
+
+
+def make_config(**kw) -> _lib.Config:
+    """mpcekf_config with the runMPC.m defaults, overridden by keyword."""
+    L = _lib.load()
+    c = _lib.Config()
+    L.mpcekf_config_defaults(C.byref(c))
+    alias = {"targetSOC": "target_soc", "maxHild": "max_hild"}
+    for k, v in kw.items():
+        k = alias.get(k, k)
+        if k == "constraints":
+            c.use_current, c.use_voltage, c.use_eta = (int(x) for x in v)
+        elif k == "SigmaX0":
+            for i in range(6):
+                c.SigmaX0[i] = float(v[i])
+        elif k == "bounds":
+            c.flags = (c.flags | _lib.CF_BOUNDS) if v else (c.flags & ~_lib.CF_BOUNDS)
+        else:
+            if not hasattr(c, k):
+                raise TypeError(f"unknown config field {k}")
+            setattr(c, k, type(getattr(c, k))(v))
+    return c
+
+
+class _PackedRom:
+    def __init__(self, rom: ROM):
+        self.keep = []
+
+        def arr(x, dt=np.float64):
+            a = np.ascontiguousarray(x, dtype=dt)
+            self.keep.append(a)
+            return a
+
+        r = _lib.Rom()
+        r.nT, r.nZ, r.n, r.nz = rom.nT, rom.nZ, rom.n, rom.nz
+        r.T_degC = dptr(arr(rom.T_degC))
+        r.SOC_pct = dptr(arr(rom.SOC_pct))
+        r.Ts = rom.Ts
+        r.A = dptr(arr(rom.A))
+        r.C = dptr(arr(rom.C))
+        r.D = dptr(arr(rom.D))
+        r.tf_code = iptr(arr([TF_CODE[n] for n in rom.names], np.int32))
+        r.tf_xloc = dptr(arr(rom.xloc))
+        r.F, r.R, r.Q, r.Rc, r.Tref = rom.F, rom.R, rom.Q, rom.Rc, rom.Tref
+        for side in ("neg", "pos"):
+            e = getattr(rom, side)
+            s = getattr(r, side)
+            s.theta0, s.theta100, s.Rf, s.k0ref, s.Ea_k0 = e.theta0, e.theta100, e.Rf, e.k0ref, e.Ea_k0
+            s.wDL, s.Cdl, s.nDL, s.ntab = e.wDL, e.Cdl, e.nDL, len(e.U)
+            s.U, s.dUdT, s.dU = dptr(arr(e.U)), dptr(arr(e.dUdT)), dptr(arr(e.dU))
+        self.s = r
+
+
+class Context:
+    """One device, one stream, ``ncells`` independent cells (mpcekf_ctx)."""
+
+    def __init__(self, rom: ROM, ncells: int, cfg: _lib.Config | None = None, device: int = 0):
+        self.L = _lib.load()
+        self.rom = rom
+        self.cfg = cfg if cfg is not None else make_config()
+        self.device = device
+        self._pr = _PackedRom(rom)
+        h = C.c_void_p()
+        check(self.L.mpcekf_ctx_create(C.byref(self._pr.s), C.byref(self.cfg), device, int(ncells), C.byref(h)))
+        self.h = h
+        n, nm, nz, nc = C.c_int64(), C.c_int32(), C.c_int32(), C.c_int32()
+        check(self.L.mpcekf_ctx_info(h, C.byref(n), C.byref(nm), C.byref(nz), C.byref(nc)))
+        self.n, self.NM, self.nz, self.ncon = n.value, nm.value, nz.value, nc.value
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mpcekf_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _vec(self, x, dtype=np.float64):
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(x, dtype=dtype), (self.n,)))
+        return a
+
+    # -- initKF / initMPC / first OB_step --------------------------------
+    def init_cells(self, soc0_pct, tc_degC):
+        s = self._vec(soc0_pct)
+        t = self._vec(tc_degC)
+        check(self.L.mpcekf_init_cells(self.h, dptr(s), dptr(t)))
+
+    # -- fused loop (runMPC.m:83-112) ------------------------------------
+    def step(self, nsteps, outputs=("u", "v", "soc", "phise", "nexec")):
+        n = self.n
+        out = {}
+        ptr = []
+        for k in ("u", "v", "soc", "phise"):
+            if k in outputs:
+                out[k] = np.empty((nsteps, n))
+                ptr.append(out[k].ctypes.data_as(C.c_void_p))
+            else:
+                ptr.append(None)
+        nex = None
+        if "nexec" in outputs:
+            out["nexec"] = nex = np.empty((nsteps, n), dtype=np.int32)
+        check(self.L.mpcekf_step(self.h, int(nsteps), *ptr,
+                                 nex.ctypes.data_as(C.c_void_p) if nex is not None else None, 0))
+        return out
+
+    def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
+        """Fused steps writing [nsteps][ncells] outputs to device pointers (ints)."""
+        p = [C.c_void_p(x) if x else None for x in (u, v, soc, phise, nexec)]
+        check(self.L.mpcekf_step(self.h, int(nsteps), *p, 1))
+
+    def set_timing(self, enable=True):
+        check(self.L.mpcekf_set_timing(self.h, int(bool(enable))))
+
+    def get_timing(self):
+        """{kernel: (ms_sum, launches)} since the last call (HIP events on the ctx stream)."""
+        ms = np.zeros(3)
+        nl = (C.c_int64 * 3)()
+        check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell"))}
+
+    def get_zk(self):
+        zk = np.empty((self.n, self.nz + 2))
+        zb = np.empty((self.n, self.nz + 2))
+        check(self.L.mpcekf_get_zk(self.h, dptr(zk), dptr(zb)))
+        return zk, zb
+
+    # -- MATLAB-named stage functions --------------------------------------
+    def OB_step(self, Iapp):
+        """[Vcell, ~, cellState] = OB_step(Iapp, Tc, cellState, ROM)  (OB_step.m:1)."""
+        i = self._vec(Iapp)
+        v = np.empty(self.n)
+        check(self.L.mpcekf_plant_step(self.h, dptr(i), dptr(v)))
+        return v
+
+    def iterEKF(self, vk, ik, bounds=True):
+        """[zk, boundzk, ekfData, Xind] = iterEKF(vk, ik, Tk, ekfData)  (iterEKF.m:30).
+
+        Xind is returned as dict(model=[n,4] model index t*nZ+z, theT, theZ, gamma)."""
+        v = self._vec(vk)
+        i = self._vec(ik)
+        zk = np.empty((self.n, self.nz + 2))
+        zb = np.empty((self.n, self.nz + 2)) if bounds else None
+        xm = np.empty((self.n, 4), dtype=np.int32)
+        xg = np.empty((self.n, 4))
+        check(self.L.mpcekf_ekf_step(self.h, dptr(v), dptr(i), dptr(zk), dptr(zb), iptr(xm), dptr(xg)))
+        xind = dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
+        return zk, zb, xind
+
+    def EKFmatsHandler(self, zk, Xind):
+        """[MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)  (EKFmatsHandler.m:1).
+
+        Returns the packed linearisation records [n, 35] (fields: LIN_FIELDS)."""
+        zk = np.ascontiguousarray(zk, dtype=np.float64)
+        xm = np.ascontiguousarray(Xind["model"], dtype=np.int32)
+        xg = np.ascontiguousarray(Xind["gamma"], dtype=np.float64)
+        lin = np.empty((self.n, LIN_SIZE))
+        check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(lin)))
+        return lin
+
+    def iterMPC(self, lin, SOCk_1):
+        """[uk, mpcData] = iterMPC(xk, cellState, mpcData)  (iterMPC.m:1). Returns uk, nexec."""
+        lin = np.ascontiguousarray(lin, dtype=np.float64)
+        s = self._vec(SOCk_1)
+        uk = np.empty(self.n)
+        ne = np.empty(self.n, dtype=np.int32)
+        check(self.L.mpcekf_mpc_step(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne)))
+        return uk, ne
+
+    # -- state -----------------------------------------------------------
+    def get_state(self):
+        n, NM = self.n, self.NM
+        st = dict(bigX=np.empty((n, NM, 6)), ekf=np.empty((n, NM, 20)), scal=np.empty((n, _lib.NSCAL)),
+                  lam=np.empty((n, self.ncon)), warn=np.empty(n, np.int32), status=np.empty(n, np.int32))
+        s = _lib.State(dptr(st["bigX"]), dptr(st["ekf"]), dptr(st["scal"]), dptr(st["lam"]),
+                       iptr(st["warn"]), iptr(st["status"]))
+        check(self.L.mpcekf_get_state(self.h, C.byref(s)))
+        return st
+
+    def set_state(self, st):
+        a = {k: (np.ascontiguousarray(v, dtype=np.int32 if k in ("warn", "status") else np.float64)
+                 if v is not None else None) for k, v in st.items()}
+        s = _lib.State(dptr(a.get("bigX")), dptr(a.get("ekf")), dptr(a.get("scal")), dptr(a.get("lam")),
+                       iptr(a.get("warn")), iptr(a.get("status")))
+        check(self.L.mpcekf_set_state(self.h, C.byref(s)))
+
+
+# ---------------------------------------------------------------------------
+# context-free batched functions
+# ---------------------------------------------------------------------------
+def predMat(a, Cr, D, Np=5, Nc=2, device=0):
+    """predMat.m with A = diag(a) (a [n,6]), B = ones, C [n,6], D [n] -> Phi [n,Np,7], G [n,Np,Nc]."""
+    L = _lib.load()
+    a = np.ascontiguousarray(np.atleast_2d(a), dtype=np.float64)
+    Cr = np.ascontiguousarray(np.atleast_2d(Cr), dtype=np.float64)
+    D = np.ascontiguousarray(np.atleast_1d(D), dtype=np.float64)
+    n = a.shape[0]
+    Phi = np.empty((n, Np, 7))
+    G = np.empty((n, Np, Nc))
+    check(L.mpcekf_predmat(device, n, Np, Nc, dptr(a), dptr(Cr), dptr(D), dptr(Phi), dptr(G)))
+    return Phi, G
+
+
+def constraintsMPC(lin, uk_1, SOCk_1, Q, cfg=None, device=0):
+    """constraintsMPC.m: lin [n,35] -> M [n,ncon,Nc], gamma [n,ncon]."""
+    L = _lib.load()
+    cfg = cfg if cfg is not None else make_config()
+    lin = np.ascontiguousarray(np.atleast_2d(lin), dtype=np.float64)
+    n = lin.shape[0]
+    u = np.ascontiguousarray(np.broadcast_to(uk_1, (n,)), dtype=np.float64)
+    s = np.ascontiguousarray(np.broadcast_to(SOCk_1, (n,)), dtype=np.float64)
+    ncon = 4 * cfg.Nc + 3 * cfg.Np
+    M = np.empty((n, ncon, cfg.Nc))
+    g = np.empty((n, ncon))
+    check(L.mpcekf_constraints(device, C.byref(cfg), float(Q), n, dptr(lin), dptr(u), dptr(s), dptr(M), dptr(g)))
+    return M, g
+
+
+def hildreth(E, F, M, gamma, lambda0=None, maxIter=100, tol=1e-6, device=0):
+    """hildreth.m batched: E [n,Nc,Nc], F [n,Nc], M [n,ncon,Nc], gamma [n,ncon]."""
+    L = _lib.load()
+    E = np.ascontiguousarray(E, dtype=np.float64)
+    n, Nc = E.shape[0], E.shape[1]
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    M = np.ascontiguousarray(M, dtype=np.float64)
+    g = np.ascontiguousarray(gamma, dtype=np.float64)
+    ncon = M.shape[1]
+    lam = np.zeros((n, ncon)) if lambda0 is None else np.array(lambda0, dtype=np.float64, order="C")
+    DU = np.empty((n, Nc))
+    ne = np.empty(n, dtype=np.int32)
+    check(L.mpcekf_hildreth(device, n, Nc, ncon, dptr(E), dptr(F), dptr(M), dptr(g), dptr(lam),
+                            int(maxIter), float(tol), dptr(DU), iptr(ne)))
+    return DU, lam, ne
+
+
+def runMPC(rom, SOC0, TC, nsteps, cfg=None, device=0, ncells=None):
+    """runMPC.m:72-112 for a batch of cells; returns trajectories [nsteps, ncells]."""
+    SOC0 = np.atleast_1d(np.asarray(SOC0, dtype=np.float64))
+    n = ncells or SOC0.shape[0]
+    with Context(rom, n, cfg, device) as ctx:
+        ctx.init_cells(SOC0, TC)
+        out = ctx.step(nsteps)
+        out["status"] = ctx.get_state()["status"]
+        return out
