@@ -42,7 +42,9 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds):
     bulk = 2 * 8 * NM * (20 + 6) + 2 * 8
     cell = 4 * 2 * 8 * 20 + 2 * 8 * ncon + 20 * 8 + 4 * 8 + 4 + 28 * 8 + (28 * 8 if bounds else 0)
     plant = 4 * 6 * 8 + 12 * 8 + 8
-    return dict(bulk=bulk, cell=cell, plant=plant)
+    # hild: problem record read (51 doubles), lambda read+written, outputs
+    hild = 51 * 8 + 2 * 8 * ncon + 4 * 8
+    return dict(bulk=bulk, cell=cell + 51 * 8, plant=plant, hild=hild)
 
 
 def batch_inputs(n, seed=0x5EED):
@@ -68,8 +70,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cells-per-gpu", type=int, default=65536)
     ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
-    ap.add_argument("--cpu-cells", type=int, default=8192)
-    ap.add_argument("--cpu-steps", type=int, default=300)
+    ap.add_argument("--cpu-cells", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -139,7 +141,8 @@ def main():
                 traffic = None
         cpu = None
         if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps, args.cpu_threads)
+            cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps or (W + K),
+                               args.cpu_threads)
         line = {
             "metric": METRIC,
             "value": value,

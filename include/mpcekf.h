@@ -178,10 +178,13 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
 /* ---- instrumentation (not part of the reference interface) ---- */
 /* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
  * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch
- * counts of [plant, bulk, cell] since the last call and resets them. */
+ * counts of [plant, bulk, cell, hild] (arrays of MPCEKF_NKERNELS) since the last
+ * call and resets them. */
 #define MPCEKF_K_PLANT 0
 #define MPCEKF_K_BULK 1
 #define MPCEKF_K_CELL 2
+#define MPCEKF_K_HILD 3
+#define MPCEKF_NKERNELS 4
 int mpcekf_set_timing(mpcekf_ctx *ctx, int32_t enable);
 int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
 

@@ -17,8 +17,10 @@ OUT = os.path.join(HERE, "_build")
 LIB = os.path.join(OUT, "libmpcekf.so")
 ARCH = os.environ.get("MPCEKF_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -pragma-unroll-threshold: the Hildreth sweep (23 x 23 guarded terms) must unroll
+# fully so the per-lane arrays stay in registers instead of scratch.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
-          "-Wno-unused-result"]
+          "-Wno-unused-result", "-mllvm", "-pragma-unroll-threshold=200000"]
 SOURCES = ["mpcekf_kernels.hip", "mpcekf_host.cpp"]
 DEPS = ["mpcekf_kernels.hpp", os.path.join("..", "..", "include", "mpcekf.h")]
 

@@ -66,7 +66,8 @@ struct mpcekf_ctx {
   double *d_cell_blob = nullptr, *d_plant_blob = nullptr, *d_bulk = nullptr;
   double *d_const = nullptr;  // 8 per-cell constant arrays
   double *d_scal = nullptr;   // 8 scalar state arrays + J_unc, J_fin
-  int *d_int = nullptr;       // warn, status, nviol
+  int *d_int = nullptr;       // warn, status, nviol, hflag
+  double *d_prob = nullptr;   // k_cell -> k_hild problem records
   double *d_zk = nullptr, *d_zbk = nullptr;
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
@@ -74,8 +75,8 @@ struct mpcekf_ctx {
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
   std::vector<hipEvent_t> ev;
-  double t_ms[3] = {0, 0, 0};
-  int64_t t_n[3] = {0, 0, 0};
+  double t_ms[4] = {0, 0, 0, 0};
+  int64_t t_n[4] = {0, 0, 0, 0};
   // electrode constants kept for per-cell initialisation (k0(T), Cdleff)
   double Tref = 0, Rgas = 0, th0[2] = {0, 0}, th100[2] = {0, 0}, k0ref[2] = {0, 0}, Ea[2] = {0, 0};
   double Cdl[2] = {0, 0}, wDL[2] = {0, 0}, nDL[2] = {0, 0};
@@ -377,7 +378,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.n = ncells;
   if ((rc = dalloc(&s.bigx, n * NM * 6)) || (rc = dalloc(&s.ekf, n * NM * REC)) ||
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
-      (rc = dalloc(&X->d_int, n * 3)) || (rc = dalloc(&X->d_const, n * 8)) ||
+      (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2)))) {
     mpcekf_ctx_destroy(X);
     return rc;
@@ -385,7 +386,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   double *sc = X->d_scal;
   s.SOCn = sc; s.SOCp = sc + n; s.x0 = sc + 2 * n; s.S0 = sc + 3 * n; s.priorI = sc + 4 * n;
   s.uk_1 = sc + 5 * n; s.uk = sc + 6 * n; s.vk = sc + 7 * n; s.J_unc = sc + 8 * n; s.J_fin = sc + 9 * n;
-  s.warn = X->d_int; s.status = X->d_int + n; s.nviol = X->d_int + 2 * n;
+  s.warn = X->d_int; s.status = X->d_int + n; s.nviol = X->d_int + 2 * n; s.hflag = X->d_int + 3 * n;
+  s.prob = X->d_prob;
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
   s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
@@ -398,7 +400,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   (void)hipSetDevice(X->device);
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
-  void *ptrs[] = {X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
+  void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -444,7 +446,7 @@ int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_de
   HIPCHK(hipMemcpyAsync(X->d_const, cst.data(), cst.size() * 8, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipMemsetAsync(X->s.lam, 0, n * X->ncon * 8, X->stream));
-  HIPCHK(hipMemsetAsync(X->d_int, 0, n * 3 * sizeof(int), X->stream));
+  HIPCHK(hipMemsetAsync(X->d_int, 0, n * 4 * sizeof(int), X->stream));
   int rc = launch_init_state(X->n, X->NM, X->s.ekf, X->s.bigx, X->cfg.SigmaX0, X->stream);
   if (rc) return fail(MPCEKF_E_HIP, "init kernel: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(hipStreamSynchronize(X->stream));
@@ -489,14 +491,14 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     if (traj_nexec) dnex = (int *)p;
   }
   const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
-  if (X->timing && X->ev.size() < (size_t)nsteps * 4) {
+  if (X->timing && X->ev.size() < (size_t)nsteps * 5) {
     size_t old = X->ev.size();
-    X->ev.resize((size_t)nsteps * 4);
+    X->ev.resize((size_t)nsteps * 5);
     for (size_t i = old; i < X->ev.size(); ++i) HIPCHK(hipEventCreate(&X->ev[i]));
   }
   for (int k = 0; k < nsteps; ++k) {
     const size_t o = (size_t)k * n;
-    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * 4] : nullptr;
+    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * 5] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
     if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, X->stream), "plant"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[1], X->stream));
@@ -513,6 +515,8 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.zbk = bounds ? X->d_zbk : nullptr;
     if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+    if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[4], X->stream));
   }
   if (!outputs_on_device) {
     for (int i = 0; i < 4; ++i)
@@ -522,9 +526,9 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
   HIPCHK(hipStreamSynchronize(X->stream));
   if (X->timing)
     for (int k = 0; k < nsteps; ++k)
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < 4; ++j) {
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * 4 + j], X->ev[(size_t)k * 4 + j + 1]));
+        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * 5 + j], X->ev[(size_t)k * 5 + j + 1]));
         X->t_ms[j] += ms;
         X->t_n[j] += 1;
       }
@@ -539,7 +543,7 @@ int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {
 
 int mpcekf_get_timing(mpcekf_ctx *X, double *ms_sum, int64_t *launches) {
   if (!X) return fail(MPCEKF_E_ARG, "null ctx");
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < 4; ++j) {
     if (ms_sum) ms_sum[j] = X->t_ms[j];
     if (launches) launches[j] = X->t_n[j];
     X->t_ms[j] = 0;
@@ -665,6 +669,7 @@ int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, doub
   io.uk_out = du;
   io.nexec = dn;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+  if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
   HIPCHK(hipMemcpyAsync(uk, du, n * 8, hipMemcpyDeviceToHost, X->stream));
   if (nexec) HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));

@@ -802,9 +802,42 @@ struct MpcOut {
   int nexec, nviol;
 };
 
-// iterMPC.m:17-95 (poles/sv diagnostics of :54-60 are out of scope)
-__device__ __forceinline__ void mpc_step(const KCfg &cf, const Lin &L, double &uk_1, double SOCk_1, double lam[NCON],
-                                         MpcOut &o) {
+// Hildreth problem record handed from k_cell to k_hild, SoA [field][cell].
+enum { PB_E = 0, PB_F = PB_E + NC * NC, PB_HV = PB_F + NC, PB_HE = PB_HV + NP, PB_HS = PB_HE + NP,
+       PB_GAM = PB_HS + NP, PB_ERR = PB_GAM + NCON, PB_RU = PB_ERR + NP, PB_UK1 = PB_RU + 1, PB_N = PB_UK1 + 1 };
+
+// iterMPC.m:50-51,85-86 cost J = ||e - G*DU||^2 + DU'*Ru*DU
+__device__ __forceinline__ double mpc_cost(const double Hs[NP], const double e[NP], double Ru, const double du[NC]) {
+  double J = 0.0, Jq = 0.0;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc = acc + (j <= i ? Hs[i - j] : 0.0) * du[j];
+    double rr = e[i] - acc;
+    J = J + rr * rr;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) acc = acc + (Ru * (c == k ? 1.0 : 0.0)) * du[k];
+    Jq = Jq + acc * du[c];
+  }
+  return J + Jq;
+}
+
+// iterMPC.m:17-66: predictions, adaptive Ru, unconstrained LS solve, constraint
+// stack and the violation test.  Returns true when hildreth.m must run.
+static_assert(PB_N == PROB_DOUBLES, "problem record size");
+
+struct MpcSetup {
+  Cons Cn;
+  double E[NC][NC], F[NC], e[NP], Ru, DU[NC];
+};
+
+__device__ __forceinline__ bool mpc_setup(const KCfg &cf, const Lin &L, double uk_1, double SOCk_1, MpcSetup &P,
+                                          MpcOut &o) {
   double dx[NA];
 #pragma unroll
   for (int k = 0; k < 6; ++k) dx[k] = L.xhat[k];
@@ -814,26 +847,19 @@ __device__ __forceinline__ void mpc_step(const KCfg &cf, const Lin &L, double &u
   for (int k = 0; k < 6; ++k) Cb[k] = L.Csoc[k];
   Cb[6] = L.Dsoc;
   predmat_s(L.a, Cb, Phis, Hs);
-  double Gs[NP][NC];
-#pragma unroll
-  for (int i = 0; i < NP; ++i)
-#pragma unroll
-    for (int j = 0; j < NC; ++j) Gs[i][j] = j <= i ? Hs[i - j] : 0.0;
-  double e[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < NA; ++k) acc = acc + Phis[i][k] * dx[k];
-    e[i] = cf.ref * 1.0 - acc;
+    P.e[i] = cf.ref * 1.0 - acc;
   }
-  double F[NC];
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
     double acc = 0.0;
 #pragma unroll
-    for (int i = 0; i < NP; ++i) acc = acc + (-2 * Gs[i][j]) * e[i];
-    F[j] = acc;
+    for (int i = 0; i < NP; ++i) acc = acc + (-2 * (j <= i ? Hs[i - j] : 0.0)) * P.e[i];
+    P.F[j] = acc;
   }
   double GtG[NC][NC];
 #pragma unroll
@@ -842,61 +868,45 @@ __device__ __forceinline__ void mpc_step(const KCfg &cf, const Lin &L, double &u
     for (int b = 0; b < NC; ++b) {
       double acc = 0.0;
 #pragma unroll
-      for (int i = 0; i < NP; ++i) acc = acc + Gs[i][a] * Gs[i][b];
+      for (int i = 0; i < NP; ++i) acc = acc + (a <= i ? Hs[i - a] : 0.0) * (b <= i ? Hs[i - b] : 0.0);
       GtG[a][b] = acc;
     }
   double smin = sigma_min_n<NC>(GtG);
   double nF = 0.0;
 #pragma unroll
-  for (int j = 0; j < NC; ++j) nF = nF + F[j] * F[j];
+  for (int j = 0; j < NC; ++j) nF = nF + P.F[j] * P.F[j];
   nF = sqrt(nF);
-  double Ru = (nF / (2 * cf.du_max * sqrt((double)NC))) - smin;
-  double E[NC][NC], mE[NC][NC];
+  P.Ru = (nF / (2 * cf.du_max * sqrt((double)NC))) - smin;
+  double mE[NC][NC];
 #pragma unroll
   for (int a = 0; a < NC; ++a)
 #pragma unroll
     for (int b = 0; b < NC; ++b) {
-      E[a][b] = 2 * (GtG[a][b] + Ru * (a == b ? 1.0 : 0.0));
-      mE[a][b] = -E[a][b];
+      P.E[a][b] = 2 * (GtG[a][b] + P.Ru * (a == b ? 1.0 : 0.0));
+      mE[a][b] = -P.E[a][b];
     }
-  double DU[NC];
-  lu_solve_n<NC>(mE, F, DU);
-  auto cost = [&](const double du[NC]) {
-    double J = 0.0, Jq = 0.0;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < NC; ++j) acc = acc + Gs[i][j] * du[j];
-      double rr = e[i] - acc;
-      J = J + rr * rr;
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < NC; ++k) acc = acc + (Ru * (c == k ? 1.0 : 0.0)) * du[k];
-      Jq = Jq + acc * du[c];
-    }
-    return J + Jq;
-  };
-  o.J_unc = cost(DU);
-  Cons Cn;
-  constraints_s(cf, L, dx, uk_1, SOCk_1, Phis, Hs, Cn);
-  ConsM Mf{Cn};
+  lu_solve_n<NC>(mE, P.F, P.DU);
+  o.J_unc = mpc_cost(Hs, P.e, P.Ru, P.DU);
+  constraints_s(cf, L, dx, uk_1, SOCk_1, Phis, Hs, P.Cn);
+  ConsM Mf{P.Cn};
   int nv = 0;
 #pragma unroll
   for (int i = 0; i < NCON; ++i) {
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc = acc + Mf(i, j) * DU[j];
-    if (acc - Cn.gam[i] > 0) nv++;
+    for (int j = 0; j < NC; ++j) acc = acc + Mf(i, j) * P.DU[j];
+    if (acc - P.Cn.gam[i] > 0) nv++;
   }
-  o.nexec = 0;
-  if (nv > 0) o.nexec = hildreth_core(Mf, E, F, Cn.gam, lam, cf.max_hild, cf.hild_tol, DU);
+  return nv > 0;
+}
+
+// iterMPC.m:75-95 after the (optional) Hildreth solve
+__device__ __forceinline__ void mpc_finish(const Cons &Cn, const double e[NP], double Ru, const double DU[NC],
+                                           double &uk_1, MpcOut &o) {
   double uk = DU[0] + uk_1;
   uk_1 = uk;
   o.uk = uk;
+  ConsM Mf{Cn};
   int nviol = 0;
 #pragma unroll
   for (int i = 0; i < NCON; ++i) {
@@ -906,7 +916,122 @@ __device__ __forceinline__ void mpc_step(const KCfg &cf, const Lin &L, double &u
     if (acc - Cn.gam[i] > 1e-9) nviol++;
   }
   o.nviol = nviol;
-  o.J_fin = cost(DU);
+  o.J_fin = mpc_cost(Cn.Hs, e, Ru, DU);
+}
+
+// hildreth.m:17-46 in the exact dense summation order, skipping only the terms
+// H(i,j)*lambda(j) whose lambda(j) is +0 in every lane of the wave: such a term
+// is +-0 when H(i,j) is finite, and adding +-0 to the running sum (which starts
+// at +0 and so can never be -0) leaves it bit-identical.  If any lane has a
+// non-finite M or X entry the wave keeps every term (dense order, as hildreth.m).
+//
+// X = E\M' is kept for the 15 Toeplitz rows plus three solves for the constant
+// current rows: X(-b) = -X(b) exactly under round-to-nearest; the sign of a
+// zero in those X entries cannot reach the sweep (it only feeds products whose
+// sum is added to a never -0 running sum, and their diagonal H_ii = E^-1_00 > 0).
+struct XS {
+  double a[NC], b[NC], c[NC];        // E\[1;0], E\[1;1], E\[0;1]
+  double t[3 * NP][NC];              // E\M(i,:)' for the V / eta / SOC rows
+};
+__device__ __forceinline__ double xval(const XS &X, int j, int k) {
+  switch (j) {  // rows of [Cu; -Cu; I; -I] for NC == 2
+    case 0: return X.a[k];
+    case 1: return X.b[k];
+    case 2: return -X.a[k];
+    case 3: return -X.b[k];
+    case 4: return X.a[k];
+    case 5: return X.c[k];
+    case 6: return -X.a[k];
+    case 7: return -X.c[k];
+    default: return X.t[j - 4 * NC][k];
+  }
+}
+
+// Register-resident sweep (rows and columns unrolled at compile time, so lambda,
+// K and X never leave VGPRs).  Two exact shortcuts keep the per-sweep latency
+// down once most lanes of a wave have converged:
+//  * the column skip mask and the dense flag are rebuilt at the start of every
+//    sweep from the lanes still iterating (a converged lane is masked off and no
+//    longer forces its own active columns on the others);
+//  * the division of row i is skipped when, in every live lane, lambda(i) == +0,
+//    H(i,i) > 0 and K(i) + s >= 0 (or NaN): then w = -(K(i)+s)/H(i,i) <= 0 and
+//    max(0, w) = +0 exactly, as hildreth.m:37-39 would produce.
+__device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
+                                              double tol, const double K[NCON], double Mtl[NC]) {
+  static_assert(NC == 2, "written for Nc = 2");
+  ConsM Mf{Cn};
+  double R[NC][NC];
+  bool ok = chol_n<NC>(E, R);
+  XS Xs;
+  {
+    double b1[NC] = {1.0, 0.0}, b2[NC] = {1.0, 1.0}, b3[NC] = {0.0, 1.0};
+    mldiv_spd<NC>(E, R, ok, b1, Xs.a);
+    mldiv_spd<NC>(E, R, ok, b2, Xs.b);
+    mldiv_spd<NC>(E, R, ok, b3, Xs.c);
+  }
+#pragma unroll
+  for (int i = 4 * NC; i < NCON; ++i) {
+    double b[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) b[k] = Mf(i, k);
+    mldiv_spd<NC>(E, R, ok, b, Xs.t[i - 4 * NC]);
+  }
+  bool fin = true;
+#pragma unroll
+  for (int j = 0; j < NCON; ++j)
+    fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
+  int it;
+#pragma unroll 1
+  for (it = 1; it <= maxIter; ++it) {
+    // opaque per sweep: stops the 23 x 23 entries of H being hoisted (and spilled)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      launder(Xs.a[k]); launder(Xs.b[k]); launder(Xs.c[k]);
+#pragma unroll
+      for (int i = 0; i < 3 * NP; ++i) launder(Xs.t[i][k]);
+    }
+    unsigned amask = 0;
+#pragma unroll
+    for (int j = 0; j < NCON; ++j)
+      if (__any(L[j] != 0.0)) amask |= 1u << j;
+    if (__any(!fin)) amask = (1u << NCON) - 1;
+    bool conv = true;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) {
+      const double m0 = Mf(i, 0), m1 = Mf(i, 1);
+      const double hii = (0.0 + m0 * xval(Xs, i, 0)) + m1 * xval(Xs, i, 1);
+      double s = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCON; ++j) {
+        if (amask & (1u << j)) {
+          asm volatile("" ::: "memory");  // keep the skip a real (uniform) branch, not a select
+          double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
+          s = s + h * L[j];
+        }
+      }
+      const double ks = K[i] + s;
+      const double li = L[i];
+      double nl = 0.0;
+      if (__any(!(li == 0.0 && hii > 0.0 && !(ks < 0.0)))) {
+        asm volatile("" ::: "memory");
+        double w = -(ks - hii * li) / hii;
+        nl = w > 0 ? w : 0.0;
+      }
+      if (!(fabs(nl - li) < tol)) conv = false;
+      L[i] = nl;
+      if (__any(nl != 0.0)) amask |= 1u << i;
+    }
+    if (conv) break;
+  }
+  if (it > maxIter) it = maxIter;
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) s = s + Mf(i, k) * L[i];
+    Mtl[k] = s;  // M'*lambda; the caller adds F and solves -E\(.)
+  }
+  return it;
 }
 
 // ---------------------------------------------------------------------------
@@ -1075,6 +1200,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   cc.k0p = s.k0p[c];
   int st = s.status[c];
   const bool fused = io.mode & MODE_FUSED;
+  if (io.mode & (MODE_MPC | MODE_FUSED)) s.hflag[c] = 0;  // set again only if hildreth.m must run
 
   auto fail_outputs = [&]() {
     if (io.u) io.u[c] = NaN;
@@ -1306,9 +1432,6 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       lin_load(io.lin_in + c * 35, L);
       Zsoc = io.soc_k1_in[c];
     }
-    double lam[NCON];
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * s.n + c];
     double uk_1 = s.uk_1[c];
     double ukin = fused ? s.uk[c] : 0.0;
     double phise = 0.0;
@@ -1319,24 +1442,127 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       phise = acc + ukin * L.Dphi + L.bphi;  // runMPC.m:94-95
     }
     MpcOut o;
-    mpc_step(cf, L, uk_1, Zsoc, lam, o);
-    s.uk_1[c] = uk_1;
-    if (o.nexec > 0) {
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * s.n + c] = lam[i];  // iterMPC.m:68
-    }
-    if (s.J_unc) { s.J_unc[c] = o.J_unc; s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
-    if (io.uk_out) io.uk_out[c] = o.uk;
-    if (io.nexec) io.nexec[c] = o.nexec;
+    MpcSetup Pm;
+    bool need = mpc_setup(cf, L, uk_1, Zsoc, Pm, o);
     if (fused) {
-      s.uk[c] = o.uk;
-      if (io.u) io.u[c] = o.uk;
       if (io.v) io.v[c] = vk;
       if (io.soc) io.soc[c] = Zsoc;
       if (io.phise) io.phise[c] = phise;
     }
+    if (s.J_unc) s.J_unc[c] = o.J_unc;
+    s.hflag[c] = need ? 1 : 0;
+    if (need) {  // hildreth.m runs in k_hild
+      double *pb = s.prob;
+      const int64_t n = s.n;
+#pragma unroll
+      for (int a = 0; a < NC; ++a) {
+        pb[(PB_F + a) * n + c] = Pm.F[a];
+#pragma unroll
+        for (int b = 0; b < NC; ++b) pb[(PB_E + a * NC + b) * n + c] = Pm.E[a][b];
+      }
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        pb[(PB_HV + i) * n + c] = Pm.Cn.Hv[i];
+        pb[(PB_HE + i) * n + c] = Pm.Cn.He[i];
+        pb[(PB_HS + i) * n + c] = Pm.Cn.Hs[i];
+        pb[(PB_ERR + i) * n + c] = Pm.e[i];
+      }
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) pb[(PB_GAM + i) * n + c] = Pm.Cn.gam[i];
+      pb[PB_RU * n + c] = Pm.Ru;
+      pb[PB_UK1 * n + c] = uk_1;
+    } else {
+      o.nexec = 0;
+      mpc_finish(Pm.Cn, Pm.e, Pm.Ru, Pm.DU, uk_1, o);
+      s.uk_1[c] = uk_1;
+      if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
+      if (io.uk_out) io.uk_out[c] = o.uk;
+      if (io.nexec) io.nexec[c] = 0;
+      if (fused) {
+        s.uk[c] = o.uk;
+        if (io.u) io.u[c] = o.uk;
+      }
+    }
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_hild: hildreth.m + iterMPC.m:68-95 for the cells k_cell flagged
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  if (!s.hflag[c]) return;
+  const int64_t n = s.n;
+  const double *pb = s.prob;
+  Cons Cn;
+  double E[NC][NC], F[NC], K[NCON];
+  {
+    double y[NC], R[NC][NC];
+#pragma unroll
+    for (int a = 0; a < NC; ++a) {
+      F[a] = pb[(PB_F + a) * n + c];
+#pragma unroll
+      for (int b = 0; b < NC; ++b) E[a][b] = pb[(PB_E + a * NC + b) * n + c];
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      Cn.Hv[i] = pb[(PB_HV + i) * n + c];
+      Cn.He[i] = pb[(PB_HE + i) * n + c];
+      Cn.Hs[i] = pb[(PB_HS + i) * n + c];
+    }
+    bool ok = chol_n<NC>(E, R);
+    mldiv_spd<NC>(E, R, ok, F, y);
+    ConsM Mf{Cn};
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) sum = sum + Mf(i, k) * y[k];
+      K[i] = sum + pb[(PB_GAM + i) * n + c];  // K = M*(E\F) + gamma (hildreth.m:29)
+    }
+  }
+  double lam[NCON];
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+  double Mtl[NC];
+  MpcOut o;
+  o.nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
+  // DU = -E\(F + M'*lambda) (hildreth.m:46); operands re-read after the sweeps
+  const double *pb2 = pb;
+  asm volatile("" : "+v"(pb2));
+  MpcSetup P;
+  double rhs[NC], mE[NC][NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) {
+    rhs[a] = pb2[(PB_F + a) * n + c] + Mtl[a];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) mE[a][b] = -pb2[(PB_E + a * NC + b) * n + c];
+  }
+  lu_solve_n<NC>(mE, rhs, P.DU);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    P.e[i] = pb2[(PB_ERR + i) * n + c];
+    P.Cn.Hv[i] = Cn.Hv[i];
+    P.Cn.He[i] = Cn.He[i];
+    P.Cn.Hs[i] = Cn.Hs[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) P.Cn.gam[i] = pb2[(PB_GAM + i) * n + c];
+  P.Ru = pb2[PB_RU * n + c];
+  double uk_1 = pb2[PB_UK1 * n + c];
+  mpc_finish(P.Cn, P.e, P.Ru, P.DU, uk_1, o);
+  s.uk_1[c] = uk_1;
+  if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
+  if (io.uk_out) io.uk_out[c] = o.uk;
+  if (io.nexec) io.nexec[c] = o.nexec;
+  if (io.mode & MODE_FUSED) {
+    s.uk[c] = o.uk;
+    if (io.u) io.u[c] = o.uk;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1483,6 +1709,12 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
     case 32: launch_cell_t<32>(r, c, s, io, st); break;
     default: return -1;
   }
+  return (int)hipGetLastError();
+}
+
+int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
+  if (s.n == 0) return 0;
+  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, c, s, io);
   return (int)hipGetLastError();
 }
 

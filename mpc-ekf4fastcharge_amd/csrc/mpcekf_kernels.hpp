@@ -57,6 +57,9 @@ struct KState {
   // diagnostics of the last MPC step
   double *J_unc, *J_fin;
   int *nviol;
+  // hand-off k_cell -> k_hild
+  int *hflag;      // [n] 1: hildreth.m must run this step
+  double *prob;    // [PB_N][n] problem records (mpcekf_kernels.hip PB_*)
 };
 
 // Inputs/outputs of one cell-kernel launch.  Any pointer may be null.
@@ -82,6 +85,8 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
 int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream);
+int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream);
+constexpr int PROB_DOUBLES = 51;  // PB_N for Np = 5, Nc = 2
 int launch_predmat(int64_t n, int Np, int Nc, const double *a, const double *C, const double *D, double *Phi,
                    double *G, void *stream);
 int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double *uk_1, const double *soc_k1,

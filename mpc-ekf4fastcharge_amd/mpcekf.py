@@ -155,10 +155,10 @@ class Context:
 
     def get_timing(self):
         """{kernel: (ms_sum, launches)} since the last call (HIP events on the ctx stream)."""
-        ms = np.zeros(3)
-        nl = (C.c_int64 * 3)()
+        ms = np.zeros(4)
+        nl = (C.c_int64 * 4)()
         check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
-        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell"))}
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell", "hild"))}
 
     def get_zk(self):
         zk = np.empty((self.n, self.nz + 2))

@@ -130,3 +130,58 @@ def test_full_size_properties(rom, M):
     part = M.runMPC(rom, soc0[sl], tc[sl], steps)
     for k in ("u", "v", "soc", "phise"):
         np.testing.assert_array_equal(part[k], out[k][:, sl])
+
+
+def _golden(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+
+
+@pytest.mark.parametrize("fixture,romkw,rtol", [
+    ("batch8_200", {}, 1e-9),
+    ("rom_nt1_200", dict(T_degC=(25.0,)), 1e-9),
+    ("edge_cells_400", {}, 1e-8),
+])
+def test_gpu_matches_golden_fixtures(P, M, fixture, romkw, rtol):
+    """Against the MATLAB-faithful numpy restatement (tests/golden, tools/make_golden.py)."""
+    g = _golden(fixture)
+    rom = P.make_synth_rom(**romkw)
+    out = M.runMPC(rom, g["soc0"], g["tc"], g["u"].shape[0])
+    np.testing.assert_array_equal(out["status"], g["status"])
+    for k in ("u", "v", "soc", "phise"):
+        assert _rel(out[k], g[k]).max() <= rtol, k
+    np.testing.assert_array_equal(out["nexec"], g["nexec"])
+
+
+def test_zk_and_boundzk_match_oracle(rom, oc, M):
+    n, steps = 40, 60
+    soc0, tc = batch_inputs(n, seed=11)
+    ref = oc.run(rom, soc0, tc, steps, nthreads=4, want_zk=True)
+    cfg = M.make_config(bounds=True)
+    with M.Context(rom, n, cfg) as ctx:
+        ctx.init_cells(soc0, tc)
+        ctx.step(steps)
+        zk, zb = ctx.get_zk()
+    assert _rel(zk, ref["zk"]).max() <= RTOL_TIGHT
+    assert _rel(zb, ref["zbk"]).max() <= RTOL_TIGHT
+
+
+def test_checkpoint_restore_is_exact(rom, M):
+    n = 2048
+    soc0, tc = batch_inputs(n, seed=5)
+    with M.Context(rom, n) as ctx:
+        ctx.init_cells(soc0, tc)
+        ctx.step(15)
+        snap = ctx.get_state()
+        a = ctx.step(25)
+        ctx.set_state(snap)
+        b = ctx.step(25)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_runmpc_cell_prefix_matches_golden(rom, M):
+    g = _golden("runmpc_soc10_tc25")
+    out = M.runMPC(rom, g["soc0"], g["tc"], 3001)
+    for k in ("u", "v", "soc", "phise"):
+        assert _rel(out[k][:2400], g[k][:2400]).max() <= 1e-9, k

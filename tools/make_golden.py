@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Generates tests/golden/*.npz with the numpy oracle (oracle/oracle_np.py).
+
+The reference itself cannot run here (MATLAB, missing ROM), so
+these vectors come from the MATLAB-faithful numpy restatement on the synthetic
+ROM.  They pin the C oracle and the kernels to that restatement (parity with the
+MATLAB reference stays unpinned).  Re-run only when the oracle or ROM generator
+changes:  python tools/make_golden.py
+"""
+import hashlib
+import importlib
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle_np as O  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def rom_hash(rom):
+    h = hashlib.sha256()
+    for k, v in sorted(rom.to_npz_dict().items()):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()
+
+
+def run_cells(rom, soc0, tc, steps):
+    outs = [O.run_cell(rom, s, t, steps) for s, t in zip(soc0, tc)]
+    res = {k: np.stack([o[k] for o in outs], axis=1) for k in ("u", "v", "soc", "phise", "nexec")}
+    res["status"] = np.array([o["status"][-1] for o in outs])
+    res["zk_last"] = np.stack([o["zk"][-1] for o in outs])
+    res["zbk_last"] = np.stack([o["zbk"][-1] for o in outs])
+    return res
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    rom = P.make_synth_rom()
+    hsh = rom_hash(rom)
+    t0 = time.time()
+    # 1. the runMPC.m cell: SOC0 = 10 %, TC = 25 degC, 3001 steps (runMPC.m:8-13)
+    r = run_cells(rom, [10.0], [25.0], 3001)
+    np.savez_compressed(os.path.join(OUT, "runmpc_soc10_tc25.npz"), rom_hash=hsh, soc0=[10.0], tc=[25.0], **r)
+    # 2. eight cells of the batched workload, 200 steps
+    rng = np.random.Generator(np.random.PCG64(0x5EED))
+    soc0, tc = rng.uniform(5, 30, 8), rng.uniform(20, 30, 8)
+    r = run_cells(rom, soc0, tc, 200)
+    np.savez_compressed(os.path.join(OUT, "batch8_200.npz"), rom_hash=hsh, soc0=soc0, tc=tc, **r)
+    # 3. edge cells: thetae < 0 error (SOC0 130 %), EKF lock-out (SOC0 -15 %: warnCount > 10),
+    #    near target (88 %: voltage limit + Hildreth maxIter), exact set-point temperatures
+    #    (15 / 35 degC) and a set-point SOC (25 %)
+    soc0 = np.array([130.0, 88.0, 25.0, 60.0, 5.0, -15.0])
+    tc = np.array([25.0, 30.0, 15.0, 35.0, 25.0, 25.0])
+    r = run_cells(rom, soc0, tc, 400)
+    np.savez_compressed(os.path.join(OUT, "edge_cells_400.npz"), rom_hash=hsh, soc0=soc0, tc=tc, **r)
+    # 4. single-temperature ROM (nT = 1: the single-setpoint branches of getXind/OB_step)
+    rom1 = P.make_synth_rom(T_degC=(25.0,))
+    r = run_cells(rom1, [12.0, 40.0], [25.0, 22.0], 200)
+    np.savez_compressed(os.path.join(OUT, "rom_nt1_200.npz"), rom_hash=rom_hash(rom1), soc0=[12.0, 40.0],
+                        tc=[25.0, 22.0], **r)
+    # 5. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
+    rng = np.random.default_rng(11)
+    n = 24
+    a = np.concatenate([rng.uniform(0.2, 0.999, (n, 5)), np.ones((n, 1))], 1)
+    Cr = np.concatenate([rng.normal(0, 1e-3, (n, 5)), rng.normal(0, 1e-5, (n, 1))], 1)
+    D = rng.normal(0, 1e-3, n)
+    Phi = np.zeros((n, 5, 7))
+    G = np.zeros((n, 5, 2))
+    for i in range(n):
+        Phi[i], G[i] = O.pred_mat(a[i], Cr[i], D[i], 5, 2)
+    E = np.zeros((n, 2, 2))
+    F = rng.normal(0, 1, (n, 2))
+    M = rng.normal(0, 1, (n, 23, 2))
+    gam = rng.normal(0.5, 1.0, (n, 23))
+    M[:, 18, :] = 0.0                           # G_soc row 1 is identically zero
+    gam[: n // 2, 18] = np.abs(gam[: n // 2, 18]) + 0.1   # gamma > 0: lambda stays 0
+    gam[n // 2:, 18] = -np.abs(gam[n // 2:, 18]) - 0.1    # gamma < 0: inf/NaN period-2 pattern
+    lam0 = np.abs(rng.normal(0, 0.1, (n, 23)))
+    DU = np.zeros((n, 2))
+    lam = np.zeros((n, 23))
+    nexec = np.zeros(n, dtype=np.int64)
+    with np.errstate(all="ignore"):
+        for i in range(n):
+            A = rng.normal(0, 1, (2, 2))
+            E[i] = A @ A.T + 0.5 * np.eye(2)
+            E[i] = (E[i] + E[i].T) / 2
+            DU[i], lam[i], nexec[i] = O.hildreth(E[i], F[i], M[i], gam[i], lam0[i].copy(), 100)
+    np.savez_compressed(os.path.join(OUT, "functions.npz"), a=a, C=Cr, D=D, Phi=Phi, G=G, E=E, F=F, M=M,
+                        gamma=gam, lam0=lam0, DU=DU, lam=lam, nexec=nexec)
+    print(f"golden fixtures written to {OUT} in {time.time() - t0:.0f} s (rom {hsh[:12]})")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Reduce rocprofv3 PMC CSVs to per-launch HBM bytes for each bench kernel.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
+exactly half the bytes of a wide (16 B/lane) coalesced streaming read
+(MI355X_MICROARCH.md §HBM), so reads are doubled; WRITE_SIZE is exact for
+16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,bulk,cell}.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {"k_plant": "plant", "k_bulk": "bulk", "k_cell": "cell"}
+
+
+def read_counter(d, name):
+    vals = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != name:
+                    continue
+                kn = row.get("Kernel_Name", "")
+                for k, short in KERNELS.items():
+                    if k in kn:
+                        vals[short].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items() if v}
+
+
+def main():
+    base = sys.argv[1]
+    fetch = read_counter(os.path.join(base, "fetch"), "FETCH_SIZE")
+    write = read_counter(os.path.join(base, "write"), "WRITE_SIZE")
+    out = {"unit": "bytes per launch", "fetch_kib_raw": fetch, "write_kib_raw": write,
+           "correction": "reads x2 (gfx950 FETCH_SIZE halves 16-B/lane streaming reads)",
+           "per_launch_bytes": {}}
+    for k in set(fetch) | set(write):
+        out["per_launch_bytes"][k] = 2 * fetch.get(k, 0.0) * 1024 + write.get(k, 0.0) * 1024
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,17 @@
+#!/bin/bash
+# rocprofv3 evidence for the bench: kernel trace + stats, then one PMC pass per
+# counter (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass; MI355X_MICROARCH.md).
+# Usage (on the GPU box): bash tools/profile.sh TAG
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-r01}
+O=gpurun_out/prof_$TAG
+mkdir -p $O
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- \
+  python3 bench.py --steps 100 --warmup 5 --no-cpu > $O/bench_under_trace.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o run -- \
+  python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_fetch.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o run -- \
+  python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_write.log 2>&1 && \
+python3 tools/pmc_traffic.py $O > $O/pmc_traffic.json
