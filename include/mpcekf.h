@@ -187,6 +187,12 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
 #define MPCEKF_NKERNELS 4
 int mpcekf_set_timing(mpcekf_ctx *ctx, int32_t enable);
 int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
+/* The Hildreth problem records of the last fused step, as k_cell left them for
+ * k_hild (field-major [MPCEKF_PROB_DOUBLES][ncells]: E(2x2) F(2) Hv(5) He(5) Hs(5)
+ * gamma(23) e(5) Ru uk_1), and hflag [ncells] (1 = the QP ran).  For replaying the
+ * solver offline (tools/micro); either pointer may be NULL. */
+#define MPCEKF_PROB_DOUBLES 51
+int mpcekf_get_hild_problems(mpcekf_ctx *ctx, double *prob, int32_t *hflag);
 
 /* ---- state access (open-loop parity, checkpoint/restore) ---- */
 typedef struct {

@@ -769,6 +769,17 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
   return MPCEKF_OK;
 }
 
+int mpcekf_get_hild_problems(mpcekf_ctx *X, double *prob, int32_t *hflag) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  static_assert(MPCEKF_PROB_DOUBLES == PROB_DOUBLES, "problem record size");
+  const size_t n = (size_t)X->n;
+  if (prob) HIPCHK(hipMemcpyAsync(prob, X->s.prob, n * PROB_DOUBLES * 8, hipMemcpyDeviceToHost, X->stream));
+  if (hflag) HIPCHK(hipMemcpyAsync(hflag, X->s.hflag, n * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
 // ---- state access ------------------------------------------------------------
 static const int kScalMap[MPCEKF_NSCAL] = {0, 1, 2, 3, 4, 5, 6, 7};  // MPCEKF_S_* -> d_scal slot
 

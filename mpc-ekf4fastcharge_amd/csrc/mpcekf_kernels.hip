@@ -947,17 +947,42 @@ __device__ __forceinline__ double xval(const XS &X, int j, int k) {
   }
 }
 
-// Register-resident sweep (rows and columns unrolled at compile time, so lambda,
-// K and X never leave VGPRs).  Two exact shortcuts keep the per-sweep latency
-// down once most lanes of a wave have converged:
-//  * the column skip mask and the dense flag are rebuilt at the start of every
-//    sweep from the lanes still iterating (a converged lane is masked off and no
-//    longer forces its own active columns on the others);
-//  * the division of row i is skipped when, in every live lane, lambda(i) == +0,
-//    H(i,i) > 0 and K(i) + s >= 0 (or NaN): then w = -(K(i)+s)/H(i,i) <= 0 and
-//    max(0, w) = +0 exactly, as hildreth.m:37-39 would produce.
+// h(i,j) = M(i,:)*X(:,j) when every operand is finite, exact up to the sign of
+// a zero result: the dense form (0 + m0*x0) + m1*x1 differs from these only
+// when a partial result is a signed zero.  A zero h(i,j) only ever feeds
+// h(i,j)*lambda(j) (+-0, or NaN for lambda = inf either way) added to a running
+// sum that starts at +0 and so is never -0: the sum is bit-identical.
+__device__ __forceinline__ double hfast(const Cons &C, int i, double x0, double x1) {
+  switch (i) {  // the constant rows [Cu; -Cu; I; -I] for NC == 2
+    case 0: case 4: return x0;
+    case 1: return x0 + x1;
+    case 2: case 6: return -x0;
+    case 3: return -(x0 + x1);
+    case 5: return x1;
+    case 7: return -x1;
+    default: break;
+  }
+  const int r = (i - 4 * NC) % NP;  // Toeplitz row r of G_v / -G_e / G_soc: M(i,2) == +-0 when r == 0
+  if (r == 0) return mval(C, i, 0) * x0;
+  return mval(C, i, 0) * x0 + mval(C, i, 1) * x1;
+}
+
+// Register-resident sweep, rows and columns unrolled at compile time so lambda,
+// K and X never leave VGPRs, and straight-line (no per-term branches: a
+// wave-uniform skip test costs more than the two DP ops it saves).  Every term
+// H(i,j)*lambda(j) is kept, in the order of hildreth.m:35; while every live
+// lane of the wave is finite, H(i,j) is formed by hfast (for the constant
+// columns +-E\[1;0], +-E\[1;1], +-E\[0;1] only three values per row, negated
+// exactly); a wave holding a non-finite lane uses the dense formula.
+//
+// A lane that has converged stays in the loop with its lambda and sweep count
+// frozen (selects, not a per-lane exit) until the whole wave is done: on MI355X a
+// wave whose EXEC holds fewer than 16 lanes issues FP64 VALU up to 2.6x slower
+// under full-chip load (tools/micro/exec_micro.hip), and Hildreth's convergence
+// is very uneven across cells.  `done` = true makes a lane a passenger from the
+// start (no QP this step: its operands are a finite dummy and nothing is kept).
 __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
-                                              double tol, const double K[NCON], double Mtl[NC]) {
+                                              double tol, const double K[NCON], double Mtl[NC], bool done) {
   static_assert(NC == 2, "written for Nc = 2");
   ConsM Mf{Cn};
   double R[NC][NC];
@@ -980,50 +1005,61 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
 #pragma unroll
   for (int j = 0; j < NCON; ++j)
     fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
-  int it;
+  int nexec = maxIter;
 #pragma unroll 1
-  for (it = 1; it <= maxIter; ++it) {
-    // opaque per sweep: stops the 23 x 23 entries of H being hoisted (and spilled)
+  for (int it = 1; it <= maxIter; ++it) {
+    if (__all(done)) break;
+    // opaque per sweep: stops the entries of H being hoisted out of the loop (and spilled)
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       launder(Xs.a[k]); launder(Xs.b[k]); launder(Xs.c[k]);
 #pragma unroll
       for (int i = 0; i < 3 * NP; ++i) launder(Xs.t[i][k]);
     }
-    unsigned amask = 0;
-#pragma unroll
-    for (int j = 0; j < NCON; ++j)
-      if (__any(L[j] != 0.0)) amask |= 1u << j;
-    if (__any(!fin)) amask = (1u << NCON) - 1;
     bool conv = true;
+    if (__all(fin || done)) {
 #pragma unroll
-    for (int i = 0; i < NCON; ++i) {
-      const double m0 = Mf(i, 0), m1 = Mf(i, 1);
-      const double hii = (0.0 + m0 * xval(Xs, i, 0)) + m1 * xval(Xs, i, 1);
-      double s = 0.0;
+      for (int i = 0; i < NCON; ++i) {
+        const double hii = (0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1);
+        const double ha = hfast(Cn, i, Xs.a[0], Xs.a[1]);
+        const double hb = hfast(Cn, i, Xs.b[0], Xs.b[1]);
+        const double hc = hfast(Cn, i, Xs.c[0], Xs.c[1]);
+        const double hconst[4 * NC] = {ha, hb, -ha, -hb, ha, hc, -ha, -hc};
+        double s = 0.0;
 #pragma unroll
-      for (int j = 0; j < NCON; ++j) {
-        if (amask & (1u << j)) {
-          asm volatile("" ::: "memory");  // keep the skip a real (uniform) branch, not a select
-          double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
+        for (int j = 0; j < NCON; ++j) {
+          const double h = j < 4 * NC ? hconst[j] : hfast(Cn, i, Xs.t[j - 4 * NC][0], Xs.t[j - 4 * NC][1]);
           s = s + h * L[j];
         }
+        const double li = L[i];
+        const double w = -((K[i] + s) - hii * li) / hii;
+        const double nl = w > 0 ? w : 0.0;
+        if (!(fabs(nl - li) < tol)) conv = false;
+        L[i] = done ? li : nl;
       }
-      const double ks = K[i] + s;
-      const double li = L[i];
-      double nl = 0.0;
-      if (__any(!(li == 0.0 && hii > 0.0 && !(ks < 0.0)))) {
-        asm volatile("" ::: "memory");
-        double w = -(ks - hii * li) / hii;
-        nl = w > 0 ? w : 0.0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) {
+        const double m0 = Mf(i, 0), m1 = Mf(i, 1);
+        double s = 0.0, hii = 0.0;
+#pragma unroll
+        for (int j = 0; j < NCON; ++j) {
+          const double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
+          if (j == i) hii = h;
+          s = s + h * L[j];
+        }
+        const double li = L[i];
+        const double w = -((K[i] + s) - hii * li) / hii;
+        const double nl = w > 0 ? w : 0.0;
+        if (!(fabs(nl - li) < tol)) conv = false;
+        L[i] = done ? li : nl;
       }
-      if (!(fabs(nl - li) < tol)) conv = false;
-      L[i] = nl;
-      if (__any(nl != 0.0)) amask |= 1u << i;
     }
-    if (conv) break;
+    if (!done && conv) {
+      done = true;
+      nexec = it;
+    }
   }
-  if (it > maxIter) it = maxIter;
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
     double s = 0.0;
@@ -1031,7 +1067,7 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
     for (int i = 0; i < NCON; ++i) s = s + Mf(i, k) * L[i];
     Mtl[k] = s;  // M'*lambda; the caller adds F and solves -E\(.)
   }
-  return it;
+  return nexec;
 }
 
 // ---------------------------------------------------------------------------
@@ -1493,12 +1529,26 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
-  if (!s.hflag[c]) return;
+  // every lane of the wave stays in the solve (see hildreth_sweep); cells without a
+  // QP this step ride along on a finite dummy problem and store nothing
+  const bool qp = s.hflag[c] != 0;
   const int64_t n = s.n;
   const double *pb = s.prob;
   Cons Cn;
   double E[NC][NC], F[NC], K[NCON];
-  {
+  double lam[NCON];
+  if (!qp) {
+#pragma unroll
+    for (int a = 0; a < NC; ++a) {
+      F[a] = 0.0;
+#pragma unroll
+      for (int b = 0; b < NC; ++b) E[a][b] = a == b ? 1.0 : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) Cn.Hv[i] = Cn.He[i] = Cn.Hs[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) K[i] = lam[i] = 0.0;
+  } else {
     double y[NC], R[NC][NC];
 #pragma unroll
     for (int a = 0; a < NC; ++a) {
@@ -1522,13 +1572,13 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
       for (int k = 0; k < NC; ++k) sum = sum + Mf(i, k) * y[k];
       K[i] = sum + pb[(PB_GAM + i) * n + c];  // K = M*(E\F) + gamma (hildreth.m:29)
     }
-  }
-  double lam[NCON];
 #pragma unroll
-  for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+  }
   double Mtl[NC];
   MpcOut o;
-  o.nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl);
+  o.nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp);
+  if (!qp) return;
 #pragma unroll
   for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
   // DU = -E\(F + M'*lambda) (hildreth.m:46); operands re-read after the sweeps
@@ -1695,7 +1745,7 @@ static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const K
   static bool attr = false;
   int lds = cell_lds_bytes(r);
   if (!attr) {
-    hipFuncSetAttribute((const void *)k_cell<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_cell<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   hipLaunchKernelGGL(k_cell<NZ>, dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);

@@ -160,6 +160,13 @@ class Context:
         check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
         return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell", "hild"))}
 
+    def get_hild_problems(self):
+        """(prob [51][ncells] field-major, hflag [ncells]) of the last fused step (diagnostic)."""
+        prob = np.empty((51, self.n))
+        hflag = np.empty(self.n, dtype=np.int32)
+        check(self.L.mpcekf_get_hild_problems(self.h, dptr(prob), iptr(hflag)))
+        return prob, hflag
+
     def get_zk(self):
         zk = np.empty((self.n, self.nz + 2))
         zb = np.empty((self.n, self.nz + 2))
