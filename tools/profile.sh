@@ -9,7 +9,7 @@ TAG=${1:-r01}
 O=gpurun_out/prof_$TAG
 mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- \
-  python3 bench.py --steps 100 --warmup 5 --no-cpu > $O/bench_under_trace.log 2>&1 && \
+  python3 bench.py --no-cpu > $O/bench_under_trace.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o run -- \
   python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o run -- \
