@@ -69,6 +69,8 @@ struct mpcekf_ctx {
   int *d_int = nullptr;       // warn, status, nviol, hflag
   double *d_prob = nullptr;   // k_cell -> k_hild problem records
   double *d_zk = nullptr, *d_zbk = nullptr;
+  int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
+  double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -285,6 +287,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       b[NPLANT * NX + q] = Cval(m, perm[q], NX);  // res0 column (Phise rows are not among these)
       b[NPLANT * NX + NPLANT + q] = Dval(m, perm[q]);
     }
+    for (int e = 0; e < 6; ++e) b[NPLANT * NX + 2 * NPLANT + e] = R->A[(size_t)m * n1 + e];  // bigA column
   }
   r.plant_tab = (int)pb.size();
   pb.insert(pb.end(), tabs.begin(), tabs.end());
@@ -379,7 +382,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   if ((rc = dalloc(&s.bigx, n * NM * 6)) || (rc = dalloc(&s.ekf, n * NM * REC)) ||
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
       (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
-      (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2)))) {
+      (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
+      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))) {
     mpcekf_ctx_destroy(X);
     return rc;
   }
@@ -388,6 +392,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.uk_1 = sc + 5 * n; s.uk = sc + 6 * n; s.vk = sc + 7 * n; s.J_unc = sc + 8 * n; s.J_fin = sc + 9 * n;
   s.warn = X->d_int; s.status = X->d_int + n; s.nviol = X->d_int + 2 * n; s.hflag = X->d_int + 3 * n;
   s.prob = X->d_prob;
+  s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
+  s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
   s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
@@ -401,7 +407,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -447,6 +453,7 @@ int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_de
   HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), sc.size() * 8, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipMemsetAsync(X->s.lam, 0, n * X->ncon * 8, X->stream));
   HIPCHK(hipMemsetAsync(X->d_int, 0, n * 4 * sizeof(int), X->stream));
+  HIPCHK(hipMemsetAsync(X->d_ts, 0, n * X->NM * 2 * sizeof(int), X->stream));  // every model current
   int rc = launch_init_state(X->n, X->NM, X->s.ekf, X->s.bigx, X->cfg.SigmaX0, X->stream);
   if (rc) return fail(MPCEKF_E_HIP, "init kernel: %s", hipGetErrorString((hipError_t)rc));
   HIPCHK(hipStreamSynchronize(X->stream));
@@ -496,16 +503,21 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     X->ev.resize((size_t)nsteps * 5);
     for (size_t i = old; i < X->ev.size(); ++i) HIPCHK(hipEventCreate(&X->ev[i]));
   }
+  // Deferred all-model time update: step t advances only the models it
+  // touches (k_plant: plant corners, k_cell: EKF corners); k_flush brings every model
+  // current each LAZY_H steps and at the end of the call, so between calls (stage entry
+  // points, get/set_state) every model is current, exactly as after eager updates.
+  std::vector<char> flushed((size_t)nsteps, 0);
   for (int k = 0; k < nsteps; ++k) {
     const size_t o = (size_t)k * n;
+    const int t = k + 1;
     hipEvent_t *E = X->timing ? &X->ev[(size_t)k * 5] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
-    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, X->stream), "plant"))) return rc;
+    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, X->stream), "plant"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[1], X->stream));
-    if ((rc = lerr(launch_bulk(X->r, X->k, X->s, X->s.uk, 1, 1, X->stream), "bulk"))) return rc;
-    if (E) HIPCHK(hipEventRecord(E[2], X->stream));
     KIO io{};
     io.mode = MODE_FUSED;
+    io.lazy_t = t;
     io.u = dev[0] ? dev[0] + o : nullptr;
     io.v = dev[1] ? dev[1] + o : nullptr;
     io.soc = dev[2] ? dev[2] + o : nullptr;
@@ -514,8 +526,13 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.zk = X->d_zk;
     io.zbk = bounds ? X->d_zbk : nullptr;
     if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-    if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+    if (E) HIPCHK(hipEventRecord(E[2], X->stream));
     if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+    if (t % LAZY_H == 0 || t == nsteps) {
+      if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
+      flushed[k] = 1;
+    }
     if (E) HIPCHK(hipEventRecord(E[4], X->stream));
   }
   if (!outputs_on_device) {
@@ -524,14 +541,17 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     if (traj_nexec) HIPCHK(hipMemcpyAsync(traj_nexec, dnex, per * 4, hipMemcpyDeviceToHost, X->stream));
   }
   HIPCHK(hipStreamSynchronize(X->stream));
-  if (X->timing)
+  if (X->timing) {
+    static const int slot[4] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_HILD, MPCEKF_K_BULK};
     for (int k = 0; k < nsteps; ++k)
       for (int j = 0; j < 4; ++j) {
+        if (j == 3 && !flushed[k]) continue;
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * 5 + j], X->ev[(size_t)k * 5 + j + 1]));
-        X->t_ms[j] += ms;
-        X->t_n[j] += 1;
+        X->t_ms[slot[j]] += ms;
+        X->t_n[slot[j]] += 1;
       }
+  }
   return MPCEKF_OK;
 }
 
@@ -586,7 +606,7 @@ int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, double *vcell) {
   Slab sl{(char *)X->d_tmp};
   double *di = sl.take<double>(n), *dv = sl.take<double>(n);
   HIPCHK(hipMemcpyAsync(di, iapp, n * 8, hipMemcpyHostToDevice, X->stream));
-  if ((rc = lerr(launch_plant(X->r, X->s, di, dv, X->stream), "plant"))) return rc;
+  if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, X->stream), "plant"))) return rc;
   if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
   HIPCHK(hipMemcpyAsync(vcell, dv, n * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));

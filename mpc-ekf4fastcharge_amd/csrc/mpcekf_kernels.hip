@@ -1084,7 +1084,8 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
 // ---------------------------------------------------------------------------
 // k_plant: OB_step simStep outputs for every cell (lane per cell)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout) {
+__global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout,
+                                               const int lazy_t) {
   extern __shared__ double lds[];
   stage_lds(lds, r.plant_blob, r.plant_len);
   __syncthreads();
@@ -1092,6 +1093,11 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   const double *Zp = Tp + MAXT;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
+  if (lazy_t) {  // this step's inputs, for the deferred updates of every model (k_cell, k_flush)
+    const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
+    s.hist_u[slot] = iapp[c];
+    s.hist_p[slot] = s.priorI[c];
+  }
   if (s.status[c] & ST_ERROR) {
     vout[c] = __builtin_nan("");
     return;
@@ -1127,12 +1133,33 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   double Zu = Zp[iZu], Zl = Zp[iZl], Tu = Tp[iTu], Tl = Tp[iTl];
   int mm[4] = {iTl * r.nZ + iZl, iTl * r.nZ + iZu, iTu * r.nZ + iZl, iTu * r.nZ + iZu};
   double y[4][NPLANT];
-  const double *bx = s.bigx + (size_t)c * r.NM * 6;
+  double *bx = s.bigx + (size_t)c * r.NM * 6;
+  // the 4 corner states as of step t-1: all loads before any store (duplicate corners)
+  double xs[4][6];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const double2 *p = reinterpret_cast<const double2 *>(bx + (size_t)mm[j] * 6);
     double2 q0 = p[0], q1 = p[1], q2 = p[2];
-    double x[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+    xs[j][0] = q0.x; xs[j][1] = q0.y; xs[j][2] = q1.x; xs[j][3] = q1.y; xs[j][4] = q2.x; xs[j][5] = q2.y;
+  }
+  int tsj[4] = {0, 0, 0, 0};
+  if (lazy_t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tsj[j] = s.ts_plant[c * r.NM + mm[j]];
+      const double *a = lds + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
+      for (int k = tsj[j] + 1; k < lazy_t; ++k) {  // OB_step.m:198-200 for the skipped steps
+        const double u = s.hist_u[(size_t)(k % LAZY_H) * s.n + c];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) xs[j][e] = a[e] * xs[j][e] + u;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double x[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) x[e] = xs[j][e];
     const double *B = lds + mm[j] * PREC;
 #pragma unroll
     for (int q = 0; q < NPLANT; ++q) {
@@ -1166,6 +1193,21 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   s.SOCn[c] = SOCnAvg;
   s.SOCp[c] = SOCpAvg;
   vout[c] = V;
+  if (lazy_t) {  // advance the corners through step t in place (eager mode: k_bulk does all models)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (tsj[j] >= lazy_t) continue;
+      const double *a = lds + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
+      double2 *p = reinterpret_cast<double2 *>(bx + (size_t)mm[j] * 6);
+      double x[6];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) x[e] = a[e] * xs[j][e] + Iapp;
+      p[0] = make_double2(x[0], x[1]);
+      p[1] = make_double2(x[2], x[3]);
+      p[2] = make_double2(x[4], x[5]);
+      s.ts_plant[c * r.NM + mm[j]] = lazy_t;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1205,6 +1247,92 @@ __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const
       }
     }
   }
+}
+
+// k_flush: brings every local model (EKF record and plant state) of every cell
+// from its timestamp to step t with the logged inputs, then stamps it new_ts.
+// Block per cell, the cell's input rings and timestamps staged in LDS.
+__global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, const KState s, const int t,
+                                               const int new_ts) {
+  extern __shared__ double lds[];
+  const int NM = r.NM;
+  const int ne = NM * REC, np = NM * 6;
+  stage_lds(lds, r.bulk_tab, 2 * ne + np);
+  double *hp = lds + 2 * ne + np, *hu = hp + LAZY_H;
+  int *tse = reinterpret_cast<int *>(hu + LAZY_H), *tsp = tse + NM;
+  const double *cA = lds, *cB = lds + ne, *cP = lds + 2 * ne;
+  const double W = cf.SigmaW;
+  for (int64_t c = blockIdx.x; c < s.n; c += gridDim.x) {
+    __syncthreads();  // previous cell's LDS rings/timestamps fully consumed
+    for (int k = threadIdx.x; k < LAZY_H; k += blockDim.x) {
+      hp[k] = s.hist_p[(size_t)k * s.n + c];
+      hu[k] = s.hist_u[(size_t)k * s.n + c];
+    }
+    for (int m = threadIdx.x; m < NM; m += blockDim.x) {
+      tse[m] = s.ts_ekf[c * NM + m];
+      tsp[m] = s.ts_plant[c * NM + m];
+    }
+    __syncthreads();
+    double2 *be = reinterpret_cast<double2 *>(s.ekf + (size_t)c * ne);
+    for (int j = threadIdx.x; j < ne / 2; j += blockDim.x) {
+      const int e0 = 2 * j, m = e0 / REC;
+      const int ts = tse[m];
+      if (ts >= t) continue;
+      double2 v = be[j];
+      const bool x0 = (e0 % REC) < NX, x1 = ((e0 + 1) % REC) < NX;
+      for (int k = ts + 1; k <= t; ++k) {
+        const double p = hp[k % LAZY_H];
+        v.x = (cA[e0] * v.x) * cB[e0] + (x0 ? p : W);
+        v.y = (cA[e0 + 1] * v.y) * cB[e0 + 1] + (x1 ? p : W);
+      }
+      be[j] = v;
+    }
+    double2 *bp = reinterpret_cast<double2 *>(s.bigx + (size_t)c * np);
+    for (int j = threadIdx.x; j < np / 2; j += blockDim.x) {
+      const int e0 = 2 * j, m = e0 / 6;
+      const int ts = tsp[m];
+      if (ts >= t) continue;
+      double2 v = bp[j];
+      for (int k = ts + 1; k <= t; ++k) {
+        const double u = hu[k % LAZY_H];
+        v.x = cP[e0] * v.x + u;
+        v.y = cP[e0 + 1] * v.y + u;
+      }
+      bp[j] = v;
+    }
+    for (int m = threadIdx.x; m < NM; m += blockDim.x) {
+      s.ts_ekf[c * NM + m] = new_ts;
+      s.ts_plant[c * NM + m] = new_ts;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Deferred time update (fused mpcekf_step): iterEKF.m:73-84 for the steps model m
+// skipped, replayed in the per-step order of the eager update (k_bulk / the oracle),
+// so the record is bit-identical to one advanced every step.
+// ---------------------------------------------------------------------------
+template <int NZ>
+__device__ __forceinline__ void ekf_catch_up(const KState &s, const CellCtx &cc, int NM, int m, int64_t c, int t,
+                                             double W) {
+  int *tsp = s.ts_ekf + c * NM + m;
+  const int ts = *tsp;
+  if (ts >= t) return;
+  const double *a = cc.L + m * cc.stride + NZ * NX + NZ;  // diag(A) of the model (cell blob)
+  double *rec = cc.erec + (size_t)m * REC;
+  double x[NX], S[NPK];
+  load_rec(rec, x, S);
+  for (int k = ts + 1; k <= t; ++k) {
+    const double p = s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+#pragma unroll
+    for (int e = 0; e < NX; ++e) x[e] = a[e] * x[e] + p;
+#pragma unroll
+    for (int i = 0, pp = 0; pp < NX; ++pp)
+#pragma unroll
+      for (int q = pp; q < NX; ++q, ++i) S[i] = (a[pp] * S[i]) * a[q] + W;
+  }
+  store_rec(rec, x, S);
+  *tsp = t;
 }
 
 // ---------------------------------------------------------------------------
@@ -1279,6 +1407,10 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     const double SOC0 = s.SOC0[c];
     double SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
+    if (io.lazy_t) {
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) ekf_catch_up<NZ>(s, cc, r.NM, xi.m[j], c, io.lazy_t, cf.SigmaW);
+    }
     vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
     if (st & ST_ERROR) {
       s.status[c] = st;
@@ -1329,6 +1461,10 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     S0 = S0 - L0 * St0 * L0;
     SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
+    if (io.lazy_t) {
+#pragma unroll 1
+      for (int j = 0; j < 4; ++j) ekf_catch_up<NZ>(s, cc, r.NM, xi.m[j], c, io.lazy_t, cf.SigmaW);
+    }
     vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
     __builtin_amdgcn_sched_barrier(0);
     s.warn[c] = warn;
@@ -1724,10 +1860,18 @@ int plant_lds_bytes(const KRom &r) { return (int)((r.plant_len + 1) * sizeof(dou
 
 bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
 
-int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, void *stream) {
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, void *stream) {
   if (s.n == 0) return 0;
   hipLaunchKernelGGL(k_plant, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r, s,
-                     iapp, vout);
+                     iapp, vout, lazy_t);
+  return (int)hipGetLastError();
+}
+
+int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream) {
+  if (s.n == 0) return 0;
+  int lds = (int)((2 * r.NM * REC + r.NM * 6 + 2 * LAZY_H) * sizeof(double) + 2 * r.NM * sizeof(int));
+  int grid = (int)(s.n < 2048 ? s.n : 2048);
+  hipLaunchKernelGGL(k_flush, dim3(grid), dim3(256), lds, (hipStream_t)stream, r, c, s, t, new_ts);
   return (int)hipGetLastError();
 }
 

@@ -15,7 +15,8 @@ constexpr int MAXT = 8;    // max temperature set-points
 constexpr int MAXZ = 40;   // max SOC set-points
 constexpr int MAXROWS = 64;
 constexpr int NPLANT = 9;  // role rows the plant needs (OB_step.m:289-344)
-constexpr int PREC = NPLANT * NX + NPLANT + NPLANT;  // plant blob record per model: C[9][5], res0[9], D[9]
+constexpr int PREC = NPLANT * NX + NPLANT + NPLANT + 6;  // plant blob record per model: C[9][5], res0[9], D[9], a[6]
+constexpr int LAZY_H = 32;  // deferred time update: input ring length = flush period (steps)
 
 // role slots = the first rows of the permuted output vector (rom.py ROLE_NAMES)
 enum { R_IFDL0 = 0, R_IFDL3, R_IF0, R_IF3, R_TH0, R_TH3, R_TE1, R_TEE, R_PHIE, R_PHISE0, R_NPHISE2, NROLE };
@@ -60,6 +61,11 @@ struct KState {
   // hand-off k_cell -> k_hild
   int *hflag;      // [n] 1: hildreth.m must run this step
   double *prob;    // [PB_N][n] problem records (mpcekf_kernels.hip PB_*)
+  // deferred all-model time update (fused mpcekf_step only): each local
+  // model's record is current through step ts[c][m] of the running call; the inputs
+  // of the last LAZY_H steps sit in per-cell rings
+  int *ts_ekf, *ts_plant;    // [n][NM]
+  double *hist_p, *hist_u;   // [LAZY_H][n] priorI (EKF) and Iapp (plant) of step t at slot t % LAZY_H
 };
 
 // Inputs/outputs of one cell-kernel launch.  Any pointer may be null.
@@ -76,12 +82,16 @@ struct KIO {
   const double *zk_in; const int *xm_in; const double *xg_in;  // linearize stage
   double *lin_out; const double *lin_in;                        // [n][35]
   const double *soc_k1_in; double *uk_out;                      // mpc stage
+  int lazy_t;             // > 0: fused step t of the running call with deferred time update
 };
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 
 // host-side launchers (defined in mpcekf_kernels.hip)
-int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, void *stream);
+// lazy_t > 0: deferred mode (corners replayed/advanced in place, inputs logged to the rings)
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, void *stream);
+// brings every model of every cell from its ts to step t, then sets ts = new_ts
+int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream);
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
 int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream);

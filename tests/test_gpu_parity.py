@@ -185,3 +185,23 @@ def test_runmpc_cell_prefix_matches_golden(rom, M):
     out = M.runMPC(rom, g["soc0"], g["tc"], 3001)
     for k in ("u", "v", "soc", "phise"):
         assert _rel(out[k][:2400], g[k][:2400]).max() <= 1e-9, k
+
+
+def test_deferred_time_update_is_schedule_invariant(rom, M):
+    """The fused step defers the all-model time update (ring of LAZY_H = 32 inputs,
+    flush every 32 steps and at the end of each call).  Splitting the same run into
+    calls that straddle the flush boundaries must give bit-identical trajectories
+    and an identical full state (every local model's record and plant state)."""
+    n = 2048
+    soc0, tc = batch_inputs(n, seed=9)
+    chunks = [1, 31, 32, 33, 53, 250]
+    with M.Context(rom, n) as a, M.Context(rom, n) as b:
+        a.init_cells(soc0, tc)
+        b.init_cells(soc0, tc)
+        ra = a.step(sum(chunks))
+        rb = [b.step(k) for k in chunks]
+        sa, sb = a.get_state(), b.get_state()
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        np.testing.assert_array_equal(ra[k], np.concatenate([r[k] for r in rb]), err_msg=k)
+    for k in ("bigX", "ekf", "scal", "lam", "warn", "status"):
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
