@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libmpcekf.so")
+# MPCEKF_LIB selects a profiling build (tools/stamps.py); the product path is _build/libmpcekf.so
+LIB_PATH = os.environ.get("MPCEKF_LIB") or os.path.join(HERE, "_build", "libmpcekf.so")
 
 MPCEKF_OK = 0
 ST_ERROR, ST_LOCKOUT, ST_THETAE_NEG = 1, 2, 4
@@ -61,7 +62,7 @@ EXPORTS = [
     "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_get_zk",
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
-    "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems",
+    "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps",
 ]
 
 _lib = None
@@ -100,6 +101,7 @@ def load():
     L.mpcekf_set_timing.argtypes = [vp, C.c_int32]
     L.mpcekf_get_timing.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     L.mpcekf_get_hild_problems.argtypes = [vp, _dp, _ip]
+    L.mpcekf_get_stamps.argtypes = [vp, C.POINTER(C.c_int64), _ip]
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults"):
             getattr(L, nm).restype = C.c_int

@@ -34,16 +34,20 @@ def _stale(obj, src):
     return _mtime(obj) < newest
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, variant=""):
+    """variant "stamps": profiling build _build/libmpcekf_stamps.so (-DMPCEKF_STAMPS)."""
     os.makedirs(OUT, exist_ok=True)
     jobs = []
     objs = []
+    sfx = f"_{variant}" if variant else ""
+    extra = ["-DMPCEKF_STAMPS"] if variant == "stamps" else []
+    lib = os.path.join(OUT, f"libmpcekf{sfx}.so")
     for s in SOURCES:
         src = os.path.join(SRC, s)
-        obj = os.path.join(OUT, os.path.splitext(s)[0] + ".o")
+        obj = os.path.join(OUT, os.path.splitext(s)[0] + sfx + ".o")
         objs.append(obj)
         if force or _stale(obj, src):
-            jobs.append([HIPCC, *CFLAGS, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *CFLAGS, *extra, "-c", src, "-o", obj])
 
     def run(cmd):
         if verbose:
@@ -55,10 +59,10 @@ def build(force=False, verbose=False):
     if jobs:
         with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
             list(ex.map(run, jobs))
-    if jobs or force or not os.path.exists(LIB) or any(_mtime(o) > _mtime(LIB) for o in objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs])
-    return LIB
+    if jobs or force or not os.path.exists(lib) or any(_mtime(o) > _mtime(lib) for o in objs):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs])
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, variant="stamps" if "--stamps" in sys.argv else ""))

@@ -71,6 +71,7 @@ struct mpcekf_ctx {
   double *d_zk = nullptr, *d_zbk = nullptr;
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
+  long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -383,7 +384,11 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
       (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
-      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))) {
+      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))
+#ifdef MPCEKF_STAMPS
+      || (rc = dalloc(&X->d_stamps, n * NSTAMPS))
+#endif
+  ) {
     mpcekf_ctx_destroy(X);
     return rc;
   }
@@ -407,7 +412,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -518,6 +523,7 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     KIO io{};
     io.mode = MODE_FUSED;
     io.lazy_t = t;
+    io.stamps = X->d_stamps;
     io.u = dev[0] ? dev[0] + o : nullptr;
     io.v = dev[1] ? dev[1] + o : nullptr;
     io.soc = dev[2] ? dev[2] + o : nullptr;
@@ -797,6 +803,18 @@ int mpcekf_get_hild_problems(mpcekf_ctx *X, double *prob, int32_t *hflag) {
   if (prob) HIPCHK(hipMemcpyAsync(prob, X->s.prob, n * PROB_DOUBLES * 8, hipMemcpyDeviceToHost, X->stream));
   if (hflag) HIPCHK(hipMemcpyAsync(hflag, X->s.hflag, n * 4, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
+int mpcekf_get_stamps(mpcekf_ctx *X, int64_t *stamps, int32_t *nstamps) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  static_assert(MPCEKF_NSTAMPS == NSTAMPS, "stamp count");
+  if (nstamps) *nstamps = X->d_stamps ? NSTAMPS : 0;
+  if (X->d_stamps && stamps) {
+    HIPCHK(hipMemcpyAsync(stamps, X->d_stamps, (size_t)X->n * NSTAMPS * 8, hipMemcpyDeviceToHost, X->stream));
+    HIPCHK(hipStreamSynchronize(X->stream));
+  }
   return MPCEKF_OK;
 }
 

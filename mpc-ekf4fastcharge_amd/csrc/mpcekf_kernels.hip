@@ -33,6 +33,18 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 // live registers.
 __device__ __forceinline__ void launder(double &x) { asm volatile("" : "+v"(x)); }
 
+// Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
+#ifdef MPCEKF_STAMPS
+#define STAMP(i)                                                                          \
+  do {                                                                                    \
+    if (io.stamps) io.stamps[(size_t)(i) * s.n + c] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
 __device__ __forceinline__ int pk(int r, int c) {
   // packed upper-triangular index, row-major over r <= c
   return r <= c ? r * NX - (r * (r - 1)) / 2 + (c - r) : c * NX - (c * (c - 1)) / 2 + (r - c);
@@ -200,6 +212,28 @@ __device__ __forceinline__ void jacobi5(double a[NPK], double V[NX * NX]) {
   }
 }
 
+// Positive definiteness of a packed symmetric 5x5 by LDL' pivots (orc_is_pd, same order).
+__device__ __forceinline__ bool is_pd5(const double a[NPK]) {
+  double l[NX][NX], d[NX];
+  bool pd = true;
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    double s = a[pk(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s = s - (l[j][k] * l[j][k]) * d[k];
+    pd = pd && (s > 0);
+    d[j] = s;
+#pragma unroll
+    for (int i = j + 1; i < NX; ++i) {
+      double t = a[pk(j, i)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t = t - (l[i][k] * l[j][k]) * d[k];
+      l[i][j] = t / s;
+    }
+  }
+  return pd;
+}
+
 // iterEKF.m:137-153 on one corner record (orc_meas_cov + state update).
 // P = Sigma - (L*St)*L' is only ever used as P + P', so only that sum is kept.
 __device__ __forceinline__ void meas_update(double *rec, const double L[NX], double St, double res) {
@@ -220,26 +254,43 @@ __device__ __forceinline__ void meas_update(double *rec, const double L[NX], dou
       Ps[pk(r, c)] = prc + pcr;
       a[pk(r, c)] = (prc + pcr) * 0.5;
     }
-  double V[NX * NX];
-  jacobi5(a, V);
-  double w[NX];
+  const bool bump = res * res > 9 * St;
+  // HH = VV*SS*VV' (iterEKF.m:145-146) is the polar factor of the symmetric part a:
+  // a itself when a is positive definite (the usual case), else V|Lambda|V' (Jacobi).
+  // The decomposition runs only if some lane of the wave needs it.
+  const bool pd = is_pd5(a);
+  if (__all(pd)) {
 #pragma unroll
-  for (int k = 0; k < NX; ++k) w[k] = fabs(a[pk(k, k)]);
-  bool bump = res * res > 9 * St;
-#pragma unroll
-  for (int r = 0; r < NX; ++r)
-#pragma unroll
-    for (int c = r; c < NX; ++c) {
-      double hrc = 0.0, hcr = 0.0;
-#pragma unroll
-      for (int k = 0; k < NX; ++k) {
-        hrc = hrc + (V[r * NX + k] * w[k]) * V[c * NX + k];
-        hcr = hcr + (V[c * NX + k] * w[k]) * V[r * NX + k];
-      }
-      double v = ((Ps[pk(r, c)] + hrc) + hcr) / 4.0;
+    for (int i = 0; i < NPK; ++i) {
+      double v = ((Ps[i] + a[i]) + a[i]) / 4.0;
       if (bump) v = v * 2.0;
-      S[pk(r, c)] = v;
+      S[i] = v;
     }
+  } else {
+    double H[NPK];
+#pragma unroll
+    for (int i = 0; i < NPK; ++i) H[i] = a[i];
+    double V[NX * NX];
+    jacobi5(a, V);
+    double w[NX];
+#pragma unroll
+    for (int k = 0; k < NX; ++k) w[k] = fabs(a[pk(k, k)]);
+#pragma unroll
+    for (int r = 0; r < NX; ++r)
+#pragma unroll
+      for (int c = r; c < NX; ++c) {
+        double hrc = 0.0, hcr = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) {
+          hrc = hrc + (V[r * NX + k] * w[k]) * V[c * NX + k];
+          hcr = hcr + (V[c * NX + k] * w[k]) * V[r * NX + k];
+        }
+        if (pd) { hrc = H[pk(r, c)]; hcr = H[pk(r, c)]; }
+        double v = ((Ps[pk(r, c)] + hrc) + hcr) / 4.0;
+        if (bump) v = v * 2.0;
+        S[pk(r, c)] = v;
+      }
+  }
   store_rec(rec, x, S);
 }
 
@@ -1313,26 +1364,46 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
 // so the record is bit-identical to one advanced every step.
 // ---------------------------------------------------------------------------
 template <int NZ>
-__device__ __forceinline__ void ekf_catch_up(const KState &s, const CellCtx &cc, int NM, int m, int64_t c, int t,
-                                             double W) {
-  int *tsp = s.ts_ekf + c * NM + m;
-  const int ts = *tsp;
-  if (ts >= t) return;
-  const double *a = cc.L + m * cc.stride + NZ * NX + NZ;  // diag(A) of the model (cell blob)
-  double *rec = cc.erec + (size_t)m * REC;
-  double x[NX], S[NPK];
-  load_rec(rec, x, S);
-  for (int k = ts + 1; k <= t; ++k) {
-    const double p = s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+__device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc, int NM, const int m[4], int64_t c,
+                                              int t, double W) {
+  // all timestamps, then all lagging records, in flight together (latency, not bytes,
+  // is the cost here); a model named by several corners is advanced once
+  int ts[4];
 #pragma unroll
-    for (int e = 0; e < NX; ++e) x[e] = a[e] * x[e] + p;
+  for (int j = 0; j < 4; ++j) ts[j] = s.ts_ekf[c * NM + m[j]];
+  bool need[4];
 #pragma unroll
-    for (int i = 0, pp = 0; pp < NX; ++pp)
+  for (int j = 0; j < 4; ++j) {
+    need[j] = ts[j] < t;
 #pragma unroll
-      for (int q = pp; q < NX; ++q, ++i) S[i] = (a[pp] * S[i]) * a[q] + W;
+    for (int i = 0; i < j; ++i) need[j] = need[j] && m[i] != m[j];
   }
-  store_rec(rec, x, S);
-  *tsp = t;
+  if (!(need[0] || need[1] || need[2] || need[3])) return;
+  const double pt = s.hist_p[(size_t)(t % LAZY_H) * s.n + c];  // the usual (lag-1) input
+  double x[4][NX], S[4][NPK];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (need[j]) load_rec(cc.erec + (size_t)m[j] * REC, x[j], S[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!need[j]) continue;
+    const double *a = cc.L + m[j] * cc.stride + NZ * NX + NZ;  // diag(A) of the model (cell blob)
+    for (int k = ts[j] + 1; k <= t; ++k) {
+      const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+#pragma unroll
+      for (int e = 0; e < NX; ++e) x[j][e] = a[e] * x[j][e] + p;
+#pragma unroll
+      for (int i = 0, pp = 0; pp < NX; ++pp)
+#pragma unroll
+        for (int q = pp; q < NX; ++q, ++i) S[j][i] = (a[pp] * S[j][i]) * a[q] + W;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (need[j]) {
+      store_rec(cc.erec + (size_t)m[j] * REC, x[j], S[j]);
+      s.ts_ekf[c * NM + m[j]] = t;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1365,6 +1436,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   int st = s.status[c];
   const bool fused = io.mode & MODE_FUSED;
   if (io.mode & (MODE_MPC | MODE_FUSED)) s.hflag[c] = 0;  // set again only if hildreth.m must run
+  STAMP(0);
 
   auto fail_outputs = [&]() {
     if (io.u) io.u[c] = NaN;
@@ -1407,11 +1479,10 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     const double SOC0 = s.SOC0[c];
     double SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
-    if (io.lazy_t) {
-#pragma unroll 1
-      for (int j = 0; j < 4; ++j) ekf_catch_up<NZ>(s, cc, r.NM, xi.m[j], c, io.lazy_t, cf.SigmaW);
-    }
+    if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
+    STAMP(1);
     vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
+    STAMP(2);
     if (st & ST_ERROR) {
       s.status[c] = st;
       s.warn[c] = warn;
@@ -1452,21 +1523,21 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int k = 0; k < NX; ++k) launder(Lg[j][k]);
     }
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(3);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       meas_update(cc.erec + (size_t)xi.m[j] * REC, Lg[j], St[j], res);
       __builtin_amdgcn_sched_barrier(0);
     }
+    STAMP(4);
     x0 = x0 + L0 * res;
     S0 = S0 - L0 * St0 * L0;
     SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
-    if (io.lazy_t) {
-#pragma unroll 1
-      for (int j = 0; j < 4; ++j) ekf_catch_up<NZ>(s, cc, r.NM, xi.m[j], c, io.lazy_t, cf.SigmaW);
-    }
+    if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
     vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
     __builtin_amdgcn_sched_barrier(0);
+    STAMP(5);
     s.warn[c] = warn;
     if (st & ST_ERROR) {
       s.status[c] = st;
@@ -1563,6 +1634,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       io.zbk[c * (nz + 2) + nz + 1] = 3 * sqrt(SigSOC);
     }
 #endif
+    STAMP(6);
     s.x0[c] = x0;
     s.S0[c] = S0;
     s.priorI[c] = ik;  // iterEKF.m:210
@@ -1596,6 +1668,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
   }
+  STAMP(7);
 
 #ifndef PROBE_NO_MPC
   if (io.mode & (MODE_MPC | MODE_FUSED)) {
@@ -1622,6 +1695,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       if (io.phise) io.phise[c] = phise;
     }
     if (s.J_unc) s.J_unc[c] = o.J_unc;
+    STAMP(8);
     s.hflag[c] = need ? 1 : 0;
     if (need) {  // hildreth.m runs in k_hild
       double *pb = s.prob;

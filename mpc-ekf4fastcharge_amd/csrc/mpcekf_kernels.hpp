@@ -83,7 +83,9 @@ struct KIO {
   double *lin_out; const double *lin_in;                        // [n][35]
   const double *soc_k1_in; double *uk_out;                      // mpc stage
   int lazy_t;             // > 0: fused step t of the running call with deferred time update
+  long long *stamps;      // [MPCEKF_NSTAMPS][n] s_memtime per k_cell section (-DMPCEKF_STAMPS builds only)
 };
+constexpr int NSTAMPS = 9;
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 

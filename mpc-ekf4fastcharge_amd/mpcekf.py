@@ -160,6 +160,16 @@ class Context:
         check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
         return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell", "hild"))}
 
+    def get_stamps(self):
+        """k_cell section stamps of the last fused step [NSTAMPS][ncells] (profiling builds; else None)."""
+        ns = C.c_int32(0)
+        check(self.L.mpcekf_get_stamps(self.h, None, C.byref(ns)))
+        if ns.value == 0:
+            return None
+        out = np.empty((ns.value, self.n), dtype=np.int64)
+        check(self.L.mpcekf_get_stamps(self.h, out.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(ns)))
+        return out
+
     def get_hild_problems(self):
         """(prob [51][ncells] field-major, hflag [ncells]) of the last fused step (diagnostic)."""
         prob = np.empty((51, self.n))

@@ -305,6 +305,24 @@ double orc_sigma_min(int n, const double *G) {
 /* iterEKF.m:141-151 on one packed covariance.
  * P = Sigma - (L*St)*L' ; S_new = ((P + P') + HH + HH')/4 with HH = V|D|V',
  * V,D from Jacobi of (P+P')/2 ; then Q-bump x2. */
+/* Positive definiteness of a symmetric NX x NX matrix by LDL' pivots (no square
+ * roots): every pivot d_j > 0.  The kernels evaluate the identical sequence. */
+int orc_is_pd(const double *a /*full, symmetric*/) {
+  double l[NX][NX], d[NX];
+  for (int j = 0; j < NX; ++j) {
+    double s = a[j * NX + j];
+    for (int k = 0; k < j; ++k) s = s - (l[j][k] * l[j][k]) * d[k];
+    if (!(s > 0)) return 0;
+    d[j] = s;
+    for (int i = j + 1; i < NX; ++i) {
+      double t = a[i * NX + j];
+      for (int k = 0; k < j; ++k) t = t - (l[i][k] * l[j][k]) * d[k];
+      l[i][j] = t / s;
+    }
+  }
+  return 1;
+}
+
 void orc_meas_cov(double *S /*packed*/, const double *L, double St, int bump) {
   double P[NX][NX], a[NX * NX], V[NX * NX], w[NX];
   double LS[NX];
@@ -313,14 +331,23 @@ void orc_meas_cov(double *S /*packed*/, const double *L, double St, int bump) {
     for (int c = 0; c < NX; ++c) P[r][c] = S[PK[r][c]] - LS[r] * L[c];
   for (int r = 0; r < NX; ++r)
     for (int c = 0; c < NX; ++c) a[r * NX + c] = (P[r][c] + P[c][r]) * 0.5;
-  orc_jacobi(NX, a, V, w);
+  /* HH = VV*SS*VV' of svd (iterEKF.m:145-146) is the polar factor of SigmaX; for the
+   * symmetric part a it is V|Lambda|V' (Jacobi).  When a is positive definite that
+   * is a itself: take it directly (no reconstruction rounding) and skip the
+   * eigen-decomposition. */
   double HH[NX][NX];
-  for (int r = 0; r < NX; ++r)
-    for (int c = 0; c < NX; ++c) {
-      double acc = 0.0;
-      for (int k = 0; k < NX; ++k) acc = acc + (V[r * NX + k] * fabs(w[k])) * V[c * NX + k];
-      HH[r][c] = acc;
-    }
+  if (orc_is_pd(a)) {
+    for (int r = 0; r < NX; ++r)
+      for (int c = 0; c < NX; ++c) HH[r][c] = a[r * NX + c];
+  } else {
+    orc_jacobi(NX, a, V, w);
+    for (int r = 0; r < NX; ++r)
+      for (int c = 0; c < NX; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < NX; ++k) acc = acc + (V[r * NX + k] * fabs(w[k])) * V[c * NX + k];
+        HH[r][c] = acc;
+      }
+  }
   for (int r = 0; r < NX; ++r)
     for (int c = r; c < NX; ++c) {
       double v = (((P[r][c] + P[c][r]) + HH[r][c]) + HH[c][r]) / 4.0;

@@ -4,7 +4,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 exactly half the bytes of a wide (16 B/lane) coalesced streaming read
 (MI355X_MICROARCH.md §HBM), so reads are doubled; WRITE_SIZE is exact for
-16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,bulk,cell,hild}.
+16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,bulk,cell,hild} (bulk = the all-model
+time update: k_bulk eager / k_flush deferred) and fp64_flops_per_launch.
 """
 import csv
 import glob
@@ -13,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_plant": "plant", "k_bulk": "bulk", "k_cell": "cell", "k_hild": "hild"}
+KERNELS = {"k_plant": "plant", "k_bulk": "bulk", "k_flush": "bulk", "k_cell": "cell", "k_hild": "hild"}
 
 
 def read_counter(d, name):
@@ -39,6 +40,15 @@ def main():
            "per_launch_bytes": {}}
     for k in set(fetch) | set(write):
         out["per_launch_bytes"][k] = 2 * fetch.get(k, 0.0) * 1024 + write.get(k, 0.0) * 1024
+    # FP64 work per launch: the SQ_INSTS_VALU_*_F64 counters count wave instructions;
+    # x64 lanes (an upper bound when EXEC is partial), FMA = 2 flops
+    fd = os.path.join(base, "fp64")
+    if os.path.isdir(fd):
+        cnt = {nm: read_counter(fd, f"SQ_INSTS_VALU_{nm}_F64") for nm in ("ADD", "MUL", "FMA", "TRANS")}
+        out["fp64_flops_per_launch"] = {
+            k: 64.0 * (cnt["ADD"].get(k, 0) + cnt["MUL"].get(k, 0) + cnt["TRANS"].get(k, 0) + 2 * cnt["FMA"].get(k, 0))
+            for k in set().union(*[set(v) for v in cnt.values()])}
+        out["fp64_wave_instructions_per_launch"] = cnt
     print(json.dumps(out, indent=1))
 
 
