@@ -30,21 +30,34 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds):
-    """Algorithmic HBM bytes each kernel moves per cell per step (DESIGN.md "Roofline").
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32):
+    """Algorithmic HBM bytes each kernel moves per cell per launch:
+    the state it must read and write once, with nothing re-read.
 
-    bulk : every local model's EKF record (xhat 5 + packed SigmaX 15 doubles) and
-           plant state (6 doubles) read and written once, + 2 per-cell scalars.
-    cell : the 4 corner EKF records read+written, warm-start lambda read+written,
-           per-cell scalars/constants, trajectory outputs and zk.
-    plant: the 4 corner plant states read, per-cell scalars.
+    flush: the all-model time update, run as k_flush every lazy_h steps: every EKF
+           record (xhat 5 + packed Sigma 15) and plant state (6) read + written,
+           the model timestamps (2 x NM int32) read + written, the two input rings.
+    cell : the 4 corner EKF records read + written, their timestamps, the step's
+           ring input, per-cell scalars/constants, outputs u/v/soc/phise, zk
+           (+ boundzk) and the QP record.
+    plant: the 4 corner plant states read + written, timestamps, ring writes,
+           per-cell scalars.
+    hild : the QP record read, lambda read + written, outputs.
     """
-    bulk = 2 * 8 * NM * (20 + 6) + 2 * 8
-    cell = 4 * 2 * 8 * 20 + 2 * 8 * ncon + 20 * 8 + 4 * 8 + 4 + 28 * 8 + (28 * 8 if bounds else 0)
-    plant = 4 * 6 * 8 + 12 * 8 + 8
-    # hild: problem record read (51 doubles), lambda read+written, outputs
+    flush = 2 * 8 * NM * (20 + 6) + 2 * 2 * 4 * NM + 2 * 8 * lazy_h
+    zk = 8 * 28 * (2 if bounds else 1)
+    cell = 4 * 2 * 8 * 20 + 4 * 2 * 4 + 8 + 20 * 8 + 4 * 8 + zk + 51 * 8
+    plant = 4 * 2 * 6 * 8 + 4 * 2 * 4 + 2 * 8 + 12 * 8 + 8
     hild = 51 * 8 + 2 * 8 * ncon + 4 * 8
-    return dict(bulk=bulk, cell=cell + 51 * 8, plant=plant, hild=hild)
+    return dict(flush=flush, cell=cell, plant=plant, hild=hild)
+
+
+def survey_bytes_per_cell_step(NM, ncon):
+    """the whole step's persistent state read + written once."""
+    return 416 * NM + 16 * ncon + 160
+
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (AMD spec; FMA = 2 flops); no FMA here -> 39.3 reachable
 
 
 def batch_inputs(n, seed=0x5EED):
@@ -129,16 +142,25 @@ def main():
         cell_steps = total * K
         value = cell_steps / dt if dt > 0 else 0.0
         bpc = algorithmic_bytes_per_cell(rom.NM, 23, bool(args.bounds))
-        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1]) for k in tim}
-        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_per_launch"])
+        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1], ms_total=tim[k][0])
+                      for k in tim}
+        # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
         ms = per_kernel[dom]["ms_per_launch"]
         achieved = bpc[dom] * cpg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        traffic = None
+        pmc = {}
         if os.path.exists(args.pmc):
             try:
-                traffic = json.load(open(args.pmc)).get("per_launch_bytes", {}).get(dom)
+                pmc = json.load(open(args.pmc))
             except Exception:
-                traffic = None
+                pmc = {}
+        traffic = pmc.get("per_launch_bytes", {}).get(dom)
+        flops = pmc.get("fp64_flops_per_launch", {}).get(dom)
+        fp64 = None
+        if flops and ms > 0:
+            tf = flops / (ms * 1e-3) / 1e12
+            fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                    "flops_per_launch": flops, "source": os.path.relpath(args.pmc, ROOT)}
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps or (W + K),
@@ -166,8 +188,15 @@ def main():
                 "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "algorithmic_bytes_per_cell": bpc[dom],
+                "fp64": fp64,
+                "step_equivalent": {
+                    "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, 23),
+                    "achieved": value * survey_bytes_per_cell_step(rom.NM, 23) / 1e9, "unit": "GB/s",
+                    "note": "SURVEY.md 8(d): whole-step state r+w per cell-step x cell-steps/s",
+                },
             },
             "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
+                                ms_per_step=round(v["ms_total"] / K, 5) if K else None,
                                 gbs_algorithmic=round(bpc[k] * cpg / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
                                 if v["ms_per_launch"] > 0 else None)
                         for k, v in per_kernel.items()},

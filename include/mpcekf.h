@@ -178,10 +178,11 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
 /* ---- instrumentation (not part of the reference interface) ---- */
 /* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
  * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch
- * counts of [plant, bulk, cell, hild] (arrays of MPCEKF_NKERNELS) since the last
- * call and resets them. */
+ * counts of [plant, flush, cell, hild] (arrays of MPCEKF_NKERNELS) since the last
+ * call and resets them.  "flush" is the all-model time update (k_flush, every
+ * 32 steps and at the end of each call). */
 #define MPCEKF_K_PLANT 0
-#define MPCEKF_K_BULK 1
+#define MPCEKF_K_FLUSH 1
 #define MPCEKF_K_CELL 2
 #define MPCEKF_K_HILD 3
 #define MPCEKF_NKERNELS 4

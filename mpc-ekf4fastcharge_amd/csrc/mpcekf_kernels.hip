@@ -805,15 +805,16 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
     bool conv = true;
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
-      double s = 0.0, hii = 0.0;
+      double p4[4] = {0.0, 0.0, 0.0, 0.0}, hii = 0.0;
 #pragma unroll
       for (int j = 0; j < NCON; ++j) {
         double h = 0.0;
 #pragma unroll
         for (int k = 0; k < NC; ++k) h = h + Mf(i, k) * X[j][k];
         if (j == i) hii = h;
-        s = s + h * lam[j];
+        p4[j & 3] = p4[j & 3] + h * lam[j];
       }
+      const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);  // orc_hildreth's defined order
       double w = -((K[i] + s) - hii * lam[i]) / hii;
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];
@@ -970,16 +971,14 @@ __device__ __forceinline__ void mpc_finish(const Cons &Cn, const double e[NP], d
   o.J_fin = mpc_cost(Cn.Hs, e, Ru, DU);
 }
 
-// hildreth.m:17-46 in the exact dense summation order, skipping only the terms
-// H(i,j)*lambda(j) whose lambda(j) is +0 in every lane of the wave: such a term
-// is +-0 when H(i,j) is finite, and adding +-0 to the running sum (which starts
-// at +0 and so can never be -0) leaves it bit-identical.  If any lane has a
-// non-finite M or X entry the wave keeps every term (dense order, as hildreth.m).
+// hildreth.m:17-46.  H(i,:)*lambda is summed in orc_hildreth's defined order: four
+// interleaved partial sums p_q (terms j = q mod 4, each from +0 in ascending j),
+// combined as (p0 + p1) + (p2 + p3).  None of these sums can be -0.
 //
 // X = E\M' is kept for the 15 Toeplitz rows plus three solves for the constant
 // current rows: X(-b) = -X(b) exactly under round-to-nearest; the sign of a
-// zero in those X entries cannot reach the sweep (it only feeds products whose
-// sum is added to a never -0 running sum, and their diagonal H_ii = E^-1_00 > 0).
+// zero in those X entries cannot reach the sweep (it only feeds products added to
+// sums that are never -0, and their diagonal H_ii = E^-1_00 > 0).
 struct XS {
   double a[NC], b[NC], c[NC];        // E\[1;0], E\[1;1], E\[0;1]
   double t[3 * NP][NC];              // E\M(i,:)' for the V / eta / SOC rows
@@ -1001,7 +1000,7 @@ __device__ __forceinline__ double xval(const XS &X, int j, int k) {
 // h(i,j) = M(i,:)*X(:,j) when every operand is finite, exact up to the sign of
 // a zero result: the dense form (0 + m0*x0) + m1*x1 differs from these only
 // when a partial result is a signed zero.  A zero h(i,j) only ever feeds
-// h(i,j)*lambda(j) (+-0, or NaN for lambda = inf either way) added to a running
+// h(i,j)*lambda(j) (+-0, or NaN for lambda = inf either way) added to a partial
 // sum that starts at +0 and so is never -0: the sum is bit-identical.
 __device__ __forceinline__ double hfast(const Cons &C, int i, double x0, double x1) {
   switch (i) {  // the constant rows [Cu; -Cu; I; -I] for NC == 2
@@ -1032,13 +1031,11 @@ __device__ __forceinline__ double hfast(const Cons &C, int i, double x0, double 
 // under full-chip load (tools/micro/exec_micro.hip), and Hildreth's convergence
 // is very uneven across cells.  `done` = true makes a lane a passenger from the
 // start (no QP this step: its operands are a finite dummy and nothing is kept).
-__device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
-                                              double tol, const double K[NCON], double Mtl[NC], bool done) {
-  static_assert(NC == 2, "written for Nc = 2");
+// X = E\M' in compressed form (hildreth.m:25); fin = every X and M entry finite.
+__device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], XS &Xs, bool &fin) {
   ConsM Mf{Cn};
   double R[NC][NC];
   bool ok = chol_n<NC>(E, R);
-  XS Xs;
   {
     double b1[NC] = {1.0, 0.0}, b2[NC] = {1.0, 1.0}, b3[NC] = {0.0, 1.0};
     mldiv_spd<NC>(E, R, ok, b1, Xs.a);
@@ -1052,14 +1049,33 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
     for (int k = 0; k < NC; ++k) b[k] = Mf(i, k);
     mldiv_spd<NC>(E, R, ok, b, Xs.t[i - 4 * NC]);
   }
-  bool fin = true;
+  fin = true;
 #pragma unroll
   for (int j = 0; j < NCON; ++j)
     fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
+}
+
+// Returns hildreth.m's nexec when the lane finished (converged, or maxIter sweeps
+// done), or -(sweeps done) - 1 when the wave thinned out to at most `handoff`
+// iterating lanes first (handoff > 0): k_hild2 continues such a cell from its
+// stored lambda.
+__device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
+                                              int handoff, double tol, const double K[NCON], double Mtl[NC],
+                                              bool done) {
+  static_assert(NC == 2, "written for Nc = 2");
+  ConsM Mf{Cn};
+  XS Xs;
+  bool fin;
+  hild_x(Cn, E, Xs, fin);
   int nexec = maxIter;
 #pragma unroll 1
   for (int it = 1; it <= maxIter; ++it) {
-    if (__all(done)) break;
+    const int active = __popcll(__ballot(!done));
+    if (active == 0) break;
+    if (active <= handoff) {
+      if (!done) nexec = -it;  // it - 1 sweeps done
+      break;
+    }
     // opaque per sweep: stops the entries of H being hoisted out of the loop (and spilled)
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
@@ -1076,12 +1092,13 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
         const double hb = hfast(Cn, i, Xs.b[0], Xs.b[1]);
         const double hc = hfast(Cn, i, Xs.c[0], Xs.c[1]);
         const double hconst[4 * NC] = {ha, hb, -ha, -hb, ha, hc, -ha, -hc};
-        double s = 0.0;
+        double p4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NCON; ++j) {
           const double h = j < 4 * NC ? hconst[j] : hfast(Cn, i, Xs.t[j - 4 * NC][0], Xs.t[j - 4 * NC][1]);
-          s = s + h * L[j];
+          p4[j & 3] = p4[j & 3] + h * L[j];
         }
+        const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
         const double li = L[i];
         const double w = -((K[i] + s) - hii * li) / hii;
         const double nl = w > 0 ? w : 0.0;
@@ -1092,13 +1109,14 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
 #pragma unroll
       for (int i = 0; i < NCON; ++i) {
         const double m0 = Mf(i, 0), m1 = Mf(i, 1);
-        double s = 0.0, hii = 0.0;
+        double p4[4] = {0.0, 0.0, 0.0, 0.0}, hii = 0.0;
 #pragma unroll
         for (int j = 0; j < NCON; ++j) {
           const double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
           if (j == i) hii = h;
-          s = s + h * L[j];
+          p4[j & 3] = p4[j & 3] + h * L[j];
         }
+        const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
         const double li = L[i];
         const double w = -((K[i] + s) - hii * li) / hii;
         const double nl = w > 0 ? w : 0.0;
@@ -1734,86 +1752,77 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 }
 
 // ---------------------------------------------------------------------------
-// k_hild: hildreth.m + iterMPC.m:68-95 for the cells k_cell flagged
+// k_hild / k_hild2: hildreth.m + iterMPC.m:68-95 for the cells k_cell flagged
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= s.n) return;
-  // every lane of the wave stays in the solve (see hildreth_sweep); cells without a
-  // QP this step ride along on a finite dummy problem and store nothing
-  const bool qp = s.hflag[c] != 0;
+// The QP record of cell c (PB_*) -> Cons, E and K = M*(E\F) + gamma (hildreth.m:29).
+__device__ __forceinline__ void hild_load(const KState &s, int64_t c, Cons &Cn, double E[NC][NC], double K[NCON]) {
   const int64_t n = s.n;
   const double *pb = s.prob;
-  Cons Cn;
-  double E[NC][NC], F[NC], K[NCON];
-  double lam[NCON];
-  if (!qp) {
+  double F[NC], y[NC], R[NC][NC];
 #pragma unroll
-    for (int a = 0; a < NC; ++a) {
-      F[a] = 0.0;
+  for (int a = 0; a < NC; ++a) {
+    F[a] = pb[(PB_F + a) * n + c];
 #pragma unroll
-      for (int b = 0; b < NC; ++b) E[a][b] = a == b ? 1.0 : 0.0;
-    }
-#pragma unroll
-    for (int i = 0; i < NP; ++i) Cn.Hv[i] = Cn.He[i] = Cn.Hs[i] = 0.0;
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) K[i] = lam[i] = 0.0;
-  } else {
-    double y[NC], R[NC][NC];
-#pragma unroll
-    for (int a = 0; a < NC; ++a) {
-      F[a] = pb[(PB_F + a) * n + c];
-#pragma unroll
-      for (int b = 0; b < NC; ++b) E[a][b] = pb[(PB_E + a * NC + b) * n + c];
-    }
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      Cn.Hv[i] = pb[(PB_HV + i) * n + c];
-      Cn.He[i] = pb[(PB_HE + i) * n + c];
-      Cn.Hs[i] = pb[(PB_HS + i) * n + c];
-    }
-    bool ok = chol_n<NC>(E, R);
-    mldiv_spd<NC>(E, R, ok, F, y);
-    ConsM Mf{Cn};
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) {
-      double sum = 0.0;
-#pragma unroll
-      for (int k = 0; k < NC; ++k) sum = sum + Mf(i, k) * y[k];
-      K[i] = sum + pb[(PB_GAM + i) * n + c];  // K = M*(E\F) + gamma (hildreth.m:29)
-    }
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+    for (int b = 0; b < NC; ++b) E[a][b] = pb[(PB_E + a * NC + b) * n + c];
   }
-  double Mtl[NC];
-  MpcOut o;
-  o.nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp);
-  if (!qp) return;
 #pragma unroll
-  for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
-  // DU = -E\(F + M'*lambda) (hildreth.m:46); operands re-read after the sweeps
-  const double *pb2 = pb;
-  asm volatile("" : "+v"(pb2));
+  for (int i = 0; i < NP; ++i) {
+    Cn.Hv[i] = pb[(PB_HV + i) * n + c];
+    Cn.He[i] = pb[(PB_HE + i) * n + c];
+    Cn.Hs[i] = pb[(PB_HS + i) * n + c];
+  }
+  bool ok = chol_n<NC>(E, R);
+  mldiv_spd<NC>(E, R, ok, F, y);
+  ConsM Mf{Cn};
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) sum = sum + Mf(i, k) * y[k];
+    K[i] = sum + pb[(PB_GAM + i) * n + c];
+  }
+}
+
+// A finite dummy QP for lanes that only ride along (no QP this step / no queued cell).
+__device__ __forceinline__ void hild_dummy(Cons &Cn, double E[NC][NC], double K[NCON]) {
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) E[a][b] = a == b ? 1.0 : 0.0;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) Cn.Hv[i] = Cn.He[i] = Cn.Hs[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) K[i] = 0.0;
+}
+
+// DU = -E\(F + M'*lambda) (hildreth.m:46), then iterMPC.m:75-95 and the outputs.
+__device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int64_t c, const Cons &Cn,
+                                            const double Mtl[NC], int nexec) {
+  const int64_t n = s.n;
+  const double *pb = s.prob;
+  asm volatile("" : "+v"(pb));  // operands re-read after the sweeps, not kept live across them
+  MpcOut o;
+  o.nexec = nexec;
   MpcSetup P;
   double rhs[NC], mE[NC][NC];
 #pragma unroll
   for (int a = 0; a < NC; ++a) {
-    rhs[a] = pb2[(PB_F + a) * n + c] + Mtl[a];
+    rhs[a] = pb[(PB_F + a) * n + c] + Mtl[a];
 #pragma unroll
-    for (int b = 0; b < NC; ++b) mE[a][b] = -pb2[(PB_E + a * NC + b) * n + c];
+    for (int b = 0; b < NC; ++b) mE[a][b] = -pb[(PB_E + a * NC + b) * n + c];
   }
   lu_solve_n<NC>(mE, rhs, P.DU);
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    P.e[i] = pb2[(PB_ERR + i) * n + c];
+    P.e[i] = pb[(PB_ERR + i) * n + c];
     P.Cn.Hv[i] = Cn.Hv[i];
     P.Cn.He[i] = Cn.He[i];
     P.Cn.Hs[i] = Cn.Hs[i];
   }
 #pragma unroll
-  for (int i = 0; i < NCON; ++i) P.Cn.gam[i] = pb2[(PB_GAM + i) * n + c];
-  P.Ru = pb2[PB_RU * n + c];
-  double uk_1 = pb2[PB_UK1 * n + c];
+  for (int i = 0; i < NCON; ++i) P.Cn.gam[i] = pb[(PB_GAM + i) * n + c];
+  P.Ru = pb[PB_RU * n + c];
+  double uk_1 = pb[PB_UK1 * n + c];
   mpc_finish(P.Cn, P.e, P.Ru, P.DU, uk_1, o);
   s.uk_1[c] = uk_1;
   if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
@@ -1823,6 +1832,183 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
     s.uk[c] = o.uk;
     if (io.u) io.u[c] = o.uk;
   }
+}
+
+// Phase 1: lane per cell while the wave is dense; the cells still iterating when at
+// most cf.hild_handoff lanes remain are queued for k_hild2.
+__global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  // every lane of the wave stays in the solve (see hildreth_sweep); cells without a
+  // QP this step ride along on a finite dummy problem and store nothing
+  const bool qp = s.hflag[c] != 0;
+  const int64_t n = s.n;
+  Cons Cn;
+  double E[NC][NC], K[NCON], lam[NCON];
+  if (!qp) {
+    hild_dummy(Cn, E, K);
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = 0.0;
+  } else {
+    hild_load(s, c, Cn, E, K);
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+  }
+  double Mtl[NC];
+  const int nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_handoff, cf.hild_tol, K, Mtl, !qp);
+  // queue the cells handed off to k_hild2: one atomic per wave
+  const bool enq = qp && nexec < 0;
+  const unsigned long long bal = __ballot(enq);
+  if (bal) {
+    const int leader = __ffsll((long long)bal) - 1;
+    int base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(s.hq_n, __popcll(bal));
+    base = __shfl(base, leader);
+    if (enq) {
+      const int slot = base + __popcll(bal & ((1ull << __lane_id()) - 1));
+      s.hq[slot] = (int)c;
+      s.hq_it[slot] = -nexec - 1;
+    }
+  }
+  if (!qp) return;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
+  if (enq) return;
+  hild_finish(s, io, c, Cn, Mtl, nexec);
+}
+
+// v from the quad lane selected by DPP quad_perm control CTRL.
+template <int CTRL>
+__device__ __forceinline__ double qperm(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Broadcast lane Q's value of v to its quad (DPP quad_perm [Q,Q,Q,Q]).
+template <int Q>
+__device__ __forceinline__ double qbc(double v) {
+  constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, ctrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctrl, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ double qbc_q(double v, int q) {  // q folds to a constant after unrolling
+  switch (q & 3) {
+    case 0: return qbc<0>(v);
+    case 1: return qbc<1>(v);
+    case 2: return qbc<2>(v);
+    default: return qbc<3>(v);
+  }
+}
+
+// (p0 + p1) + (p2 + p3) of a quad's partials in every lane of the quad, by two
+// butterfly steps: lanes 0/1 form p0+p1 (= p1+p0: IEEE addition commutes), 2/3 form
+// p2+p3, then each adds the other pair's sum.
+__device__ __forceinline__ double quad_sum(double p) {
+  const double t = p + qperm<1 | (0 << 2) | (3 << 4) | (2 << 6)>(p);   // quad_perm [1,0,3,2]
+  return t + qperm<2 | (3 << 2) | (0 << 4) | (1 << 6)>(t);              // quad_perm [2,3,0,1]
+}
+
+constexpr int QT = (NCON + 3) / 4;  // terms per lane of a quad
+
+// Phase 2: a lane quad per queued cell continues hildreth.m from its next sweep.
+// Lane q of the quad owns the columns j = q mod 4 (X and lambda in registers at slot
+// j / 4) and forms partial sum p_q of H(i,:)*lambda; every lane then combines the
+// four partials as (p0 + p1) + (p2 + p3) (quad_sum) -- orc_hildreth's order,
+// identical to the one-lane form of k_hild -- so all four lanes hold the same w,
+// lambda(i) and convergence flag and need no further exchange.
+__global__ void __launch_bounds__(256) k_hild2(const KCfg cf, const KState s, const KIO io) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int count = *s.hq_n;
+  if (((gt & ~63ll) >> 2) >= count) return;  // no queued cell in this wave
+  const int q = (int)(gt & 3);
+  const int64_t g = gt >> 2;
+  const bool real = g < count;
+  const int64_t c = real ? s.hq[g] : 0;
+  const int it0 = real ? s.hq_it[g] : cf.max_hild;
+  const int64_t n = s.n;
+  Cons Cn;
+  double E[NC][NC], K[NCON];
+  if (real) hild_load(s, c, Cn, E, K);
+  else hild_dummy(Cn, E, K);
+  ConsM Mf{Cn};
+  XS Xs;
+  bool fin;
+  hild_x(Cn, E, Xs, fin);
+  double hii[NCON];
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) hii[i] = (0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1);
+  double Xq[QT][NC], Lq[QT];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) { Xq[t][0] = Xq[t][1] = 0.0; Lq[t] = 0.0; }
+#pragma unroll
+  for (int j = 0; j < NCON; ++j)
+    if ((j & 3) == q) {
+      Xq[j >> 2][0] = xval(Xs, j, 0);
+      Xq[j >> 2][1] = xval(Xs, j, 1);
+      if (real) Lq[j >> 2] = s.lam[(size_t)j * n + c];
+    }
+  bool done = !real || it0 >= cf.max_hild;
+  int nexec = cf.max_hild;
+  int it = it0;
+#pragma unroll 1
+  while (!__all(done)) {
+    ++it;
+#pragma unroll
+    for (int t = 0; t < QT; ++t) { launder(Xq[t][0]); launder(Xq[t][1]); }
+    bool conv = true;
+    auto row = [&](int i, double p) {
+      const double sum = quad_sum(p);
+      const double li = qbc_q(Lq[i >> 2], i);
+      const double w = -((K[i] + sum) - hii[i] * li) / hii[i];
+      const double nl = w > 0 ? w : 0.0;
+      if (!(fabs(nl - li) < cf.hild_tol)) conv = false;
+      if (!done && q == (i & 3)) Lq[i >> 2] = nl;
+    };
+    if (__all(fin || done)) {
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) {
+        double p = 0.0;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) p = p + hfast(Cn, i, Xq[t][0], Xq[t][1]) * Lq[t];
+        row(i, p);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) {
+        const double m0 = Mf(i, 0), m1 = Mf(i, 1);
+        double p = 0.0;
+#pragma unroll
+        for (int t = 0; t < QT; ++t) p = p + ((0.0 + m0 * Xq[t][0]) + m1 * Xq[t][1]) * Lq[t];
+        row(i, p);
+      }
+    }
+    if (!done && conv) {
+      done = true;
+      nexec = it;
+    }
+    if (it >= cf.max_hild) done = true;  // nexec stays max_hild
+  }
+  if (!real) return;
+  // full lambda in every lane of the quad, in column order
+  double lam[NCON];
+#pragma unroll
+  for (int j = 0; j < NCON; ++j) lam[j] = qbc_q(Lq[j >> 2], j);
+  double Mtl[NC];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) acc = acc + Mf(i, k) * lam[i];
+    Mtl[k] = acc;
+  }
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+    if (4 * t + q < NCON) s.lam[(size_t)(4 * t + q) * n + c] = Lq[t];  // iterMPC.m:68
+  if (q == 0) hild_finish(s, io, c, Cn, Mtl, nexec);
 }
 
 // ---------------------------------------------------------------------------
@@ -1982,7 +2168,11 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
 
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
   if (s.n == 0) return 0;
-  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, c, s, io);
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(s.hq_n, 0, sizeof(int), st);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, st, c, s, io);
+  if (c.hild_handoff > 0) hipLaunchKernelGGL(k_hild2, dim3(grid_for(4 * s.n, 256)), dim3(256), 0, st, c, s, io);
   return (int)hipGetLastError();
 }
 

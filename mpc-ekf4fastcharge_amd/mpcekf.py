@@ -158,7 +158,7 @@ class Context:
         ms = np.zeros(4)
         nl = (C.c_int64 * 4)()
         check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
-        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "bulk", "cell", "hild"))}
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "flush", "cell", "hild"))}
 
     def get_stamps(self):
         """k_cell section stamps of the last fused step [NSTAMPS][ncells] (profiling builds; else None)."""

@@ -430,8 +430,13 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
   for (it = 1; it <= maxIter; ++it) {
     int conv = 1;
     for (int i = 0; i < nC; ++i) {
-      double s = 0.0;
-      for (int j = 0; j < nC; ++j) s = s + H[i * HMAX + j] * lam[j];
+      /* H(i,:)*lambda (hildreth.m:35) in a defined order: 4 interleaved partial sums
+       * (terms j = q mod 4, each from +0 in ascending j) combined as (p0+p1)+(p2+p3),
+       * the order of a 4-wide SIMD dot (MATLAB's BLAS order is itself unpinned).  The
+       * kernels form the same partials in one lane or across a lane quad. */
+      double p[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];
+      double s = (p[0] + p[1]) + (p[2] + p[3]);
       double w = -((K[i] + s) - H[i * HMAX + i] * lam[i]) / H[i * HMAX + i];
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];

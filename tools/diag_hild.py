@@ -27,7 +27,7 @@ for k in range(steps):
     t = ctx.get_timing()
     ne = out["nexec"][0]
     wmax = ne.reshape(-1, 64).max(1)
-    rows.append(dict(k=k, hild_ms=t["hild"][0], cell_ms=t["cell"][0], bulk_ms=t["bulk"][0],
+    rows.append(dict(k=k, hild_ms=t["hild"][0], cell_ms=t["cell"][0], flush_ms=t["flush"][0],
                      mean=float(ne.mean()), wmax=float(wmax.mean()), frac100=float((ne == 100).mean())))
 json.dump(rows, open(sys.argv[3] if len(sys.argv) > 3 else "gpurun_out/diag_hild.json", "w"))
 a = np.array([[r["hild_ms"], r["mean"], r["wmax"]] for r in rows])

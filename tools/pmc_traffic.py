@@ -4,8 +4,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 exactly half the bytes of a wide (16 B/lane) coalesced streaming read
 (MI355X_MICROARCH.md §HBM), so reads are doubled; WRITE_SIZE is exact for
-16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,bulk,cell,hild} (bulk = the all-model
-time update: k_bulk eager / k_flush deferred) and fp64_flops_per_launch.
+16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,flush,cell,hild} (flush = the all-model
+time update of the fused path) and fp64_flops_per_launch.
 """
 import csv
 import glob
@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_plant": "plant", "k_bulk": "bulk", "k_flush": "bulk", "k_cell": "cell", "k_hild": "hild"}
+KERNELS = {"k_plant": "plant", "k_flush": "flush", "k_cell": "cell", "k_hild": "hild", "k_bulk": "bulk"}
 
 
 def read_counter(d, name):

@@ -11,9 +11,9 @@ mkdir -p $O
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/trace -o run -- \
   python3 bench.py --no-cpu > $O/bench_under_trace.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -f csv -d $O/fetch -o run -- \
-  python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_fetch.log 2>&1 && \
+  python3 bench.py --no-cpu > $O/bench_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -f csv -d $O/write -o run -- \
-  python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_write.log 2>&1 && \
+  python3 bench.py --no-cpu > $O/bench_write.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
-  -f csv -d $O/fp64 -o run -- python3 bench.py --steps 20 --warmup 2 --no-cpu > $O/bench_fp64.log 2>&1 && \
+  -f csv -d $O/fp64 -o run -- python3 bench.py --no-cpu > $O/bench_fp64.log 2>&1 && \
 python3 tools/pmc_traffic.py $O > $O/pmc_traffic.json
