@@ -197,7 +197,7 @@ int mpcekf_get_hild_problems(mpcekf_ctx *ctx, double *prob, int32_t *hflag);
 /* Profiling builds only (-DMPCEKF_STAMPS, tools/stamps.py): shader-clock stamps at the
  * MPCEKF_NSTAMPS section boundaries of the EKF/MPC kernel for the last fused step,
  * [MPCEKF_NSTAMPS][ncells].  *nstamps = 0 (and nothing written) in normal builds. */
-#define MPCEKF_NSTAMPS 9
+#define MPCEKF_NSTAMPS 12
 int mpcekf_get_stamps(mpcekf_ctx *ctx, int64_t *stamps, int32_t *nstamps);
 
 /* ---- state access (open-loop parity, checkpoint/restore) ---- */

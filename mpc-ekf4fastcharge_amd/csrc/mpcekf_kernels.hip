@@ -236,9 +236,8 @@ __device__ __forceinline__ bool is_pd5(const double a[NPK]) {
 
 // iterEKF.m:137-153 on one corner record (orc_meas_cov + state update).
 // P = Sigma - (L*St)*L' is only ever used as P + P', so only that sum is kept.
-__device__ __forceinline__ void meas_update(double *rec, const double L[NX], double St, double res) {
-  double x[NX], S[NPK];
-  load_rec(rec, x, S);
+__device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], const double L[NX], double St,
+                                                 double res) {
 #pragma unroll
   for (int k = 0; k < NX; ++k) x[k] = x[k] + L[k] * res;
   double LS[NX];
@@ -291,6 +290,12 @@ __device__ __forceinline__ void meas_update(double *rec, const double L[NX], dou
         S[pk(r, c)] = v;
       }
   }
+}
+
+__device__ __forceinline__ void meas_update(double *rec, const double L[NX], double St, double res) {
+  double x[NX], S[NPK];
+  load_rec(rec, x, S);
+  meas_update_regs(x, S, L, St, res);
   store_rec(rec, x, S);
 }
 
@@ -309,7 +314,8 @@ struct CellCtx {
 // getVariables (iterEKF.m:259-417).  Z is the permuted output vector.
 template <int NZ>
 __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, const XI &xi, double ik, double x0,
-                                           double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc) {
+                                           double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc,
+                                           const double (*xr)[NX] = nullptr) {
   double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
   double SOCnAvg = r.th0n + xSOC * (r.th100n - r.th0n);
   double SOCpAvg = r.th0p + xSOC * (r.th100p - r.th0p);
@@ -322,7 +328,12 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double x[NX];
-    load_x(cc.erec + (size_t)xi.m[j] * REC, x);
+    if (xr) {
+#pragma unroll
+      for (int k = 0; k < NX; ++k) x[k] = xr[j][k];
+    } else {
+      load_x(cc.erec + (size_t)xi.m[j] * REC, x);
+    }
     const double *Cm = cc.L + xi.m[j] * cc.stride;
     const double *Dm = Cm + NZ * NX;
     double g = xi.g[j];
@@ -1381,6 +1392,24 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
 // skipped, replayed in the per-step order of the eager update (k_bulk / the oracle),
 // so the record is bit-identical to one advanced every step.
 // ---------------------------------------------------------------------------
+// The skipped time updates of one model, steps ts+1..t (pt = the step-t input).
+__device__ __forceinline__ void replay_x(double x[NX], const double *a, int ts, int t, double pt, const KState &s,
+                                        int64_t c) {
+  for (int k = ts + 1; k <= t; ++k) {
+    const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+#pragma unroll
+    for (int e = 0; e < NX; ++e) x[e] = a[e] * x[e] + p;
+  }
+}
+__device__ __forceinline__ void replay_S(double S[NPK], const double *a, int ts, int t, double W) {
+  for (int k = ts + 1; k <= t; ++k) {
+#pragma unroll
+    for (int i = 0, pp = 0; pp < NX; ++pp)
+#pragma unroll
+      for (int q = pp; q < NX; ++q, ++i) S[i] = (a[pp] * S[i]) * a[q] + W;
+  }
+}
+
 template <int NZ>
 __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc, int NM, const int m[4], int64_t c,
                                               int t, double W) {
@@ -1496,11 +1525,41 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     double S0 = s.S0[c] + cf.SigmaW;
     const double SOC0 = s.SOC0[c];
     double SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
-    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
-    if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
     STAMP(1);
-    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
     STAMP(2);
+    // The 4 corner models stay in registers from one load to one store: xhat now,
+    // Sigma at its measurement update, each advanced over the steps its (deferred)
+    // time update skipped.  A corner repeating an earlier one (single-set-point grids)
+    // is a duplicate: the reference updates that model twice in sequence.
+    const int t = io.lazy_t;
+    bool dup[4];
+    int tsj[4];
+    double xr[4][NX];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dup[j] = false;
+#pragma unroll
+      for (int i = 0; i < j; ++i) dup[j] = dup[j] || xi.m[i] == xi.m[j];
+      load_x(cc.erec + (size_t)xi.m[j] * REC, xr[j]);
+      tsj[j] = t ? s.ts_ekf[c * r.NM + xi.m[j]] : 0;
+    }
+    const double pt = t ? s.hist_p[(size_t)(t % LAZY_H) * s.n + c] : 0.0;
+    if (t) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (!dup[j]) replay_x(xr[j], cc.L + xi.m[j] * cc.stride + NZ * NX + NZ, tsj[j], t, pt, s, c);
+#pragma unroll
+      for (int j = 1; j < 4; ++j)
+#pragma unroll
+        for (int i = j - 1; i >= 0; --i)
+          if (xi.m[i] == xi.m[j])
+#pragma unroll
+            for (int k = 0; k < NX; ++k) xr[j][k] = xr[i][k];
+    }
+    STAMP(3);
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr);
+    STAMP(4);
     if (st & ST_ERROR) {
       s.status[c] = st;
       s.warn[c] = warn;
@@ -1513,6 +1572,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     get_chatv<NZ>(r, cc, xi, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
     double S1[NPK];
     load_S(cc.erec + (size_t)xi.m[0] * REC, S1);
+    if (t) replay_S(S1, cc.L + xi.m[0] * cc.stride + NZ * NX + NZ, tsj[0], t, cf.SigmaW);
     double St[4], Lg[4][NX];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1541,21 +1601,39 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int k = 0; k < NX; ++k) launder(Lg[j][k]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    STAMP(3);
+    STAMP(5);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      meas_update(cc.erec + (size_t)xi.m[j] * REC, Lg[j], St[j], res);
+      double *rec = cc.erec + (size_t)xi.m[j] * REC;
+      double xj[NX], Sj[NPK];
+      if (dup[j]) {
+        load_rec(rec, xj, Sj);  // as the earlier update of this model left it
+      } else {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) xj[k] = xr[j][k];
+        if (j == 0) {
+#pragma unroll
+          for (int k = 0; k < NPK; ++k) Sj[k] = S1[k];
+        } else {
+          load_S(rec, Sj);
+          if (t) replay_S(Sj, cc.L + xi.m[j] * cc.stride + NZ * NX + NZ, tsj[j], t, cf.SigmaW);
+        }
+      }
+      meas_update_regs(xj, Sj, Lg[j], St[j], res);
+      store_rec(rec, xj, Sj);
+      if (t) s.ts_ekf[c * r.NM + xi.m[j]] = t;
       __builtin_amdgcn_sched_barrier(0);
     }
-    STAMP(4);
+    STAMP(6);
     x0 = x0 + L0 * res;
     S0 = S0 - L0 * St0 * L0;
     SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
     if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
+    STAMP(7);
     vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
     __builtin_amdgcn_sched_barrier(0);
-    STAMP(5);
+    STAMP(8);
     s.warn[c] = warn;
     if (st & ST_ERROR) {
       s.status[c] = st;
@@ -1652,7 +1730,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       io.zbk[c * (nz + 2) + nz + 1] = 3 * sqrt(SigSOC);
     }
 #endif
-    STAMP(6);
+    STAMP(9);
     s.x0[c] = x0;
     s.S0[c] = S0;
     s.priorI[c] = ik;  // iterEKF.m:210
@@ -1686,7 +1764,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
   }
-  STAMP(7);
+  STAMP(10);
 
 #ifndef PROBE_NO_MPC
   if (io.mode & (MODE_MPC | MODE_FUSED)) {
@@ -1713,7 +1791,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       if (io.phise) io.phise[c] = phise;
     }
     if (s.J_unc) s.J_unc[c] = o.J_unc;
-    STAMP(8);
+    STAMP(11);
     s.hflag[c] = need ? 1 : 0;
     if (need) {  // hildreth.m runs in k_hild
       double *pb = s.prob;

@@ -91,7 +91,7 @@ struct KIO {
   int lazy_t;             // > 0: fused step t of the running call with deferred time update
   long long *stamps;      // [MPCEKF_NSTAMPS][n] s_memtime per k_cell section (-DMPCEKF_STAMPS builds only)
 };
-constexpr int NSTAMPS = 9;
+constexpr int NSTAMPS = 12;
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 

@@ -205,3 +205,48 @@ def test_deferred_time_update_is_schedule_invariant(rom, M):
         np.testing.assert_array_equal(ra[k], np.concatenate([r[k] for r in rb]), err_msg=k)
     for k in ("bigX", "ekf", "scal", "lam", "warn", "status"):
         np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+
+
+def _run_with_env(M, rom, soc0, tc, steps, **env):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        with M.Context(rom, len(soc0)) as ctx:   # the overrides are read at context creation
+            ctx.init_cells(soc0, tc)
+            out = ctx.step(steps)
+            out["state"] = ctx.get_state()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return out
+
+
+def test_hildreth_phase_split_is_exact(rom, M):
+    """k_hild hands a wave's still-iterating cells to the lane-quad k_hild2 once at most
+    MPCEKF_HILD_HANDOFF lanes remain.  One phase (0), the default (16) and an immediate
+    hand-off of every QP (64) must agree bit for bit, through the infeasible-QP window
+    where cells run to maxIter."""
+    n = 1024
+    soc0, tc = batch_inputs(n, seed=21)
+    runs = [_run_with_env(M, rom, soc0, tc, 700, MPCEKF_HILD_HANDOFF=h) for h in (0, 16, 64)]
+    assert (runs[0]["nexec"] == 100).any()       # the maxIter window is exercised
+    for r in runs[1:]:
+        for k in ("u", "v", "soc", "phise", "nexec"):
+            np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
+        np.testing.assert_array_equal(r["state"]["lam"], runs[0]["state"]["lam"])
+
+
+def test_flush_period_is_exact(rom, M):
+    """The deferred time update gives the same bits for any flush period <= the ring."""
+    n = 1024
+    soc0, tc = batch_inputs(n, seed=22)
+    runs = [_run_with_env(M, rom, soc0, tc, 300, MPCEKF_FLUSH_PERIOD=p) for p in (32, 1, 7)]
+    for r in runs[1:]:
+        for k in ("u", "v", "soc", "phise", "nexec"):
+            np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
+        for k in ("ekf", "bigX"):
+            np.testing.assert_array_equal(r["state"][k], runs[0]["state"][k], err_msg=k)
