@@ -14,7 +14,10 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_plant": "plant", "k_flush": "flush", "k_cell": "cell", "k_hild": "hild", "k_bulk": "bulk"}
+# kernel (exact name prefix) -> bench stage; a stage's per-step figure is the sum of
+# its kernels' per-dispatch averages (each launches once per step)
+KERNELS = {"k_plant(": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild2(": "hild",
+           "k_bulk(": "bulk"}
 
 
 def read_counter(d, name):
@@ -25,10 +28,14 @@ def read_counter(d, name):
                 if row.get("Counter_Name") != name:
                     continue
                 kn = row.get("Kernel_Name", "")
-                for k, short in KERNELS.items():
-                    if k in kn:
-                        vals[short].append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items() if v}
+                for k in KERNELS:
+                    if ("mk::" + k) in kn or (" " + k) in kn or kn.startswith(k):
+                        vals[k].append(float(row["Counter_Value"]))
+    stage = defaultdict(float)
+    for k, v in vals.items():
+        if v:
+            stage[KERNELS[k]] += sum(v) / len(v)
+    return dict(stage)
 
 
 def main():
