@@ -73,7 +73,6 @@ struct mpcekf_ctx {
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
-  int *d_hq = nullptr;            // Hildreth phase-2 queue [n] + its length
   int flush_period = LAZY_H;      // steps between all-model flushes (<= LAZY_H)
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
@@ -351,7 +350,6 @@ static void fill_kcfg(const mpcekf_config *c, double Q, KCfg &k) {
   k.max_warn = c->max_warn;
   k.max_hild = c->max_hild;
   k.flags = c->flags;
-  k.hild_handoff = HILD_HANDOFF;
 }
 
 int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int device, int64_t ncells,
@@ -372,15 +370,11 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   X->ncon = NCON_BUILT;
   if ((rc = build_rom(X, rom))) { mpcekf_ctx_destroy(X); return rc; }
   fill_kcfg(cfg, rom->Q, X->k);
-  // Diagnostic overrides (tests/test_gpu_parity.py shows results do not depend on them):
-  // MPCEKF_FLUSH_PERIOD in [1, LAZY_H], MPCEKF_HILD_HANDOFF in [0, 64] (0 = one phase).
+  // Diagnostic override (tests/test_gpu_parity.py shows results do not depend on it):
+  // MPCEKF_FLUSH_PERIOD in [1, LAZY_H].
   if (const char *e = std::getenv("MPCEKF_FLUSH_PERIOD")) {
     const int v = std::atoi(e);
     if (v >= 1 && v <= LAZY_H) X->flush_period = v;
-  }
-  if (const char *e = std::getenv("MPCEKF_HILD_HANDOFF")) {
-    const int v = std::atoi(e);
-    if (v >= 0 && v <= 64) X->k.hild_handoff = v;
   }
   X->Tref = rom->Tref;
   X->Rgas = rom->R;
@@ -398,8 +392,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
       (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
-      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2)) ||
-      (rc = dalloc(&X->d_hq, 2 * n + 1))
+      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))
 #ifdef MPCEKF_STAMPS
       || (rc = dalloc(&X->d_stamps, n * NSTAMPS))
 #endif
@@ -414,7 +407,6 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.prob = X->d_prob;
   s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
-  s.hq = X->d_hq; s.hq_it = X->d_hq + n; s.hq_n = X->d_hq + 2 * n;
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
   s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
@@ -428,7 +420,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_hq};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);

@@ -807,6 +807,22 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
     for (int k = 0; k < NC; ++k) s = s + Mf(i, k) * y[k];
     K[i] = s + gam[i];
   }
+  bool fin = true;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) fin = fin && isfinite(X[i][k]) && isfinite(Mf(i, k));
+  // orc_hildreth's defined evaluation: rank-Nc form with v = X*lambda when X and M are
+  // finite, else the dense H(i,:)*lambda as 4 interleaved partial sums
+  auto xv = [&](double v[NC]) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCON; ++j) a = a + X[j][k] * lam[j];
+      v[k] = a;
+    }
+  };
   int it;
   for (it = 1; it <= maxIter; ++it) {
 #pragma unroll
@@ -814,23 +830,41 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
 #pragma unroll
       for (int k = 0; k < NC; ++k) launder(X[i][k]);
     bool conv = true;
+    double v[NC];
+    if (fin) xv(v);
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
-      double p4[4] = {0.0, 0.0, 0.0, 0.0}, hii = 0.0;
+      double hii = 0.0;
 #pragma unroll
-      for (int j = 0; j < NCON; ++j) {
-        double h = 0.0;
+      for (int k = 0; k < NC; ++k) hii = hii + Mf(i, k) * X[i][k];
+      double s = 0.0;
+      if (fin) {
 #pragma unroll
-        for (int k = 0; k < NC; ++k) h = h + Mf(i, k) * X[j][k];
-        if (j == i) hii = h;
-        p4[j & 3] = p4[j & 3] + h * lam[j];
+        for (int k = 0; k < NC; ++k) s = s + Mf(i, k) * v[k];
+      } else {
+        double p4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < NCON; ++j) {
+          double h = 0.0;
+#pragma unroll
+          for (int k = 0; k < NC; ++k) h = h + Mf(i, k) * X[j][k];
+          p4[j & 3] = p4[j & 3] + h * lam[j];
+        }
+        s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
       }
-      const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);  // orc_hildreth's defined order
       double w = -((K[i] + s) - hii * lam[i]) / hii;
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = false;
       lam[i] = nl;
+      if (fin) {
+        if (isfinite(d)) {
+#pragma unroll
+          for (int k = 0; k < NC; ++k) v[k] = v[k] + X[i][k] * d;
+        } else {
+          xv(v);
+        }
+      }
     }
     if (conv) break;
   }
@@ -1008,40 +1042,6 @@ __device__ __forceinline__ double xval(const XS &X, int j, int k) {
   }
 }
 
-// h(i,j) = M(i,:)*X(:,j) when every operand is finite, exact up to the sign of
-// a zero result: the dense form (0 + m0*x0) + m1*x1 differs from these only
-// when a partial result is a signed zero.  A zero h(i,j) only ever feeds
-// h(i,j)*lambda(j) (+-0, or NaN for lambda = inf either way) added to a partial
-// sum that starts at +0 and so is never -0: the sum is bit-identical.
-__device__ __forceinline__ double hfast(const Cons &C, int i, double x0, double x1) {
-  switch (i) {  // the constant rows [Cu; -Cu; I; -I] for NC == 2
-    case 0: case 4: return x0;
-    case 1: return x0 + x1;
-    case 2: case 6: return -x0;
-    case 3: return -(x0 + x1);
-    case 5: return x1;
-    case 7: return -x1;
-    default: break;
-  }
-  const int r = (i - 4 * NC) % NP;  // Toeplitz row r of G_v / -G_e / G_soc: M(i,2) == +-0 when r == 0
-  if (r == 0) return mval(C, i, 0) * x0;
-  return mval(C, i, 0) * x0 + mval(C, i, 1) * x1;
-}
-
-// Register-resident sweep, rows and columns unrolled at compile time so lambda,
-// K and X never leave VGPRs, and straight-line (no per-term branches: a
-// wave-uniform skip test costs more than the two DP ops it saves).  Every term
-// H(i,j)*lambda(j) is kept, in the order of hildreth.m:35; while every live
-// lane of the wave is finite, H(i,j) is formed by hfast (for the constant
-// columns +-E\[1;0], +-E\[1;1], +-E\[0;1] only three values per row, negated
-// exactly); a wave holding a non-finite lane uses the dense formula.
-//
-// A lane that has converged stays in the loop with its lambda and sweep count
-// frozen (selects, not a per-lane exit) until the whole wave is done: on MI355X a
-// wave whose EXEC holds fewer than 16 lanes issues FP64 VALU up to 2.6x slower
-// under full-chip load (tools/micro/exec_micro.hip), and Hildreth's convergence
-// is very uneven across cells.  `done` = true makes a lane a passenger from the
-// start (no QP this step: its operands are a finite dummy and nothing is kept).
 // X = E\M' in compressed form (hildreth.m:25); fin = every X and M entry finite.
 __device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], XS &Xs, bool &fin) {
   ConsM Mf{Cn};
@@ -1066,78 +1066,198 @@ __device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], X
     fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
 }
 
-// Returns hildreth.m's nexec when the lane finished (converged, or maxIter sweeps
-// done), or -(sweeps done) - 1 when the wave thinned out to at most `handoff`
-// iterating lanes first (handoff > 0): k_hild2 continues such a cell from its
-// stored lambda.
+// v = X*lambda (orc_hildreth's hild_v: sums from +0 in ascending j)
+__device__ __forceinline__ void hild_v(const XS &Xs, const double L[NCON], double &v0, double &v1) {
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NCON; ++j) {
+    a0 = a0 + xval(Xs, j, 0) * L[j];
+    a1 = a1 + xval(Xs, j, 1) * L[j];
+  }
+  v0 = a0;
+  v1 = a1;
+}
+
+// x / y, correctly rounded, with the divisor-only part of the hardware division
+// sequence (v_rcp_f64 + two Newton steps) independent of x, so it overlaps the
+// sweep's serial chain.  For |x|, |y| in [2^-400, 2^400] (or x == 0)
+// v_div_scale / v_div_fmas / v_div_fixup are identities and this is bit-identical
+// to the compiled x / y (tools/micro/div_check.hip: 2.1e9 random pairs, 0
+// mismatches); y == +-0 gives x * (1/y) = x / y exactly (inf / NaN by IEEE).  The
+// caller checks the domain (div_y_ok once per divisor, the x range per sweep).
+__device__ __forceinline__ double div_fast(double x, double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  const double r0 = r;
+  double e = __builtin_fma(-y, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-y, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q0 = x * r;
+  const double e2 = __builtin_fma(-y, q0, x);
+  const double q = __builtin_fma(e2, r, q0);
+  return y == 0.0 ? x * r0 : q;
+}
+__device__ __forceinline__ bool div_y_ok(double y) {
+  const double ay = fabs(y);
+  return y == 0.0 || (ay >= 0x1p-400 && ay <= 0x1p400);
+}
+
+// One rank-2 sweep (orc_hildreth): H(i,:)*lambda = M(i,:)*v with v = X*lambda
+// recomputed at the sweep start and updated after every row.  CAREFUL = false is
+// the straight-line form (v += X(:,i)*d always, div_fast) that flags in `bad` a
+// non-finite d or an operand outside div_fast's domain; CAREFUL = true is the
+// exact rule for those cases (plain division; v recomputed from lambda after a
+// non-finite d).
+template <bool CAREFUL>
+__device__ __forceinline__ void sweep_rank2(const Cons &Cn, const XS &Xs, const double K[NCON], double L[NCON],
+                                            bool done, double tol, bool &conv, bool &bad) {
+  ConsM Mf{Cn};
+  double v0, v1;
+  hild_v(Xs, L, v0, v1);
+  // domain / finiteness accumulators of the straight-line form, off the serial chain
+  double xmax = 0.0, xmin = 1.0, chk = 0.0;
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    const double m0 = Mf(i, 0), m1 = Mf(i, 1);
+    const double hii = (0.0 + m0 * xval(Xs, i, 0)) + m1 * xval(Xs, i, 1);
+    const double sv = (0.0 + m0 * v0) + m1 * v1;
+    const double li = L[i];
+    const double num = -((K[i] + sv) - hii * li);
+    double w;
+    if (CAREFUL) {
+      w = num / hii;
+    } else {
+      w = div_fast(num, hii);
+      const double xa = fabs(num);
+      xmax = fmax(xmax, xa);
+      xmin = fmin(xmin, num == 0.0 ? 1.0 : xa);
+    }
+    const double nl = w > 0 ? w : 0.0;
+    if (!(fabs(nl - li) < tol)) conv = false;
+    const double nli = done ? li : nl;
+    const double d = nli - li;
+    L[i] = nli;
+    if (CAREFUL && !isfinite(d)) {
+      hild_v(Xs, L, v0, v1);
+    } else {
+      v0 = v0 + xval(Xs, i, 0) * d;
+      v1 = v1 + xval(Xs, i, 1) * d;
+    }
+    if (!CAREFUL) chk = chk + (d - d);  // NaN once any d is inf or NaN
+  }
+  if (!CAREFUL) bad = !(chk == 0.0 && xmax <= 0x1p400 && xmin >= 0x1p-400);
+}
+
+// The dense sweep for lanes with a non-finite X or M entry (orc_hildreth): H(i,:)*lambda
+// as 4 interleaved partial sums combined as (p0 + p1) + (p2 + p3).
+__device__ __forceinline__ void sweep_dense(const Cons &Cn, const XS &Xs, const double K[NCON], double L[NCON],
+                                            bool done, double tol, bool &conv) {
+  ConsM Mf{Cn};
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    const double m0 = Mf(i, 0), m1 = Mf(i, 1);
+    double p4[4] = {0.0, 0.0, 0.0, 0.0}, hii = 0.0;
+#pragma unroll
+    for (int j = 0; j < NCON; ++j) {
+      const double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
+      if (j == i) hii = h;
+      p4[j & 3] = p4[j & 3] + h * L[j];
+    }
+    const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+    const double li = L[i];
+    const double w = -((K[i] + s) - hii * li) / hii;
+    const double nl = w > 0 ? w : 0.0;
+    if (!(fabs(nl - li) < tol)) conv = false;
+    L[i] = done ? li : nl;
+  }
+}
+
+// hildreth.m:32-44 for one lane; returns nexec.  Every lane of the wave stays in each
+// loop until all are done (a converged lane freezes lambda): on MI355X a wave whose
+// EXEC holds fewer than 16 lanes issues FP64 VALU up to 2.6x slower under full-chip
+// load (tools/micro/exec_micro.hip).  `done` = true makes a lane a passenger from the
+// start (no QP this step: a finite dummy problem, nothing kept).
+//
+// Three loops, so the hot one carries nothing else (register pressure):
+//  1. the straight-line rank-2 sweep (sweep_rank2<false>) for lanes with finite X, M;
+//  2. lanes whose sweep flagged a non-finite d or an operand outside div_fast's
+//     domain restart from their warm start L0 (global) with the exact rules
+//     (sweep_rank2<true>): every sweep before the flag was bit-identical to the exact
+//     form, so the result is the exact form's;
+//  3. lanes with a non-finite X or M entry: the dense sweep.
 __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
-                                              int handoff, double tol, const double K[NCON], double Mtl[NC],
-                                              bool done) {
+                                              double tol, const double K[NCON], double Mtl[NC], bool done,
+                                              const double *L0, int64_t l0_stride) {
   static_assert(NC == 2, "written for Nc = 2");
   ConsM Mf{Cn};
   XS Xs;
   bool fin;
   hild_x(Cn, E, Xs, fin);
   int nexec = maxIter;
-#pragma unroll 1
-  for (int it = 1; it <= maxIter; ++it) {
-    const int active = __popcll(__ballot(!done));
-    if (active == 0) break;
-    if (active <= handoff) {
-      if (!done) nexec = -it;  // it - 1 sweeps done
-      break;
-    }
-    // opaque per sweep: stops the entries of H being hoisted out of the loop (and spilled)
+  bool careful = false;
+  if (fin && !done) {
+    bool yok = true;
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) yok = yok && div_y_ok((0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1));
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) yok = yok && isfinite(L[i]);
+    careful = !yok;
+  }
+  auto launder_x = [&]() {  // opaque per sweep: stops loop-invariant H entries being hoisted
 #pragma unroll
     for (int k = 0; k < NC; ++k) {
       launder(Xs.a[k]); launder(Xs.b[k]); launder(Xs.c[k]);
 #pragma unroll
       for (int i = 0; i < 3 * NP; ++i) launder(Xs.t[i][k]);
     }
-    bool conv = true;
-    if (__all(fin || done)) {
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) {
-        const double hii = (0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1);
-        const double ha = hfast(Cn, i, Xs.a[0], Xs.a[1]);
-        const double hb = hfast(Cn, i, Xs.b[0], Xs.b[1]);
-        const double hc = hfast(Cn, i, Xs.c[0], Xs.c[1]);
-        const double hconst[4 * NC] = {ha, hb, -ha, -hb, ha, hc, -ha, -hc};
-        double p4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int j = 0; j < NCON; ++j) {
-          const double h = j < 4 * NC ? hconst[j] : hfast(Cn, i, Xs.t[j - 4 * NC][0], Xs.t[j - 4 * NC][1]);
-          p4[j & 3] = p4[j & 3] + h * L[j];
-        }
-        const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-        const double li = L[i];
-        const double w = -((K[i] + s) - hii * li) / hii;
-        const double nl = w > 0 ? w : 0.0;
-        if (!(fabs(nl - li) < tol)) conv = false;
-        L[i] = done ? li : nl;
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) {
-        const double m0 = Mf(i, 0), m1 = Mf(i, 1);
-        double p4[4] = {0.0, 0.0, 0.0, 0.0}, hii = 0.0;
-#pragma unroll
-        for (int j = 0; j < NCON; ++j) {
-          const double h = (0.0 + m0 * xval(Xs, j, 0)) + m1 * xval(Xs, j, 1);
-          if (j == i) hii = h;
-          p4[j & 3] = p4[j & 3] + h * L[j];
-        }
-        const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-        const double li = L[i];
-        const double w = -((K[i] + s) - hii * li) / hii;
-        const double nl = w > 0 ? w : 0.0;
-        if (!(fabs(nl - li) < tol)) conv = false;
-        L[i] = done ? li : nl;
+  };
+  {
+    bool fdone = done || !fin || careful;
+#pragma unroll 1
+    for (int it = 1; it <= maxIter; ++it) {
+      if (__all(fdone)) break;
+      launder_x();
+      bool conv = true, bad = false;
+      sweep_rank2<false>(Cn, Xs, K, L, fdone, tol, conv, bad);
+      if (!fdone && bad) {
+        fdone = true;
+        careful = true;
+      } else if (!fdone && conv) {
+        fdone = true;
+        nexec = it;
       }
     }
-    if (!done && conv) {
-      done = true;
-      nexec = it;
+  }
+  if (__any(careful)) {
+    bool cdone = !careful;
+    if (careful) {
+#pragma unroll
+      for (int j = 0; j < NCON; ++j) L[j] = L0[j * l0_stride];
+    }
+#pragma unroll 1
+    for (int it = 1; it <= maxIter; ++it) {
+      if (__all(cdone)) break;
+      launder_x();
+      bool conv = true, bad = false;
+      sweep_rank2<true>(Cn, Xs, K, L, cdone, tol, conv, bad);
+      if (!cdone && conv) {
+        cdone = true;
+        nexec = it;
+      }
+    }
+  }
+  if (__any(!fin && !done)) {
+    bool ddone = done || fin;
+#pragma unroll 1
+    for (int it = 1; it <= maxIter; ++it) {
+      if (__all(ddone)) break;
+      launder_x();
+      bool conv = true;
+      sweep_dense(Cn, Xs, K, L, ddone, tol, conv);
+      if (!ddone && conv) {
+        ddone = true;
+        nexec = it;
+      }
     }
   }
 #pragma unroll
@@ -1830,7 +1950,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 }
 
 // ---------------------------------------------------------------------------
-// k_hild / k_hild2: hildreth.m + iterMPC.m:68-95 for the cells k_cell flagged
+// k_hild: hildreth.m + iterMPC.m:68-95 for the cells k_cell flagged
 // ---------------------------------------------------------------------------
 // The QP record of cell c (PB_*) -> Cons, E and K = M*(E\F) + gamma (hildreth.m:29).
 __device__ __forceinline__ void hild_load(const KState &s, int64_t c, Cons &Cn, double E[NC][NC], double K[NCON]) {
@@ -1912,8 +2032,7 @@ __device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int6
   }
 }
 
-// Phase 1: lane per cell while the wave is dense; the cells still iterating when at
-// most cf.hild_handoff lanes remain are queued for k_hild2.
+// hildreth.m + iterMPC.m:68-95, lane per cell.
 __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
@@ -1933,160 +2052,11 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
     for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
   }
   double Mtl[NC];
-  const int nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_handoff, cf.hild_tol, K, Mtl, !qp);
-  // queue the cells handed off to k_hild2: one atomic per wave
-  const bool enq = qp && nexec < 0;
-  const unsigned long long bal = __ballot(enq);
-  if (bal) {
-    const int leader = __ffsll((long long)bal) - 1;
-    int base = 0;
-    if ((int)__lane_id() == leader) base = atomicAdd(s.hq_n, __popcll(bal));
-    base = __shfl(base, leader);
-    if (enq) {
-      const int slot = base + __popcll(bal & ((1ull << __lane_id()) - 1));
-      s.hq[slot] = (int)c;
-      s.hq_it[slot] = -nexec - 1;
-    }
-  }
+  const int nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp, s.lam + c, n);
   if (!qp) return;
 #pragma unroll
   for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
-  if (enq) return;
   hild_finish(s, io, c, Cn, Mtl, nexec);
-}
-
-// v from the quad lane selected by DPP quad_perm control CTRL.
-template <int CTRL>
-__device__ __forceinline__ double qperm(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-
-// Broadcast lane Q's value of v to its quad (DPP quad_perm [Q,Q,Q,Q]).
-template <int Q>
-__device__ __forceinline__ double qbc(double v) {
-  constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)b, ctrl, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctrl, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-__device__ __forceinline__ double qbc_q(double v, int q) {  // q folds to a constant after unrolling
-  switch (q & 3) {
-    case 0: return qbc<0>(v);
-    case 1: return qbc<1>(v);
-    case 2: return qbc<2>(v);
-    default: return qbc<3>(v);
-  }
-}
-
-// (p0 + p1) + (p2 + p3) of a quad's partials in every lane of the quad, by two
-// butterfly steps: lanes 0/1 form p0+p1 (= p1+p0: IEEE addition commutes), 2/3 form
-// p2+p3, then each adds the other pair's sum.
-__device__ __forceinline__ double quad_sum(double p) {
-  const double t = p + qperm<1 | (0 << 2) | (3 << 4) | (2 << 6)>(p);   // quad_perm [1,0,3,2]
-  return t + qperm<2 | (3 << 2) | (0 << 4) | (1 << 6)>(t);              // quad_perm [2,3,0,1]
-}
-
-constexpr int QT = (NCON + 3) / 4;  // terms per lane of a quad
-
-// Phase 2: a lane quad per queued cell continues hildreth.m from its next sweep.
-// Lane q of the quad owns the columns j = q mod 4 (X and lambda in registers at slot
-// j / 4) and forms partial sum p_q of H(i,:)*lambda; every lane then combines the
-// four partials as (p0 + p1) + (p2 + p3) (quad_sum) -- orc_hildreth's order,
-// identical to the one-lane form of k_hild -- so all four lanes hold the same w,
-// lambda(i) and convergence flag and need no further exchange.
-__global__ void __launch_bounds__(256) k_hild2(const KCfg cf, const KState s, const KIO io) {
-  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int count = *s.hq_n;
-  if (((gt & ~63ll) >> 2) >= count) return;  // no queued cell in this wave
-  const int q = (int)(gt & 3);
-  const int64_t g = gt >> 2;
-  const bool real = g < count;
-  const int64_t c = real ? s.hq[g] : 0;
-  const int it0 = real ? s.hq_it[g] : cf.max_hild;
-  const int64_t n = s.n;
-  Cons Cn;
-  double E[NC][NC], K[NCON];
-  if (real) hild_load(s, c, Cn, E, K);
-  else hild_dummy(Cn, E, K);
-  ConsM Mf{Cn};
-  XS Xs;
-  bool fin;
-  hild_x(Cn, E, Xs, fin);
-  double hii[NCON];
-#pragma unroll
-  for (int i = 0; i < NCON; ++i) hii[i] = (0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1);
-  double Xq[QT][NC], Lq[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) { Xq[t][0] = Xq[t][1] = 0.0; Lq[t] = 0.0; }
-#pragma unroll
-  for (int j = 0; j < NCON; ++j)
-    if ((j & 3) == q) {
-      Xq[j >> 2][0] = xval(Xs, j, 0);
-      Xq[j >> 2][1] = xval(Xs, j, 1);
-      if (real) Lq[j >> 2] = s.lam[(size_t)j * n + c];
-    }
-  bool done = !real || it0 >= cf.max_hild;
-  int nexec = cf.max_hild;
-  int it = it0;
-#pragma unroll 1
-  while (!__all(done)) {
-    ++it;
-#pragma unroll
-    for (int t = 0; t < QT; ++t) { launder(Xq[t][0]); launder(Xq[t][1]); }
-    bool conv = true;
-    auto row = [&](int i, double p) {
-      const double sum = quad_sum(p);
-      const double li = qbc_q(Lq[i >> 2], i);
-      const double w = -((K[i] + sum) - hii[i] * li) / hii[i];
-      const double nl = w > 0 ? w : 0.0;
-      if (!(fabs(nl - li) < cf.hild_tol)) conv = false;
-      if (!done && q == (i & 3)) Lq[i >> 2] = nl;
-    };
-    if (__all(fin || done)) {
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) {
-        double p = 0.0;
-#pragma unroll
-        for (int t = 0; t < QT; ++t) p = p + hfast(Cn, i, Xq[t][0], Xq[t][1]) * Lq[t];
-        row(i, p);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) {
-        const double m0 = Mf(i, 0), m1 = Mf(i, 1);
-        double p = 0.0;
-#pragma unroll
-        for (int t = 0; t < QT; ++t) p = p + ((0.0 + m0 * Xq[t][0]) + m1 * Xq[t][1]) * Lq[t];
-        row(i, p);
-      }
-    }
-    if (!done && conv) {
-      done = true;
-      nexec = it;
-    }
-    if (it >= cf.max_hild) done = true;  // nexec stays max_hild
-  }
-  if (!real) return;
-  // full lambda in every lane of the quad, in column order
-  double lam[NCON];
-#pragma unroll
-  for (int j = 0; j < NCON; ++j) lam[j] = qbc_q(Lq[j >> 2], j);
-  double Mtl[NC];
-#pragma unroll
-  for (int k = 0; k < NC; ++k) {
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) acc = acc + Mf(i, k) * lam[i];
-    Mtl[k] = acc;
-  }
-#pragma unroll
-  for (int t = 0; t < QT; ++t)
-    if (4 * t + q < NCON) s.lam[(size_t)(4 * t + q) * n + c] = Lq[t];  // iterMPC.m:68
-  if (q == 0) hild_finish(s, io, c, Cn, Mtl, nexec);
 }
 
 // ---------------------------------------------------------------------------
@@ -2246,11 +2216,7 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
 
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
   if (s.n == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(s.hq_n, 0, sizeof(int), st);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, st, c, s, io);
-  if (c.hild_handoff > 0) hipLaunchKernelGGL(k_hild2, dim3(grid_for(4 * s.n, 256)), dim3(256), 0, st, c, s, io);
+  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, c, s, io);
   return (int)hipGetLastError();
 }
 

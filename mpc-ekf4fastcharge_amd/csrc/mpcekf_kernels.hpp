@@ -44,7 +44,6 @@ struct KRom {
 struct KCfg {
   double SigmaV, SigmaW, ref, u_max, u_min, du_min, du_max, v_max, phise_min, zmax, hild_tol;
   int max_warn, max_hild, flags;
-  int hild_handoff;  // k_hild hands a wave's cells to k_hild2 once at most this many still iterate
 };
 
 struct KState {
@@ -67,12 +66,7 @@ struct KState {
   // of the last LAZY_H steps sit in per-cell rings
   int *ts_ekf, *ts_plant;    // [n][NM]
   double *hist_p, *hist_u;   // [LAZY_H][n] priorI (EKF) and Iapp (plant) of step t at slot t % LAZY_H
-  // Hildreth phase 2: cells still iterating when their wave thinned out (k_hild -> k_hild2)
-  int *hq;                   // [n] queued cell indices
-  int *hq_it;                // [n] sweeps already done
-  int *hq_n;                 // queue length
 };
-constexpr int HILD_HANDOFF = 16;  // default KCfg::hild_handoff
 
 // Inputs/outputs of one cell-kernel launch.  Any pointer may be null.
 struct KIO {

@@ -405,6 +405,15 @@ void orc_predmat(const double *a /*6*/, const double *C /*6*/, double D, int Np,
 /* ----------------------------------------------------------------------- */
 /* hildreth.m                                                               */
 /* ----------------------------------------------------------------------- */
+/* v = X*lambda, X(:,j) = E\M(j,:)' stored row j of X[] (sums from +0, ascending j) */
+static void hild_v(int Nc, int nC, const double *X, const double *lam, double *v) {
+  for (int k = 0; k < Nc; ++k) {
+    double a = 0.0;
+    for (int j = 0; j < nC; ++j) a = a + X[j * Nc + k] * lam[j];
+    v[k] = a;
+  }
+}
+
 int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double *M /*nC x Nc*/,
                  const double *gam, double *lam /*in: warm start, out*/, int maxIter, double tol,
                  double *DU) {
@@ -426,22 +435,44 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
     for (int k = 0; k < Nc; ++k) s = s + M[i * Nc + k] * y[k];
     K[i] = s + gam[i];
   }
+  /* H = M*X has rank Nc: H(i,:)*lambda = M(i,:)*v with v = X*lambda (an Nc-vector).
+   * Defined evaluation (the kernels evaluate the same sequence):
+   *  - finite X and M: v recomputed from lambda at the start of every sweep (sums from
+   *    +0 in ascending j), s_i = M(i,:)*v, and after row i v += X(:,i)*(new - old
+   *    lambda(i)); when that change is not finite (a zero-diagonal row going to or
+   *    from +inf) v is recomputed from lambda instead, which reproduces the dense
+   *    form's inf/NaN propagation (0*inf terms) exactly in kind.
+   *  - otherwise the dense H(i,:)*lambda as 4 interleaved partial sums (terms j = q
+   *    mod 4 from +0) combined as (p0+p1)+(p2+p3).
+   * MATLAB's own BLAS order for H(i,:)*lambda is unpinned; the math is hildreth.m:35. */
+  int finite = 1;
+  for (int i = 0; i < nC * Nc; ++i) finite = finite && isfinite(X[i]) && isfinite(M[i]);
   int it = 0;
   for (it = 1; it <= maxIter; ++it) {
     int conv = 1;
+    double v[NCMAX];
+    if (finite) hild_v(Nc, nC, X, lam, v);
     for (int i = 0; i < nC; ++i) {
-      /* H(i,:)*lambda (hildreth.m:35) in a defined order: 4 interleaved partial sums
-       * (terms j = q mod 4, each from +0 in ascending j) combined as (p0+p1)+(p2+p3),
-       * the order of a 4-wide SIMD dot (MATLAB's BLAS order is itself unpinned).  The
-       * kernels form the same partials in one lane or across a lane quad. */
-      double p[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];
-      double s = (p[0] + p[1]) + (p[2] + p[3]);
+      double s;
+      if (finite) {
+        s = 0.0;
+        for (int k = 0; k < Nc; ++k) s = s + M[i * Nc + k] * v[k];
+      } else {
+        double p[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];
+        s = (p[0] + p[1]) + (p[2] + p[3]);
+      }
       double w = -((K[i] + s) - H[i * HMAX + i] * lam[i]) / H[i * HMAX + i];
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = 0;
       lam[i] = nl;
+      if (finite) {
+        if (isfinite(d))
+          for (int k = 0; k < Nc; ++k) v[k] = v[k] + X[i * Nc + k] * d;
+        else
+          hild_v(Nc, nC, X, lam, v);
+      }
     }
     if (conv) break;
   }

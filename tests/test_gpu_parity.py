@@ -225,21 +225,6 @@ def _run_with_env(M, rom, soc0, tc, steps, **env):
     return out
 
 
-def test_hildreth_phase_split_is_exact(rom, M):
-    """k_hild hands a wave's still-iterating cells to the lane-quad k_hild2 once at most
-    MPCEKF_HILD_HANDOFF lanes remain.  One phase (0), the default (16) and an immediate
-    hand-off of every QP (64) must agree bit for bit, through the infeasible-QP window
-    where cells run to maxIter."""
-    n = 1024
-    soc0, tc = batch_inputs(n, seed=21)
-    runs = [_run_with_env(M, rom, soc0, tc, 700, MPCEKF_HILD_HANDOFF=h) for h in (0, 16, 64)]
-    assert (runs[0]["nexec"] == 100).any()       # the maxIter window is exercised
-    for r in runs[1:]:
-        for k in ("u", "v", "soc", "phise", "nexec"):
-            np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
-        np.testing.assert_array_equal(r["state"]["lam"], runs[0]["state"]["lam"])
-
-
 def test_flush_period_is_exact(rom, M):
     """The deferred time update gives the same bits for any flush period <= the ring."""
     n = 1024

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256) k_micro(const double *pr, int nprob, int 
   }
   double Mtl[NC];
   long long t0 = clock64(), r0 = wall_clock64();
-  int it = hildreth_sweep(Cn, E, L, maxIter, 0, tol, K, Mtl, false);
+  int it = hildreth_sweep(Cn, E, L, maxIter, tol, K, Mtl, false, p + 44, 1);
   long long t1 = clock64(), r1 = wall_clock64();
   for (int i = 0; i < NCON; ++i) lam_out[c * NCON + i] = L[i];
   nexec[c] = it;
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256) k_probe(const KCfg cf, const KState s, in
   for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
   double Mtl[NC];
   long long t0 = clock64(), r0 = wall_clock64();
-  int it = hildreth_sweep(Cn, E, lam, cf.max_hild, 0, cf.hild_tol, K, Mtl, !qp);
+  int it = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp, s.lam + c, n);
   long long t1 = clock64(), r1 = wall_clock64();
   if (!qp) return;
   it_out[c] = it;
@@ -130,9 +130,6 @@ static bool load_state(const char *path, Replay &R) {
   KState st{};
   st.n = n; st.prob = R.dprob; st.lam = R.dlam; st.hflag = R.dhf; st.uk_1 = R.duk1; st.uk = R.duk; st.J_fin = R.djf;
   st.nviol = R.dnv; st.J_unc = R.djf;
-  hipMalloc(&st.hq, (2 * n + 1) * sizeof(int));
-  st.hq_it = st.hq + n;
-  st.hq_n = st.hq + 2 * n;
   R.st = st;
   return true;
 }
@@ -144,44 +141,23 @@ static int ab_mode(int nfiles, char **files, int reps) {
   KCfg cf{};
   cf.max_hild = 100;
   cf.hild_tol = 1e-6;
-  cf.hild_handoff = getenv("HILD_T") ? atoi(getenv("HILD_T")) : HILD_HANDOFF;
-  printf("hild_handoff = %d\n", cf.hild_handoff);
   KIO io{};
   io.mode = MODE_FUSED;
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   std::vector<std::vector<float>> t(nfiles);
-  hipEvent_t e2;
-  hipEventCreate(&e2);
-  std::vector<std::vector<float>> t1(nfiles), t2(nfiles);
-  std::vector<int> qn(nfiles);
   for (int r = 0; r < reps; ++r)
     for (int i = 0; i < nfiles; ++i) {
       hipMemcpy(R[i].dlam, R[i].dlam0, (size_t)NCON * R[i].n * 8, hipMemcpyDeviceToDevice);
-      hipMemset(R[i].st.hq_n, 0, sizeof(int));
       hipEventRecord(e0);
-      hipLaunchKernelGGL(k_hild, dim3((R[i].n + 255) / 256), dim3(256), 0, 0, cf, R[i].st, io);
-      hipEventRecord(e2);
-      hipLaunchKernelGGL(k_hild2, dim3((4 * R[i].n + 255) / 256), dim3(256), 0, 0, cf, R[i].st, io);
+      launch_hild(cf, R[i].st, io, nullptr);
       hipEventRecord(e1);
       hipEventSynchronize(e1);
-      float ms, ms1, ms2;
+      float ms;
       hipEventElapsedTime(&ms, e0, e1);
-      hipEventElapsedTime(&ms1, e0, e2);
-      hipEventElapsedTime(&ms2, e2, e1);
       t[i].push_back(ms);
-      t1[i].push_back(ms1);
-      t2[i].push_back(ms2);
-      hipMemcpy(&qn[i], R[i].st.hq_n, sizeof(int), hipMemcpyDeviceToHost);
     }
-  for (int i = 0; i < nfiles; ++i) {
-    std::vector<float> a = t1[i], b = t2[i];
-    std::sort(a.begin(), a.end());
-    std::sort(b.begin(), b.end());
-    printf("%s: phase 1 median %.4f ms, phase 2 median %.4f ms, queued cells %d\n", files[i], a[a.size() / 2],
-           b[b.size() / 2], qn[i]);
-  }
   for (int i = 0; i < nfiles; ++i) {
     std::vector<float> v = t[i];
     std::sort(v.begin(), v.end());
@@ -249,13 +225,9 @@ static int state_mode(const char *path, const char *out) {
   KCfg cf{};
   cf.max_hild = 100;
   cf.hild_tol = 1e-6;
-  cf.hild_handoff = HILD_HANDOFF;
   KState st{};
   st.n = n; st.prob = dprob; st.lam = dlam; st.hflag = dhf; st.uk_1 = duk1; st.uk = duk; st.J_fin = djf;
   st.nviol = dnv; st.J_unc = djf;
-  hipMalloc(&st.hq, (2 * n + 1) * sizeof(int));
-  st.hq_it = st.hq + n;
-  st.hq_n = st.hq + 2 * n;
   KIO io{};
   io.mode = MODE_FUSED;
   hipEvent_t e0, e1;

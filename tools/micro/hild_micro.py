@@ -22,4 +22,6 @@ np.array(recs).astype(np.float64).tofile(os.path.join(HERE, "hild_problems.bin")
 if "--build" in sys.argv:
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
                     "-Wno-unused-result", "-Wno-unused-value", "-mllvm", "-pragma-unroll-threshold=200000",
-                    os.path.join(HERE, "hild_micro.hip"), "-o", os.path.join(HERE, "hild_micro")], check=True)
+                    *os.environ.get("MICRO_FLAGS", "").split(),
+                    os.path.join(HERE, "hild_micro.hip"), "-o",
+                    os.path.join(HERE, os.environ.get("MICRO_OUT", "hild_micro"))], check=True)
