@@ -175,6 +175,15 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
                     const double *M, const double *gamma, double *lambda, int32_t max_iter, double tol,
                     double *DU, int32_t *nexec);
 
+/* hildreth.m for the constraint pattern of constraintsMPC.m as runMPC configures it
+ * (Np = 5, Nc = 2, all three switches): M = [Cu; -Cu; I; -I; G_v; -G_e; G_soc] given by
+ * the Toeplitz columns Hv, He, Hs [n][5] (G_v(i,j) = Hv(i-j) for j <= i).  This is the
+ * solver the fused step runs (rank-2 form, hildreth.m:17-46); E [n][2][2], F [n][2],
+ * gamma/lambda [n][23], DU [n][2], nexec [n] as in mpcekf_hildreth. */
+int mpcekf_hildreth_structured(int device, int64_t n, const double *E, const double *F, const double *Hv,
+                               const double *He, const double *Hs, const double *gamma, double *lambda,
+                               int32_t max_iter, double tol, double *DU, int32_t *nexec);
+
 /* ---- instrumentation (not part of the reference interface) ---- */
 /* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
  * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch

@@ -62,7 +62,7 @@ EXPORTS = [
     "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_get_zk",
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
-    "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps",
+    "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
 ]
 
 _lib = None
@@ -102,6 +102,8 @@ def load():
     L.mpcekf_get_timing.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     L.mpcekf_get_hild_problems.argtypes = [vp, _dp, _ip]
     L.mpcekf_get_stamps.argtypes = [vp, C.POINTER(C.c_int64), _ip]
+    L.mpcekf_hildreth_structured.argtypes = [C.c_int, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int32,
+                                             C.c_double, _dp, _ip]
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults"):
             getattr(L, nm).restype = C.c_int

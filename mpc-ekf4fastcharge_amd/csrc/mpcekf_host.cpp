@@ -803,6 +803,39 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
   return MPCEKF_OK;
 }
 
+int mpcekf_hildreth_structured(int device, int64_t n, const double *E, const double *F, const double *Hv,
+                               const double *He, const double *Hs, const double *gamma, double *lambda,
+                               int32_t max_iter, double tol, double *DU, int32_t *nexec) {
+  if (n < 0 || (n && (!E || !F || !Hv || !He || !Hs || !gamma || !lambda || !DU || !nexec)))
+    return fail(MPCEKF_E_ARG, "hildreth_structured: bad argument");
+  if (max_iter < 1) return fail(MPCEKF_E_ARG, "hildreth_structured: max_iter < 1");
+  if (n == 0) return MPCEKF_OK;
+  HIPCHK(hipSetDevice(device));
+  DevScope d;
+  HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
+  const size_t NCn = 2, NPn = 5, NCONn = NCON_BUILT;
+  const size_t per = NCn * NCn + NCn + 3 * NPn + NCONn + NCONn + NCn;
+  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * per * 8 + (size_t)n * 4 + 1024));
+  double *dE = (double *)d.buf, *dF = dE + n * NCn * NCn, *dHv = dF + n * NCn, *dHe = dHv + n * NPn,
+         *dHs = dHe + n * NPn, *dg = dHs + n * NPn, *dl = dg + n * NCONn, *dD = dl + n * NCONn;
+  int *dn = (int *)(dD + n * NCn);
+  HIPCHK(hipMemcpyAsync(dE, E, n * NCn * NCn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dF, F, n * NCn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dHv, Hv, n * NPn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dHe, He, n * NPn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dHs, Hs, n * NPn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dg, gamma, n * NCONn * 8, hipMemcpyHostToDevice, d.st));
+  HIPCHK(hipMemcpyAsync(dl, lambda, n * NCONn * 8, hipMemcpyHostToDevice, d.st));
+  int rc = lerr(launch_hildreth_structured(n, dE, dF, dHv, dHe, dHs, dg, dl, max_iter, tol, dD, dn, d.st),
+                "hildreth_structured");
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(lambda, dl, n * NCONn * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(DU, dD, n * NCn * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, d.st));
+  HIPCHK(hipStreamSynchronize(d.st));
+  return MPCEKF_OK;
+}
+
 int mpcekf_get_hild_problems(mpcekf_ctx *X, double *prob, int32_t *hflag) {
   int rc = need_init(X);
   if (rc) return rc;

@@ -2134,6 +2134,67 @@ __global__ void __launch_bounds__(64) k_hildreth(int64_t n, const double *Ei, co
   nexec[c] = it;
 }
 
+// The fused solver (hildreth_sweep, as in k_hild) on constraintsMPC.m-structured
+// problems given by their Toeplitz rows: M = [Cu; -Cu; I; -I; G_v; -G_e; G_soc].
+__global__ void __launch_bounds__(256) k_hildreth_structured(int64_t n, const double *Ei, const double *Fi,
+                                                             const double *Hvi, const double *Hei,
+                                                             const double *Hsi, const double *gi, double *lami,
+                                                             int maxIter, double tol, double *DUo, int *nexec) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool real = c < n;  // lanes past n ride along (hildreth_sweep keeps the wave full)
+  const int64_t cc = real ? c : 0;
+  Cons Cn;
+  double E[NC][NC], F[NC], K[NCON], lam[NCON];
+  if (!real) {
+    hild_dummy(Cn, E, K);
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = 0.0;
+#pragma unroll
+    for (int a = 0; a < NC; ++a) F[a] = 0.0;
+  } else {
+#pragma unroll
+    for (int a = 0; a < NC; ++a) {
+      F[a] = Fi[cc * NC + a];
+#pragma unroll
+      for (int b = 0; b < NC; ++b) E[a][b] = Ei[(cc * NC + a) * NC + b];
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      Cn.Hv[i] = Hvi[cc * NP + i];
+      Cn.He[i] = Hei[cc * NP + i];
+      Cn.Hs[i] = Hsi[cc * NP + i];
+    }
+    double y[NC], R[NC][NC];
+    bool ok = chol_n<NC>(E, R);
+    mldiv_spd<NC>(E, R, ok, F, y);
+    ConsM Mf{Cn};
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) sum = sum + Mf(i, k) * y[k];
+      K[i] = sum + gi[cc * NCON + i];
+      lam[i] = lami[cc * NCON + i];
+    }
+  }
+  double Mtl[NC];
+  const int it = hildreth_sweep(Cn, E, lam, maxIter, tol, K, Mtl, !real, lami + cc * NCON, 1);
+  if (!real) return;
+  double rhs[NC], mE[NC][NC], DU[NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) {
+    rhs[a] = F[a] + Mtl[a];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) mE[a][b] = -E[a][b];
+  }
+  lu_solve_n<NC>(mE, rhs, DU);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) lami[cc * NCON + i] = lam[i];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) DUo[cc * NC + a] = DU[a];
+  nexec[cc] = it;
+}
+
 // initKF.m:94-95 / OB_step.m:185: xhat = 0, SigmaX = SigmaX0(1:5,1:5), bigX = 0
 __global__ void k_init_state(int64_t n, int NM, double *ekf, double *bigx, double s0, double s1, double s2, double s3,
                              double s4) {
@@ -2243,6 +2304,15 @@ int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_hildreth, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, E, F, M, gam, lam,
                      max_iter, tol, DU, nexec);
+  return (int)hipGetLastError();
+}
+
+int launch_hildreth_structured(int64_t n, const double *E, const double *F, const double *Hv, const double *He,
+                               const double *Hs, const double *gam, double *lam, int max_iter, double tol,
+                               double *DU, int *nexec, void *stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_hildreth_structured, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, E, F, Hv,
+                     He, Hs, gam, lam, max_iter, tol, DU, nexec);
   return (int)hipGetLastError();
 }
 

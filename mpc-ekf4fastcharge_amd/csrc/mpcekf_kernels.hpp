@@ -106,6 +106,9 @@ int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double
 int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *F, const double *M,
                     const double *gam, double *lam, int max_iter, double tol, double *DU, int *nexec,
                     void *stream);
+int launch_hildreth_structured(int64_t n, const double *E, const double *F, const double *Hv, const double *He,
+                               const double *Hs, const double *gam, double *lam, int max_iter, double tol,
+                               double *DU, int *nexec, void *stream);
 int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream);
 bool cell_kernel_supported(int nzp);
 int cell_lds_bytes(const KRom &r);

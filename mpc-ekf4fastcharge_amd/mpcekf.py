@@ -291,6 +291,39 @@ def hildreth(E, F, M, gamma, lambda0=None, maxIter=100, tol=1e-6, device=0):
     return DU, lam, ne
 
 
+def hildreth_structured(E, F, Hv, He, Hs, gamma, lambda0=None, maxIter=100, tol=1e-6, device=0):
+    """hildreth.m on constraintsMPC.m-structured problems (the fused step's solver):
+    E [n,2,2], F [n,2], Hv/He/Hs [n,5] Toeplitz columns, gamma [n,23]."""
+    L = _lib.load()
+    E = np.ascontiguousarray(E, dtype=np.float64)
+    n = E.shape[0]
+    a = [np.ascontiguousarray(x, dtype=np.float64) for x in (F, Hv, He, Hs, gamma)]
+    lam = np.zeros((n, 23)) if lambda0 is None else np.array(lambda0, dtype=np.float64, order="C")
+    DU = np.empty((n, 2))
+    ne = np.empty(n, dtype=np.int32)
+    check(L.mpcekf_hildreth_structured(device, n, dptr(E), *[dptr(x) for x in a], dptr(lam), int(maxIter),
+                                       float(tol), dptr(DU), iptr(ne)))
+    return DU, lam, ne
+
+
+def structured_M(Hv, He, Hs):
+    """The constraintsMPC.m matrix [Cu; -Cu; I; -I; G_v; -G_e; G_soc] (23 x 2) of
+    Toeplitz columns, with the kernels' exact entries (signed zeros included)."""
+    M = np.zeros((23, 2))
+    for i in range(2):
+        for k in range(2):
+            M[i, k] = 1.0 if k <= i else 0.0
+            M[2 + i, k] = -(1.0 if k <= i else 0.0)
+            M[4 + i, k] = 1.0 if i == k else 0.0
+            M[6 + i, k] = -(1.0 if i == k else 0.0)
+    for r in range(5):
+        for k in range(2):
+            M[8 + r, k] = Hv[r - k] if k <= r else 0.0
+            M[13 + r, k] = -(He[r - k] if k <= r else 0.0)
+            M[18 + r, k] = Hs[r - k] if k <= r else 0.0
+    return M
+
+
 def runMPC(rom, SOC0, TC, nsteps, cfg=None, device=0, ncells=None):
     """runMPC.m:72-112 for a batch of cells; returns trajectories [nsteps, ncells]."""
     SOC0 = np.atleast_1d(np.asarray(SOC0, dtype=np.float64))

@@ -235,3 +235,36 @@ def test_flush_period_is_exact(rom, M):
             np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
         for k in ("ekf", "bigX"):
             np.testing.assert_array_equal(r["state"][k], runs[0]["state"][k], err_msg=k)
+
+
+def test_structured_hildreth_edge_paths_match_oracle(oc, M):
+    """The fused step's QP solver (rank-2 sweep with its careful and dense fallbacks)
+    against the C oracle on structured problems built to reach every path:
+    plain problems, a zero G_soc row (Hs[0] = 0) with gamma < 0 (the dense form's
+    +inf/NaN alternation), infinite warm starts, a singular E (non-finite X:
+    the dense path), and maxIter-bound infeasible duals."""
+    rng = np.random.default_rng(31)
+    n = 640
+    Hv = rng.normal(0, 1e-3, (n, 5))
+    He = rng.normal(0, 1e-3, (n, 5))
+    Hs = rng.normal(0, 1e-5, (n, 5))
+    Hs[:, 0] = 0.0                                            # SOC(k+1) does not see u(k)
+    A = rng.normal(0, 1e-2, (n, 2, 2))
+    E = A @ A.transpose(0, 2, 1) + 1e-4 * np.eye(2)
+    F = rng.normal(0, 1e-2, (n, 2))
+    gam = np.abs(rng.normal(0.0, 0.05, (n, 23)))
+    lam0 = np.where(rng.random((n, 23)) < 0.3, np.abs(rng.normal(0, 0.5, (n, 23))), 0.0)
+    g = np.arange(n) % 8
+    gam[g == 1, 18] = -0.01                                   # zero row, gamma < 0
+    gam[g == 2, 13:18] = -np.abs(gam[g == 2, 13:18]) - 1e-3   # infeasible eta rows
+    lam0[g == 3, 18] = np.inf                                 # warm start from the inf pattern
+    E[g == 4] = 0.0                                           # singular E: non-finite X
+    F[g == 5] *= 1e3
+    DU, lam, ne = M.hildreth_structured(E, F, Hv, He, Hs, gam, lam0)
+    assert (ne == 100).any() and (ne < 100).any()
+    for i in range(n):
+        Mi = M.structured_M(Hv[i], He[i], Hs[i])
+        du_r, lam_r, ne_r = oc.hildreth(E[i], F[i], Mi, gam[i], lam0[i], 100)
+        assert ne[i] == ne_r, (i, g[i])
+        np.testing.assert_array_equal(lam[i], lam_r, err_msg=f"cell {i} group {g[i]}")
+        np.testing.assert_array_equal(DU[i], du_r, err_msg=f"cell {i} group {g[i]}")
