@@ -38,18 +38,23 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32):
            record (xhat 5 + packed Sigma 15) and plant state (6) read + written,
            the model timestamps (2 x NM int32) read + written, the two input rings.
     cell : the 4 corner EKF records read + written, their timestamps, the step's
-           ring input, per-cell scalars/constants, outputs u/v/soc/phise, zk
-           (+ boundzk) and the QP record.
+           ring input, per-cell scalars/constants, outputs u/v/soc/phise, zk,
+           the QP record (+ the 14-double boundzk hand-off record).
+    bounds: the hand-off record and corner 1's packed Sigma read, 4 per-cell
+           constants read, boundzk (28) written.
     plant: the 4 corner plant states read + written, timestamps, ring writes,
            per-cell scalars.
     hild : the QP record read, lambda read + written, outputs.
     """
     flush = 2 * 8 * NM * (20 + 6) + 2 * 2 * 4 * NM + 2 * 8 * lazy_h
-    zk = 8 * 28 * (2 if bounds else 1)
-    cell = 4 * 2 * 8 * 20 + 4 * 2 * 4 + 8 + 20 * 8 + 4 * 8 + zk + 51 * 8
+    zk = 8 * 28
+    cell = 4 * 2 * 8 * 20 + 4 * 2 * 4 + 8 + 20 * 8 + 4 * 8 + zk + 51 * 8 + (14 * 8 if bounds else 0)
     plant = 4 * 2 * 6 * 8 + 4 * 2 * 4 + 2 * 8 + 12 * 8 + 8
     hild = 51 * 8 + 2 * 8 * ncon + 4 * 8
-    return dict(flush=flush, cell=cell, plant=plant, hild=hild)
+    out = dict(flush=flush, cell=cell, plant=plant, hild=hild)
+    if bounds:
+        out["bounds"] = 14 * 8 + 15 * 8 + 4 * 8 + 28 * 8
+    return out
 
 
 def survey_bytes_per_cell_step(NM, ncon):
@@ -143,7 +148,7 @@ def main():
         value = cell_steps / dt if dt > 0 else 0.0
         bpc = algorithmic_bytes_per_cell(rom.NM, 23, bool(args.bounds))
         per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1], ms_total=tim[k][0])
-                      for k in tim}
+                      for k in tim if tim[k][1] > 0}
         # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
         dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
         ms = per_kernel[dom]["ms_per_launch"]

@@ -187,14 +187,16 @@ int mpcekf_hildreth_structured(int device, int64_t n, const double *E, const dou
 /* ---- instrumentation (not part of the reference interface) ---- */
 /* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
  * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch
- * counts of [plant, flush, cell, hild] (arrays of MPCEKF_NKERNELS) since the last
- * call and resets them.  "flush" is the all-model time update (k_flush, every
- * 32 steps and at the end of each call). */
+ * counts of [plant, flush, cell, hild, bounds] (arrays of MPCEKF_NKERNELS) since the
+ * last call and resets them.  "flush" is the all-model time update (k_flush, every
+ * 32 steps and at the end of each call); "bounds" is boundzk (k_bounds, when
+ * MPCEKF_CF_BOUNDS is set). */
 #define MPCEKF_K_PLANT 0
 #define MPCEKF_K_FLUSH 1
 #define MPCEKF_K_CELL 2
 #define MPCEKF_K_HILD 3
-#define MPCEKF_NKERNELS 4
+#define MPCEKF_K_BOUNDS 4
+#define MPCEKF_NKERNELS 5
 int mpcekf_set_timing(mpcekf_ctx *ctx, int32_t enable);
 int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
 /* The Hildreth problem records of the last fused step, as k_cell left them for

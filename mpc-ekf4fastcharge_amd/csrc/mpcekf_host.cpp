@@ -70,6 +70,7 @@ struct mpcekf_ctx {
   int *d_int = nullptr;       // warn, status, nviol, hflag
   double *d_prob = nullptr;   // k_cell -> k_hild problem records
   double *d_zk = nullptr, *d_zbk = nullptr;
+  double *d_bnd = nullptr;    // k_cell -> k_bounds records [NBND][n]
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
@@ -80,8 +81,8 @@ struct mpcekf_ctx {
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
   std::vector<hipEvent_t> ev;
-  double t_ms[4] = {0, 0, 0, 0};
-  int64_t t_n[4] = {0, 0, 0, 0};
+  double t_ms[MPCEKF_NKERNELS] = {};
+  int64_t t_n[MPCEKF_NKERNELS] = {};
   // electrode constants kept for per-cell initialisation (k0(T), Cdleff)
   double Tref = 0, Rgas = 0, th0[2] = {0, 0}, th100[2] = {0, 0}, k0ref[2] = {0, 0}, Ea[2] = {0, 0};
   double Cdl[2] = {0, 0}, wDL[2] = {0, 0}, nDL[2] = {0, 0};
@@ -392,6 +393,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
       (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
+      (rc = dalloc(&X->d_bnd, n * NBND)) ||
       (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))
 #ifdef MPCEKF_STAMPS
       || (rc = dalloc(&X->d_stamps, n * NSTAMPS))
@@ -420,7 +422,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -511,9 +513,10 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     if (traj_nexec) dnex = (int *)p;
   }
   const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
-  if (X->timing && X->ev.size() < (size_t)nsteps * 5) {
+  constexpr int NEV = 6;  // events per step: plant | cell | bounds | hild | flush |
+  if (X->timing && X->ev.size() < (size_t)nsteps * NEV) {
     size_t old = X->ev.size();
-    X->ev.resize((size_t)nsteps * 5);
+    X->ev.resize((size_t)nsteps * NEV);
     for (size_t i = old; i < X->ev.size(); ++i) HIPCHK(hipEventCreate(&X->ev[i]));
   }
   // Deferred all-model time update: step t advances only the models it
@@ -524,7 +527,7 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
   for (int k = 0; k < nsteps; ++k) {
     const size_t o = (size_t)k * n;
     const int t = k + 1;
-    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * 5] : nullptr;
+    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * NEV] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
     if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, X->stream), "plant"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[1], X->stream));
@@ -539,15 +542,18 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.nexec = dnex ? dnex + o : nullptr;
     io.zk = X->d_zk;
     io.zbk = bounds ? X->d_zbk : nullptr;
+    io.bnd = bounds ? X->d_bnd : nullptr;
     if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[2], X->stream));
-    if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+    if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, X->d_zbk, X->stream), "bounds"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+    if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+    if (E) HIPCHK(hipEventRecord(E[4], X->stream));
     if (t % X->flush_period == 0 || t == nsteps) {
       if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
       flushed[k] = 1;
     }
-    if (E) HIPCHK(hipEventRecord(E[4], X->stream));
+    if (E) HIPCHK(hipEventRecord(E[5], X->stream));
   }
   if (!outputs_on_device) {
     for (int i = 0; i < 4; ++i)
@@ -556,12 +562,12 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
   }
   HIPCHK(hipStreamSynchronize(X->stream));
   if (X->timing) {
-    static const int slot[4] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_HILD, MPCEKF_K_FLUSH};
+    static const int slot[NEV - 1] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_BOUNDS, MPCEKF_K_HILD, MPCEKF_K_FLUSH};
     for (int k = 0; k < nsteps; ++k)
-      for (int j = 0; j < 4; ++j) {
-        if (j == 3 && !flushed[k]) continue;
+      for (int j = 0; j < NEV - 1; ++j) {
+        if ((j == 4 && !flushed[k]) || (j == 2 && !bounds)) continue;
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * 5 + j], X->ev[(size_t)k * 5 + j + 1]));
+        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + j], X->ev[(size_t)k * NEV + j + 1]));
         X->t_ms[slot[j]] += ms;
         X->t_n[slot[j]] += 1;
       }
@@ -577,7 +583,7 @@ int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {
 
 int mpcekf_get_timing(mpcekf_ctx *X, double *ms_sum, int64_t *launches) {
   if (!X) return fail(MPCEKF_E_ARG, "null ctx");
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < MPCEKF_NKERNELS; ++j) {
     if (ms_sum) ms_sum[j] = X->t_ms[j];
     if (launches) launches[j] = X->t_n[j];
     X->t_ms[j] = 0;
@@ -649,9 +655,11 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, double *z
   io.ik_in = dik;
   io.zk = dzk;
   io.zbk = boundzk ? dzb : nullptr;
+  io.bnd = boundzk ? X->d_bnd : nullptr;
   io.xm_out = dxm;
   io.xg_out = dxg;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+  if (boundzk && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
   HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));

@@ -425,32 +425,47 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   return V;
 }
 
-// getChatV (iterEKF.m:421-519): voltage Jacobian rows of the 4 corners.
+// getChatV (iterEKF.m:421-519) pieces.  Cell scalars of the voltage Jacobian.
+struct ChatK {
+  double Rctn, Rctp, dUn0, dUp3;
+};
+__device__ __forceinline__ ChatK chat_k(const KRom &r, const CellCtx &cc, double zTE1, double zTH0, double zTEE,
+                                        double zTH3) {
+  ChatK k;
+  double i0n = cc.k0n * sqrt(zTE1 * (1 - zTH0) * zTH0);
+  double i0p = cc.k0p * sqrt(zTEE * (1 - zTH3) * zTH3);
+  k.Rctn = r.R * cc.T / (r.F * i0n);
+  k.Rctp = r.R * cc.T / (r.F * i0p);
+  k.dUn0 = duocp(cc.tb, cc.ntab, 0, zTH0);
+  k.dUp3 = duocp(cc.tb, cc.ntab, 1, zTH3);
+  return k;
+}
+// The row of one corner (model blob Cm, interpolation weight g).
+__device__ __forceinline__ void chat_row(const KRom &r, const ChatK &K, const double *Cm, double g, double Chat[NX]) {
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    double v = r.Rfp * (g * Cm[R_IFDL3 * NX + k]) - r.Rfn * (g * Cm[R_IFDL0 * NX + k]);
+    v = v + K.Rctp * (g * Cm[R_IF3 * NX + k]) - K.Rctn * (g * Cm[R_IF0 * NX + k]);
+    v = v + g * Cm[R_PHIE * NX + k];
+    v = v + (K.dUp3 * (g * Cm[R_TH3 * NX + k]) - K.dUn0 * (g * Cm[R_TH0 * NX + k]));
+    Chat[k] = v;
+  }
+}
+__device__ __forceinline__ double chat0(const KRom &r, const ChatK &K) {
+  double dn = (r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n));
+  double dp = (r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p));
+  double res0n = -K.dUn0 * r.Ts * dn / (3600 * r.Q);
+  double res0p = -K.dUp3 * r.Ts * dp / (3600 * r.Q);
+  return res0p - res0n;
+}
+// Voltage Jacobian rows of the 4 corners.
 template <int NZ>
 __device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, const XI &xi, double zTE1, double zTH0,
                                           double zTEE, double zTH3, double Chat[4][NX], double &Chat0) {
-  double i0n = cc.k0n * sqrt(zTE1 * (1 - zTH0) * zTH0);
-  double i0p = cc.k0p * sqrt(zTEE * (1 - zTH3) * zTH3);
-  double Rctn = r.R * cc.T / (r.F * i0n), Rctp = r.R * cc.T / (r.F * i0p);
-  double dUn0 = duocp(cc.tb, cc.ntab, 0, zTH0), dUp3 = duocp(cc.tb, cc.ntab, 1, zTH3);
+  const ChatK K = chat_k(r, cc, zTE1, zTH0, zTEE, zTH3);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    double g = xi.g[j];
-    const double *Cm = cc.L + xi.m[j] * cc.stride;
-#pragma unroll
-    for (int k = 0; k < NX; ++k) {
-      double v = r.Rfp * (g * Cm[R_IFDL3 * NX + k]) - r.Rfn * (g * Cm[R_IFDL0 * NX + k]);
-      v = v + Rctp * (g * Cm[R_IF3 * NX + k]) - Rctn * (g * Cm[R_IF0 * NX + k]);
-      v = v + g * Cm[R_PHIE * NX + k];
-      v = v + (dUp3 * (g * Cm[R_TH3 * NX + k]) - dUn0 * (g * Cm[R_TH0 * NX + k]));
-      Chat[j][k] = v;
-    }
-  }
-  double dn = (r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n));
-  double dp = (r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p));
-  double res0n = -dUn0 * r.Ts * dn / (3600 * r.Q);
-  double res0p = -dUp3 * r.Ts * dp / (3600 * r.Q);
-  Chat0 = res0p - res0n;
+  for (int j = 0; j < 4; ++j) chat_row(r, K, cc.L + xi.m[j] * cc.stride, xi.g[j], Chat[j]);
+  Chat0 = chat0(r, K);
 }
 
 // ---------------------------------------------------------------------------
@@ -1615,6 +1630,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int q = 0; q < nz + 2; ++q) io.zk[c * (nz + 2) + q] = NaN;
     if (io.zbk)
       for (int q = 0; q < nz + 2; ++q) io.zbk[c * (nz + 2) + q] = NaN;
+    if (io.bnd) io.bnd[BD_M * s.n + c] = -1.0;  // no boundzk record: k_bounds leaves zbk NaN
     if (io.uk_out) io.uk_out[c] = NaN;
     if (io.lin_out)
       for (int q = 0; q < 35; ++q) io.lin_out[c * 35 + q] = NaN;
@@ -1763,93 +1779,21 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       fail_outputs();
       return;
     }
-#ifndef PROBE_NO_BOUNDS
-    if (io.zbk) {
-      // getChatZ + boundzk (iterEKF.m:186-205, 523-602), diagonal only
-      double ChV[4][NX], ChV0;
-      get_chatv<NZ>(r, cc, xi, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChV, ChV0);
-      double res0n = -r.Ts * ((r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n))) / (3600 * r.Q);
-      double res0p = -r.Ts * ((r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p))) / (3600 * r.Q);
-      double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
-      double dUn = duocp(cc.tb, cc.ntab, 0, r.th0n + xSOC * (r.th100n - r.th0n));
-      double dUp = duocp(cc.tb, cc.ntab, 1, r.th0p + xSOC * (r.th100p - r.th0p));
-      double S1b[NPK];
-      load_S(cc.erec + (size_t)xi.m[0] * REC, S1b);
-      double SigV = 0.0;
-      double SigZ[NZ];
-#pragma unroll
-      for (int q = 0; q < NZ; ++q) SigZ[q] = 0.0;
-      const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+    if (io.bnd) {  // boundzk (iterEKF.m:186-205) runs in k_bounds from this record
+      double *bd = io.bnd;
+      const int64_t n = s.n;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        double g = xi.g[j];
-        const double *Cm = cc.L + xi.m[j] * cc.stride;
-        double cph0[NX];
-#pragma unroll
-        for (int k = 0; k < NX; ++k) {
-          double v = g * Cm[R_PHISE0 * NX + k];
-          if (ph0pp) v = v + ChV[j][k];
-          cph0[k] = v;
-        }
-#pragma unroll
-        for (int q = 0; q < NZ; ++q) {
-          double row[NX];
-          unsigned f = r.flags[q];
-#pragma unroll
-          for (int k = 0; k < NX; ++k) {
-            double v = g * Cm[q * NX + k];
-            if (f & G_PPHIS) v = v + ChV[j][k];
-            if (f & G_PHIE) v = v - cph0[k];
-            row[k] = v;
-          }
-          double qf = 0.0;
-#pragma unroll
-          for (int cI = 0; cI < NX; ++cI) {
-            double acc = 0.0;
-#pragma unroll
-            for (int k = 0; k < NX; ++k) acc = acc + row[k] * S1b[pk(k, cI)];
-            qf = qf + acc * row[cI];
-          }
-          SigZ[q] = SigZ[q] + qf;
-          launder(SigZ[q]);
-        }
-        double row2[NX];
-#pragma unroll
-        for (int cI = 0; cI < NX; ++cI) {
-          double acc = 0.0;
-#pragma unroll
-          for (int k = 0; k < NX; ++k) acc = acc + S1b[pk(k, cI)] * ChV[j][k];
-          row2[cI] = acc;
-        }
-        double acc = 0.0;
-#pragma unroll
-        for (int cI = 0; cI < NX; ++cI) acc = acc + row2[cI] * ChV[j][cI];
-        SigV = SigV + acc;
-        launder(SigV);
-        __builtin_amdgcn_sched_barrier(0);
+        bd[(BD_G + j) * n + c] = xi.g[j];
+        bd[(BD_M + j) * n + c] = xi.m[j];
       }
-#pragma unroll
-      for (int q = 0; q < NZ; ++q) {
-        double c0 = 0.0;
-        switch (r.c0k[q]) {
-          case C0_CHATV0: c0 = ChV0; break;
-          case C0_RES0N: c0 = res0n; break;
-          case C0_RES0P: c0 = res0p; break;
-          case C0_DUN: c0 = dUn * res0n; break;
-          case C0_DUP: c0 = dUp * res0p; break;
-          case C0_MDUN: c0 = -dUn * res0n; break;
-          default: break;
-        }
-        SigZ[q] = SigZ[q] + (c0 * S0) * c0;
-        if (q < nz) io.zbk[c * (nz + 2) + r.perm[q]] = 3 * sqrt(SigZ[q]);
-      }
-      SigV = SigV + ChV0 * S0 * ChV0;
-      double rr = -r.Ts / (3600 * r.Q);
-      double SigSOC = rr * S0 * rr;
-      io.zbk[c * (nz + 2) + nz] = 3 * sqrt(SigV);
-      io.zbk[c * (nz + 2) + nz + 1] = 3 * sqrt(SigSOC);
+      bd[(BD_Z + 0) * n + c] = Z[R_TE1];
+      bd[(BD_Z + 1) * n + c] = Z[R_TH0];
+      bd[(BD_Z + 2) * n + c] = Z[R_TEE];
+      bd[(BD_Z + 3) * n + c] = Z[R_TH3];
+      bd[BD_X0 * n + c] = x0;
+      bd[BD_S0 * n + c] = S0;
     }
-#endif
     STAMP(9);
     s.x0[c] = x0;
     s.S0[c] = S0;
@@ -1947,6 +1891,163 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_bounds: boundzk (iterEKF.m:186-205; getChatZ iterEKF.m:523-602), diagonal only.
+// A lane quad per cell, lane j = corner j: its getChatV row, its 26 quadratic forms
+// row' * Sigma1 * row; the corner sums keep k_cell's order ((((0 + q0) + q1) + q2)
+// + q3) through DPP broadcasts, so the result is the one-lane form's bits.
+// ---------------------------------------------------------------------------
+// v from the quad lane selected by DPP quad_perm control CTRL.
+template <int CTRL>
+__device__ __forceinline__ double qperm(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+template <int Q>
+__device__ __forceinline__ double qbc(double v) {  // lane Q's v in every lane of the quad
+  return qperm<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v);
+}
+__device__ __forceinline__ double quad_sum_seq(double v) {  // (((0 + v0) + v1) + v2) + v3
+  return (((0.0 + qbc<0>(v)) + qbc<1>(v)) + qbc<2>(v)) + qbc<3>(v);
+}
+
+// 256 cells per block: the ~90 KB model blob leaves room for one block per CU, so the
+// block is the CU's whole occupancy (4 waves per SIMD) and stages the blob once.
+constexpr int BOUNDS_BLOCK = 1024;
+__host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.cell_len + 1; }  // after the blob
+// row' * Sigma * row in symmetric form: T = Sigma with doubled off-diagonals,
+// u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, explicit fma at every step
+// (orc qform: 20 operations instead of the 60 of Sigma*row then row'*(.)).
+__device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]) {
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    double u = T[pk(k, k)] * rw[k];
+#pragma unroll
+    for (int l = k + 1; l < NX; ++l) u = __builtin_fma(T[pk(k, l)], rw[l], u);
+    q = k == 0 ? rw[0] * u : __builtin_fma(rw[k], u, q);
+  }
+  return q;
+}
+
+template <int NZ>
+__global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KState s, const double *bd, double *zbk) {
+  extern __shared__ double lds[];
+  stage_lds(lds, r.cell_blob, r.cell_len);
+  __syncthreads();
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = s.n;
+  const int j = (int)(gt & 3);
+  const int64_t cq = gt >> 2;
+  const int64_t c = cq < n ? cq : n - 1;  // lanes past n ride along (quad exchanges)
+  const int nz = r.nz;
+  const bool valid = cq < n && bd[BD_M * n + c] >= 0.0;
+  CellCtx cc;
+  cc.L = lds;
+  cc.tb = lds + r.cell_tab;
+  cc.ntab = r.ntab;
+  cc.stride = r.cell_stride;
+  const double Tc = s.Tc[c];
+  cc.T = Tc > 100 ? Tc : Tc + 273.15;
+  cc.dT = cc.T - r.Tref;
+  cc.k0n = s.k0n[c];
+  cc.k0p = s.k0p[c];
+  const double g = bd[(BD_G + j) * n + c];
+  const int m = valid ? (int)bd[(BD_M + j) * n + c] : 0;
+  const double *Cm = cc.L + m * cc.stride;
+  const double zTE1 = bd[(BD_Z + 0) * n + c], zTH0 = bd[(BD_Z + 1) * n + c];
+  const double zTEE = bd[(BD_Z + 2) * n + c], zTH3 = bd[(BD_Z + 3) * n + c];
+  const double x0 = bd[BD_X0 * n + c], S0 = bd[BD_S0 * n + c];
+  // SigmaX of the first corner for all four (iterEKF.m:191)
+  double S1b[NPK];
+  load_S(s.ekf + ((size_t)c * r.NM + (valid ? (int)bd[BD_M * n + c] : 0)) * REC, S1b);
+#pragma unroll
+  for (int k = 0; k < NX; ++k)
+#pragma unroll
+    for (int l = k + 1; l < NX; ++l) S1b[pk(k, l)] = 2 * S1b[pk(k, l)];
+  const ChatK K = chat_k(r, cc, zTE1, zTH0, zTEE, zTH3);
+  double ChV[NX];
+  chat_row(r, K, Cm, g, ChV);
+  const double ChV0 = chat0(r, K);
+  const double res0n = -r.Ts * ((r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n))) / (3600 * r.Q);
+  const double res0p = -r.Ts * ((r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p))) / (3600 * r.Q);
+  const double xSOC = s.SOC0[c] - x0 * (r.Ts / (3600 * r.Q));
+  const double dUn = duocp(cc.tb, cc.ntab, 0, r.th0n + xSOC * (r.th100n - r.th0n));
+  const double dUp = duocp(cc.tb, cc.ntab, 1, r.th0p + xSOC * (r.th100p - r.th0p));
+  const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+  double cph0[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    double v = g * Cm[R_PHISE0 * NX + k];
+    if (ph0pp) v = v + ChV[k];
+    cph0[k] = v;
+  }
+  // The constant-column terms (c0 * S0) * c0 of the 7 kinds (C0_*) in an LDS row per
+  // cell, lane j filling kinds j and j + 4: each form then adds its term by a uniform
+  // offset instead of a select chain.
+  double *c0t = lds + bounds_c0_base(r) + (threadIdx.x >> 2) * 8;
+  {
+    const double cv[8] = {0.0, ChV0, res0n, res0p, dUn * res0n, dUp * res0p, -dUn * res0n, 0.0};
+    double lo = cv[0], hi = cv[4];
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (j == i) { lo = cv[i]; hi = cv[i + 4]; }
+    c0t[j] = (lo * S0) * lo;
+    c0t[j + 4] = (hi * S0) * hi;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // Forms q = j, j + 4, ... are this lane's to finish: their sums and output slots.
+  constexpr int NOWN = (NZ + 3) / 4;
+  double mine[NOWN];
+  int slot[NOWN];
+#pragma unroll
+  for (int i = 0; i < NOWN; ++i) { mine[i] = 0.0; slot[i] = -1; }
+#pragma unroll
+  for (int q = 0; q < NZ; ++q) {
+    double row[NX];
+    const unsigned f = r.flags[q];
+    // uniform branches (the empty volatile asm keeps them from being if-converted)
+    if (f & G_PPHIS) {
+      asm volatile("");
+#pragma unroll
+      for (int k = 0; k < NX; ++k) row[k] = __builtin_fma(g, Cm[q * NX + k], ChV[k]);
+    } else {
+      asm volatile("");
+#pragma unroll
+      for (int k = 0; k < NX; ++k) row[k] = g * Cm[q * NX + k];
+    }
+    if (f & G_PHIE) {
+      asm volatile("");
+#pragma unroll
+      for (int k = 0; k < NX; ++k) row[k] = row[k] - cph0[k];
+    }
+    const double qf = qform(S1b, row);
+    const double sz = quad_sum_seq(qf) + c0t[r.c0k[q]];
+    if ((q & 3) == j && q < nz) {
+      mine[q >> 2] = sz;
+      slot[q >> 2] = r.perm[q];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one form at a time: 128 VGPRs at 4 waves/SIMD
+  }
+  double *zo = zbk + c * (nz + 2);
+#pragma unroll
+  for (int i = 0; i < NOWN; ++i)
+    if (valid && slot[i] >= 0) zo[slot[i]] = 3 * sqrt(mine[i]);
+  const double acc = qform(S1b, ChV);
+  double SigV = quad_sum_seq(acc);
+  SigV = SigV + ChV0 * S0 * ChV0;
+  const double rr = -r.Ts / (3600 * r.Q);
+  const double SigSOC = rr * S0 * rr;
+  if (valid && j == 0) {
+    zo[nz] = 3 * sqrt(SigV);
+    zo[nz + 1] = 3 * sqrt(SigSOC);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2270,6 +2371,28 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
   switch (r.nzp) {
     case 26: launch_cell_t<26>(r, c, s, io, st); break;
     case 32: launch_cell_t<32>(r, c, s, io, st); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+template <int NZ>
+static void launch_bounds_t(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
+  static bool attr = false;
+  int lds = (bounds_c0_base(r) + BOUNDS_BLOCK / 4 * 8) * (int)sizeof(double);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_bounds<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_bounds<NZ>, dim3(grid_for(4 * s.n, BOUNDS_BLOCK)), dim3(BOUNDS_BLOCK), lds, st, r, s, bnd, zbk);
+}
+
+int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk, void *stream) {
+  if (s.n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  switch (r.nzp) {
+    case 26: launch_bounds_t<26>(r, s, bnd, zbk, st); break;
+    case 32: launch_bounds_t<32>(r, s, bnd, zbk, st); break;
     default: return -1;
   }
   return (int)hipGetLastError();

@@ -83,9 +83,13 @@ struct KIO {
   double *lin_out; const double *lin_in;                        // [n][35]
   const double *soc_k1_in; double *uk_out;                      // mpc stage
   int lazy_t;             // > 0: fused step t of the running call with deferred time update
+  double *bnd;            // [NBND][n] boundzk hand-off k_cell -> k_bounds (with zbk)
   long long *stamps;      // [MPCEKF_NSTAMPS][n] s_memtime per k_cell section (-DMPCEKF_STAMPS builds only)
 };
 constexpr int NSTAMPS = 12;
+// k_cell -> k_bounds record: g[4], m[4], Z(te1, th0, tee, th3), x0, S0.  k_bounds reads
+// corner 1's Sigma from the EKF record k_cell stored (nothing writes it before the next k_cell).
+enum { BD_G = 0, BD_M = 4, BD_Z = 8, BD_X0 = 12, BD_S0 = 13, NBND = 14 };
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 
@@ -97,6 +101,8 @@ int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_t
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
 int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream);
+// boundzk (iterEKF.m:186-205) from k_cell's hand-off record, a lane quad per cell
+int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk, void *stream);
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream);
 constexpr int PROB_DOUBLES = 51;  // PB_N for Np = 5, Nc = 2
 int launch_predmat(int64_t n, int Np, int Nc, const double *a, const double *C, const double *D, double *Phi,

@@ -155,10 +155,11 @@ class Context:
 
     def get_timing(self):
         """{kernel: (ms_sum, launches)} since the last call (HIP events on the ctx stream)."""
-        ms = np.zeros(4)
-        nl = (C.c_int64 * 4)()
+        names = ("plant", "flush", "cell", "hild", "bounds")  # MPCEKF_K_* order
+        ms = np.zeros(len(names))
+        nl = (C.c_int64 * len(names))()
         check(self.L.mpcekf_get_timing(self.h, dptr(ms), nl))
-        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(("plant", "flush", "cell", "hild"))}
+        return {k: (float(ms[i]), int(nl[i])) for i, k in enumerate(names)}
 
     def get_stamps(self):
         """k_cell section stamps of the last fused step [NSTAMPS][ncells] (profiling builds; else None)."""

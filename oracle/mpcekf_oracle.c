@@ -97,6 +97,24 @@ typedef struct {
 static const int PK[NX][NX] = {{0, 1, 2, 3, 4}, {1, 5, 6, 7, 8}, {2, 6, 9, 10, 11},
                                {3, 7, 10, 12, 13}, {4, 8, 11, 13, 14}};
 
+/* boundzk's quadratic forms row' * Sigma * row (iterEKF.m:191-197, diagonal only) in the
+ * symmetric form the k_bounds kernel spells: T = Sigma with doubled off-diagonals,
+ * u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, every step an explicit fma()
+ * (correctly rounded here and on the GPU, so both sides agree bit for bit). */
+static void qform_prep(const double S[NPK], double T[NPK]) {
+  for (int k = 0; k < NX; ++k)
+    for (int l = k; l < NX; ++l) T[PK[k][l]] = k == l ? S[PK[k][l]] : 2 * S[PK[k][l]];
+}
+static double qform(const double T[NPK], const double r[NX]) {
+  double q = 0.0;
+  for (int k = 0; k < NX; ++k) {
+    double u = T[PK[k][k]] * r[k];
+    for (int l = k + 1; l < NX; ++l) u = fma(T[PK[k][l]], r[l], u);
+    q = k == 0 ? r[0] * u : fma(r[k], u, q);
+  }
+  return q;
+}
+
 /* ----------------------------------------------------------------------- */
 /* cellData.function.* (tabulated, see rom.py)                              */
 /* ----------------------------------------------------------------------- */
@@ -806,7 +824,8 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
     unsigned char isPosPhis[256] = {0}, isPhie[256] = {0};
     for (int k = 0; k < ix->nPosPhis; ++k) isPosPhis[ix->posPhis[k]] = 1;
     for (int k = 0; k < ix->nPhie; ++k) isPhie[ix->Phie[k]] = 1;
-    const double *S1b = s->S + (size_t)xi.m[0] * NPK;
+    double T1[NPK];
+    qform_prep(s->S + (size_t)xi.m[0] * NPK, T1);  /* SigmaX of the first corner (iterEKF.m:191) */
     double SigZ[256], SigV = 0.0;
     for (int q = 0; q < nz; ++q) SigZ[q] = 0.0;
     for (int j = 0; j < 4; ++j) {
@@ -822,28 +841,13 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
       for (int q = 0; q < nz; ++q) {
         double row[NX];
         for (int k = 0; k < NX; ++k) {
-          double v = g * Crow(r, m, q)[k];
-          if (isPosPhis[q]) v = v + ChV[j][k];
+          double v = isPosPhis[q] ? fma(g, Crow(r, m, q)[k], ChV[j][k]) : g * Crow(r, m, q)[k];
           if (isPhie[q]) v = v - cph0[k];
           row[k] = v;
         }
-        double qf = 0.0;
-        for (int c = 0; c < NX; ++c) {
-          double acc = 0.0;
-          for (int k = 0; k < NX; ++k) acc = acc + row[k] * S1b[PK[k][c]];
-          qf = qf + acc * row[c];
-        }
-        SigZ[q] = SigZ[q] + qf;
+        SigZ[q] = SigZ[q] + qform(T1, row);
       }
-      double row2[NX];
-      for (int c = 0; c < NX; ++c) {
-        double acc = 0.0;
-        for (int k = 0; k < NX; ++k) acc = acc + S1b[PK[k][c]] * ChV[j][k];
-        row2[c] = acc;
-      }
-      double acc = 0.0;
-      for (int c = 0; c < NX; ++c) acc = acc + row2[c] * ChV[j][c];
-      SigV = SigV + acc;
+      SigV = SigV + qform(T1, ChV[j]);
     }
     for (int q = 0; q < nz; ++q) SigZ[q] = SigZ[q] + (c0[q] * s->S0) * c0[q];
     SigV = SigV + ChV0 * s->S0 * ChV0;

@@ -162,6 +162,9 @@ def test_zk_and_boundzk_match_oracle(rom, oc, M):
         ctx.init_cells(soc0, tc)
         ctx.step(steps)
         zk, zb = ctx.get_zk()
+    for nm, a, b in (("zk", zk, ref["zk"]), ("boundzk", zb, ref["zbk"])):
+        print(nm, "bit-exact" if np.array_equal(a, b, equal_nan=True) else "differs",
+              "max rel", _rel(a, b).max(), "entries differing", int(np.sum(a != b)))
     assert _rel(zk, ref["zk"]).max() <= RTOL_TIGHT
     assert _rel(zb, ref["zbk"]).max() <= RTOL_TIGHT
 

@@ -20,7 +20,7 @@ import bench  # noqa: E402
 M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
 P = importlib.import_module("mpc-ekf4fastcharge_amd")
 NAMES = ["scalar loads + lockout", "get_xind1", "catch-up1", "get_vars1", "chatV+gains", "meas_update x4",
-         "get_xind2 + catch-up2", "get_vars2", "boundzk", "mats_handler", "mpc_setup"]
+         "get_xind2 + catch-up2", "get_vars2", "boundzk record", "mats_handler", "mpc_setup"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 rom = P.make_synth_rom()
