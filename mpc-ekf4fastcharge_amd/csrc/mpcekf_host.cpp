@@ -267,8 +267,13 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   for (int z = 0; z < nZ; ++z) pts[MAXT + z] = R->SOC_pct[z] / 100;  // ROMmdls(t,z).SOC
   auto Cval = [&](int m, int q, int k) { return R->C[((size_t)m * nz + q) * n1 + k]; };
   auto Dval = [&](int m, int q) { return R->D[(size_t)m * nz + q]; };
-  // cell blob: per model [C nzp x 5][D nzp][a 5]
-  r.cell_stride = nzp * NX + nzp + NX;
+  // cell blob: per model [C nzp x 5][D nzp][a 5][a_p a_q, packed Sigma order 15]
+  // An odd stride in doubles: lanes reading one offset of different models then spread
+  // over all LDS banks (an even stride such as 176 folds them onto 2 bank positions).
+  r.cell_stride = (nzp * NX + nzp + NX + NPK) | 1;
+  int pr[NPK], pc[NPK];
+  for (int p = 0, i = 0; p < NX; ++p)
+    for (int q = p; q < NX; ++q, ++i) { pr[i] = p; pc[i] = q; }
   std::vector<double> cb((size_t)NM * r.cell_stride, 0.0);
   for (int m = 0; m < NM; ++m) {
     double *b = cb.data() + (size_t)m * r.cell_stride;
@@ -277,6 +282,8 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       b[nzp * NX + q] = Dval(m, perm[q]);
     }
     for (int k = 0; k < NX; ++k) b[nzp * NX + nzp + k] = R->A[(size_t)m * n1 + k];
+    for (int i = 0; i < NPK; ++i)  // Sigma time update coefficients (iterEKF.m:78)
+      b[nzp * NX + nzp + NX + i] = R->A[(size_t)m * n1 + pr[i]] * R->A[(size_t)m * n1 + pc[i]];
   }
   r.cell_tab = (int)cb.size();
   cb.insert(cb.end(), tabs.begin(), tabs.end());
@@ -297,16 +304,14 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   pb.insert(pb.end(), tabs.begin(), tabs.end());
   pb.insert(pb.end(), pts.begin(), pts.end());
   r.plant_len = (int)pb.size();
-  // bulk tables: cA/cB per EKF record element, cP per plant state
-  std::vector<double> bt((size_t)NM * (2 * REC + 6));
-  double *cA = bt.data(), *cB = cA + (size_t)NM * REC, *cP = cB + (size_t)NM * REC;
-  int pr[NPK], pc[NPK];
-  for (int p = 0, i = 0; p < NX; ++p)
-    for (int q = p; q < NX; ++q, ++i) { pr[i] = p; pc[i] = q; }
+  // bulk tables: the time-update coefficient of every EKF record element (a for xhat,
+  // a_p a_q for Sigma) and of every plant state (bigA)
+  std::vector<double> bt((size_t)NM * (REC + 6));
+  double *cC = bt.data(), *cP = cC + (size_t)NM * REC;
   for (int m = 0; m < NM; ++m) {
     const double *a = R->A + (size_t)m * n1;
-    for (int e = 0; e < NX; ++e) { cA[m * REC + e] = a[e]; cB[m * REC + e] = 1.0; }
-    for (int i = 0; i < NPK; ++i) { cA[m * REC + NX + i] = a[pr[i]]; cB[m * REC + NX + i] = a[pc[i]]; }
+    for (int e = 0; e < NX; ++e) cC[m * REC + e] = a[e];
+    for (int i = 0; i < NPK; ++i) cC[m * REC + NX + i] = a[pr[i]] * a[pc[i]];
     for (int e = 0; e < 6; ++e) cP[m * 6 + e] = a[e];
   }
   if (cell_lds_bytes(r) > 160 * 1024)

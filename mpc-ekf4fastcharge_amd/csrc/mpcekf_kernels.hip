@@ -1366,7 +1366,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
       for (int k = tsj[j] + 1; k < lazy_t; ++k) {  // OB_step.m:198-200 for the skipped steps
         const double u = s.hist_u[(size_t)(k % LAZY_H) * s.n + c];
 #pragma unroll
-        for (int e = 0; e < 6; ++e) xs[j][e] = a[e] * xs[j][e] + u;
+        for (int e = 0; e < 6; ++e) xs[j][e] = __builtin_fma(a[e], xs[j][e], u);
       }
     }
   }
@@ -1416,7 +1416,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
       double2 *p = reinterpret_cast<double2 *>(bx + (size_t)mm[j] * 6);
       double x[6];
 #pragma unroll
-      for (int e = 0; e < 6; ++e) x[e] = a[e] * xs[j][e] + Iapp;
+      for (int e = 0; e < 6; ++e) x[e] = __builtin_fma(a[e], xs[j][e], Iapp);
       p[0] = make_double2(x[0], x[1]);
       p[1] = make_double2(x[2], x[3]);
       p[2] = make_double2(x[4], x[5]);
@@ -1433,9 +1433,9 @@ __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const
   extern __shared__ double lds[];
   const int NM = r.NM;
   const int ne = NM * REC, np = NM * 6;
-  stage_lds(lds, r.bulk_tab, 2 * ne + np);
+  stage_lds(lds, r.bulk_tab, ne + np);
   __syncthreads();
-  const double *cA = lds, *cB = lds + ne, *cP = lds + 2 * ne;
+  const double *cC = lds, *cP = lds + ne;
   const double W = cf.SigmaW;
   for (int64_t c = blockIdx.x; c < s.n; c += gridDim.x) {
     if (do_ekf) {
@@ -1446,8 +1446,8 @@ __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const
         double2 v = base[j];
         double add0 = e0 < NX ? pri : W;
         double add1 = e0 + 1 < NX ? pri : W;
-        v.x = (cA[2 * j] * v.x) * cB[2 * j] + add0;
-        v.y = (cA[2 * j + 1] * v.y) * cB[2 * j + 1] + add1;
+        v.x = __builtin_fma(cC[2 * j], v.x, add0);
+        v.y = __builtin_fma(cC[2 * j + 1], v.y, add1);
         base[j] = v;
       }
     }
@@ -1456,8 +1456,8 @@ __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const
       double2 *base = reinterpret_cast<double2 *>(s.bigx + (size_t)c * np);
       for (int j = threadIdx.x; j < np / 2; j += blockDim.x) {
         double2 v = base[j];
-        v.x = cP[2 * j] * v.x + u;
-        v.y = cP[2 * j + 1] * v.y + u;
+        v.x = __builtin_fma(cP[2 * j], v.x, u);
+        v.y = __builtin_fma(cP[2 * j + 1], v.y, u);
         base[j] = v;
       }
     }
@@ -1472,10 +1472,10 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
   extern __shared__ double lds[];
   const int NM = r.NM;
   const int ne = NM * REC, np = NM * 6;
-  stage_lds(lds, r.bulk_tab, 2 * ne + np);
-  double *hp = lds + 2 * ne + np, *hu = hp + LAZY_H;
+  stage_lds(lds, r.bulk_tab, ne + np);
+  double *hp = lds + ne + np, *hu = hp + LAZY_H;
   int *tse = reinterpret_cast<int *>(hu + LAZY_H), *tsp = tse + NM;
-  const double *cA = lds, *cB = lds + ne, *cP = lds + 2 * ne;
+  const double *cC = lds, *cP = lds + ne;
   const double W = cf.SigmaW;
   for (int64_t c = blockIdx.x; c < s.n; c += gridDim.x) {
     __syncthreads();  // previous cell's LDS rings/timestamps fully consumed
@@ -1497,8 +1497,8 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
       const bool x0 = (e0 % REC) < NX, x1 = ((e0 + 1) % REC) < NX;
       for (int k = ts + 1; k <= t; ++k) {
         const double p = hp[k % LAZY_H];
-        v.x = (cA[e0] * v.x) * cB[e0] + (x0 ? p : W);
-        v.y = (cA[e0 + 1] * v.y) * cB[e0 + 1] + (x1 ? p : W);
+        v.x = __builtin_fma(cC[e0], v.x, x0 ? p : W);
+        v.y = __builtin_fma(cC[e0 + 1], v.y, x1 ? p : W);
       }
       be[j] = v;
     }
@@ -1510,8 +1510,8 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
       double2 v = bp[j];
       for (int k = ts + 1; k <= t; ++k) {
         const double u = hu[k % LAZY_H];
-        v.x = cP[e0] * v.x + u;
-        v.y = cP[e0 + 1] * v.y + u;
+        v.x = __builtin_fma(cP[e0], v.x, u);
+        v.y = __builtin_fma(cP[e0 + 1], v.y, u);
       }
       bp[j] = v;
     }
@@ -1533,15 +1533,16 @@ __device__ __forceinline__ void replay_x(double x[NX], const double *a, int ts, 
   for (int k = ts + 1; k <= t; ++k) {
     const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
 #pragma unroll
-    for (int e = 0; e < NX; ++e) x[e] = a[e] * x[e] + p;
+    for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], x[e], p);
   }
 }
+// a: the model's diag(A) [NX] followed by its a_p a_q coefficients [NPK] (cell blob)
 __device__ __forceinline__ void replay_S(double S[NPK], const double *a, int ts, int t, double W) {
   for (int k = ts + 1; k <= t; ++k) {
 #pragma unroll
     for (int i = 0, pp = 0; pp < NX; ++pp)
 #pragma unroll
-      for (int q = pp; q < NX; ++q, ++i) S[i] = (a[pp] * S[i]) * a[q] + W;
+      for (int q = pp; q < NX; ++q, ++i) S[i] = __builtin_fma(a[NX + i], S[i], W);
   }
 }
 
@@ -1573,11 +1574,9 @@ __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc
     for (int k = ts[j] + 1; k <= t; ++k) {
       const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
 #pragma unroll
-      for (int e = 0; e < NX; ++e) x[j][e] = a[e] * x[j][e] + p;
+      for (int e = 0; e < NX; ++e) x[j][e] = __builtin_fma(a[e], x[j][e], p);
 #pragma unroll
-      for (int i = 0, pp = 0; pp < NX; ++pp)
-#pragma unroll
-        for (int q = pp; q < NX; ++q, ++i) S[j][i] = (a[pp] * S[j][i]) * a[q] + W;
+      for (int i = 0; i < NPK; ++i) S[j][i] = __builtin_fma(a[NX + i], S[j][i], W);
     }
   }
 #pragma unroll
@@ -1591,7 +1590,7 @@ __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc
 // ---------------------------------------------------------------------------
 // k_cell: iterEKF measurement update + EKFmatsHandler + iterMPC (lane per cell)
 // ---------------------------------------------------------------------------
-template <int NZ>
+template <int NZ, int PARTS>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
   stage_lds(lds, r.cell_blob, r.cell_len);
@@ -1642,7 +1641,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   double vhat = 0.0, Zsoc = 0.0;
   XI xi;
   double ik = 0.0, vk = 0.0;
-  if (io.mode & (MODE_EKF | MODE_FUSED)) {
+  if ((PARTS & P_EKF) && (io.mode & (MODE_EKF | MODE_FUSED))) {
     if (st & ST_ERROR) {
       fail_outputs();
       return;
@@ -1810,15 +1809,21 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
     }
   }
+  if (!(PARTS & P_MPC)) return;
+  // The fused step's second kernel: cells the iterEKF kernel failed are finished.
+  if (!(PARTS & P_EKF) && fused) {
+    if (st & ST_ERROR) return;
+    vk = s.vk[c];
+  }
 
   Lin L;
   if (io.mode & (MODE_LIN | MODE_FUSED)) {
     double zr[NROLE];
-    if (fused) {
+    if (fused && (PARTS & P_EKF)) {
 #pragma unroll
       for (int q = 0; q < NROLE; ++q) zr[q] = Z[q];
     } else {
-      if (st & ST_ERROR) { fail_outputs(); return; }
+      if (!fused && (st & ST_ERROR)) { fail_outputs(); return; }
 #pragma unroll
       for (int q = 0; q < NROLE; ++q) zr[q] = io.zk_in[c * (nz + 2) + r.perm[q]];
       Zsoc = io.zk_in[c * (nz + 2) + nz + 1];
@@ -2339,7 +2344,7 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
 
 int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream) {
   if (s.n == 0) return 0;
-  int lds = (int)((2 * r.NM * REC + r.NM * 6 + 2 * LAZY_H) * sizeof(double) + 2 * r.NM * sizeof(int));
+  int lds = (int)((r.NM * REC + r.NM * 6 + 2 * LAZY_H) * sizeof(double) + 2 * r.NM * sizeof(int));
   int grid = (int)(s.n < 2048 ? s.n : 2048);
   hipLaunchKernelGGL(k_flush, dim3(grid), dim3(256), lds, (hipStream_t)stream, r, c, s, t, new_ts);
   return (int)hipGetLastError();
@@ -2348,31 +2353,44 @@ int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_t
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream) {
   if (s.n == 0) return 0;
-  int lds = (int)((2 * r.NM * REC + r.NM * 6) * sizeof(double));
+  int lds = (int)((r.NM * REC + r.NM * 6) * sizeof(double));
   int grid = (int)(s.n < 2048 ? s.n : 2048);
   hipLaunchKernelGGL(k_bulk, dim3(grid), dim3(256), lds, (hipStream_t)stream, r, c, s, iapp, do_plant, do_ekf);
   return (int)hipGetLastError();
 }
 
-template <int NZ>
+template <int NZ, int PARTS>
 static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   int lds = cell_lds_bytes(r);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_cell<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(k_cell<NZ>, dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+  hipLaunchKernelGGL((k_cell<NZ, PARTS>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
 }
 
-int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream) {
-  if (s.n == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  switch (r.nzp) {
-    case 26: launch_cell_t<26>(r, c, s, io, st); break;
-    case 32: launch_cell_t<32>(r, c, s, io, st); break;
+template <int NZ>
+static int launch_cell_nz(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st, int parts) {
+  switch (parts) {
+    case P_EKF: launch_cell_t<NZ, P_EKF>(r, c, s, io, st); return 0;
+    case P_MPC: launch_cell_t<NZ, P_MPC>(r, c, s, io, st); return 0;
+    case P_ALL: launch_cell_t<NZ, P_ALL>(r, c, s, io, st); return 0;
     default: return -1;
   }
+}
+
+int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int parts) {
+  if (s.n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = -1;
+  switch (r.nzp) {
+    case 26: rc = launch_cell_nz<26>(r, c, s, io, st, parts); break;
+    case 32: rc = launch_cell_nz<32>(r, c, s, io, st, parts); break;
+    default: return -1;
+  }
+  if (rc) return rc;
   return (int)hipGetLastError();
 }
 

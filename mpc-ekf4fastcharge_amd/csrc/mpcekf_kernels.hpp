@@ -92,6 +92,10 @@ constexpr int NSTAMPS = 12;
 enum { BD_G = 0, BD_M = 4, BD_Z = 8, BD_X0 = 12, BD_S0 = 13, NBND = 14 };
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
+// Which blocks of k_cell an instantiation compiles: the fused step launches the iterEKF
+// part and the EKFmatsHandler + iterMPC part as two kernels (each with its own register
+// allocation), handing over zk and Xind through HBM; the stage entry points use both.
+enum { P_EKF = 1, P_MPC = 2, P_ALL = 3 };
 
 // host-side launchers (defined in mpcekf_kernels.hip)
 // lazy_t > 0: deferred mode (corners replayed/advanced in place, inputs logged to the rings)
@@ -100,7 +104,7 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
 int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream);
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
-int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream);
+int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int parts = P_ALL);
 // boundzk (iterEKF.m:186-205) from k_cell's hand-off record, a lane quad per cell
 int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk, void *stream);
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream);

@@ -619,7 +619,7 @@ double orc_plant_step(const orc_ctx *X, orc_cell *s, double Iapp) {
   for (int m = 0; m < X->NM; ++m)
     for (int k = 0; k <= NX; ++k) {
       double *x = s->bigX + (size_t)m * (NX + 1) + k;
-      *x = r->A[(size_t)m * (NX + 1) + k] * *x + Iapp;
+      *x = fma(r->A[(size_t)m * (NX + 1) + k], *x, Iapp);  /* OB_step.m:278, explicit fma */
     }
   double aZ = 0.0, aT = 0.0;
   if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
@@ -758,9 +758,11 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
     const double *a = r->A + (size_t)m * (NX + 1);
     double *x = s->xhat + (size_t)m * NX;
     double *S = s->S + (size_t)m * NPK;
-    for (int e = 0; e < NX; ++e) x[e] = a[e] * x[e] + s->priorI;
+    /* xhat = A xhat + B i, Sigma = A Sigma A' + SigmaW with A diagonal, as explicit fma:
+     * x_e = fma(a_e, x_e, i), S_pq = fma(a_p a_q, S_pq, W) (the kernels' spelling) */
+    for (int e = 0; e < NX; ++e) x[e] = fma(a[e], x[e], s->priorI);
     for (int p = 0; p < NX; ++p)
-      for (int q = p; q < NX; ++q) S[PK[p][q]] = (a[p] * S[PK[p][q]]) * a[q] + W;
+      for (int q = p; q < NX; ++q) S[PK[p][q]] = fma(a[p] * a[q], S[PK[p][q]], W);
   }
   s->x0 = s->x0 + s->priorI;
   s->S0 = s->S0 + W;
