@@ -834,7 +834,7 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
     for (int k = 0; k < NC; ++k) {
       double a = 0.0;
 #pragma unroll
-      for (int j = 0; j < NCON; ++j) a = a + X[j][k] * lam[j];
+      for (int j = 0; j < NCON; ++j) a = __builtin_fma(X[j][k], lam[j], a);
       v[k] = a;
     }
   };
@@ -852,10 +852,12 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
       double hii = 0.0;
 #pragma unroll
       for (int k = 0; k < NC; ++k) hii = hii + Mf(i, k) * X[i][k];
-      double s = 0.0;
+      double s = 0.0, w;
       if (fin) {
+        double t = K[i];
 #pragma unroll
-        for (int k = 0; k < NC; ++k) s = s + Mf(i, k) * v[k];
+        for (int k = 0; k < NC; ++k) t = __builtin_fma(Mf(i, k), v[k], t);
+        w = __builtin_fma(hii, lam[i], -t) / hii;
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -866,8 +868,8 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
           p4[j & 3] = p4[j & 3] + h * lam[j];
         }
         s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+        w = -((K[i] + s) - hii * lam[i]) / hii;
       }
-      double w = -((K[i] + s) - hii * lam[i]) / hii;
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = false;
@@ -875,7 +877,7 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
       if (fin) {
         if (isfinite(d)) {
 #pragma unroll
-          for (int k = 0; k < NC; ++k) v[k] = v[k] + X[i][k] * d;
+          for (int k = 0; k < NC; ++k) v[k] = __builtin_fma(X[i][k], d, v[k]);
         } else {
           xv(v);
         }
@@ -1081,25 +1083,13 @@ __device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], X
     fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
 }
 
-// v = X*lambda (orc_hildreth's hild_v: sums from +0 in ascending j)
-__device__ __forceinline__ void hild_v(const XS &Xs, const double L[NCON], double &v0, double &v1) {
-  double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-  for (int j = 0; j < NCON; ++j) {
-    a0 = a0 + xval(Xs, j, 0) * L[j];
-    a1 = a1 + xval(Xs, j, 1) * L[j];
-  }
-  v0 = a0;
-  v1 = a1;
-}
-
 // x / y, correctly rounded, with the divisor-only part of the hardware division
 // sequence (v_rcp_f64 + two Newton steps) independent of x, so it overlaps the
 // sweep's serial chain.  For |x|, |y| in [2^-400, 2^400] (or x == 0)
 // v_div_scale / v_div_fmas / v_div_fixup are identities and this is bit-identical
 // to the compiled x / y (tools/micro/div_check.hip: 2.1e9 random pairs, 0
 // mismatches); y == +-0 gives x * (1/y) = x / y exactly (inf / NaN by IEEE).  The
-// caller checks the domain (div_y_ok once per divisor, the x range per sweep).
+// caller checks the domain (hild_stage once per divisor, the x range per sweep).
 __device__ __forceinline__ double div_fast(double x, double y) {
   double r = __builtin_amdgcn_rcp(y);
   const double r0 = r;
@@ -1112,55 +1102,159 @@ __device__ __forceinline__ double div_fast(double x, double y) {
   const double q = __builtin_fma(e2, r, q0);
   return y == 0.0 ? x * r0 : q;
 }
-__device__ __forceinline__ bool div_y_ok(double y) {
-  const double ay = fabs(y);
-  return y == 0.0 || (ay >= 0x1p-400 && ay <= 0x1p400);
+
+// Per-lane LDS of the rank-2 sweeps: the 18 distinct X(:,i) (rows 0-7 of
+// [Cu; -Cu; I; -I] are +-a, +-b, +-c) and the 18 distinct (H_ii, 1/H_ii) pairs (H_ii of
+// a negated row is bit-identical: (-1)(-x) = x, and its 0 * (-x) term only meets
+// a nonzero sum or +0).  Layout [slot][64 lanes] double2: every read is one
+// conflict-free ds_read_b128 per wave.  1/H_ii is div_fast's divisor-only part.
+constexpr int HS_X = 3 + 3 * NP, HS_SLOTS = 2 * HS_X;
+constexpr int HILD_LDS_PER_WAVE = HS_SLOTS * 64 * 16;  // bytes
+__device__ __forceinline__ constexpr int hslot(int i) {
+  return i >= 8 ? 3 + (i - 8) : (i == 1 || i == 3) ? 1 : (i == 5 || i == 7) ? 2 : 0;
+}
+__device__ __forceinline__ constexpr bool hneg(int i) { return i == 2 || i == 3 || i == 6 || i == 7; }
+// The first row of each Toeplitz block is (H(0), 0): all zero when H(0) = 0, as for the
+// SOC block (predMat: G(1,1) = +0), so its H_ii may be 0.  These rows keep x / +-0 =
+// x * (1 / +-0) exactly (inf / NaN by IEEE) through a select; a zero H_ii elsewhere sends
+// the lane to the exact path.
+__device__ __forceinline__ constexpr bool hzero_row(int i) { return i >= 8 && (i - 8) % NP == 0; }
+__device__ __forceinline__ double2 hx(const double2 *hl, int i) {  // X(:,i)
+  const double2 x = hl[hslot(i) * 64];
+  return hneg(i) ? make_double2(-x.x, -x.y) : x;
+}
+__device__ __forceinline__ double2 hh(const double2 *hl, int i) {  // (H_ii, 1/H_ii refined)
+  return hl[(HS_X + hslot(i)) * 64];
+}
+__device__ __forceinline__ double2 *hild_lane_lds(double2 *base) {  // blocks of 256 threads
+  return base + (threadIdx.x >> 6) * (HS_SLOTS * 64) + (threadIdx.x & 63);
+}
+__device__ __forceinline__ double rcp_refined(double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  double e = __builtin_fma(-y, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-y, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+// Fills the lane's slots; returns whether every H_ii is in div_fast's divisor domain.
+__device__ __forceinline__ bool hild_stage(const Cons &Cn, const XS &Xs, double2 *hl) {
+  ConsM Mf{Cn};
+  bool yok = true;
+#pragma unroll
+  for (int sl = 0; sl < HS_X; ++sl) {
+    const int i = sl == 0 ? 0 : sl == 1 ? 1 : sl == 2 ? 5 : 8 + (sl - 3);  // representative row
+    const double x0 = xval(Xs, i, 0), x1 = xval(Xs, i, 1);
+    const double hii = (0.0 + Mf(i, 0) * x0) + Mf(i, 1) * x1;  // orc_hildreth's H(i,i)
+    const double ay = fabs(hii);
+    const bool zero_ok = hzero_row(i) && hii == 0.0;
+    yok = yok && (zero_ok || (ay >= 0x1p-400 && ay <= 0x1p400));
+    hl[sl * 64] = make_double2(x0, x1);
+    hl[(HS_X + sl) * 64] = make_double2(hii, zero_ok ? __builtin_amdgcn_rcp(hii) : rcp_refined(hii));
+  }
+  return yok;
+}
+__device__ __forceinline__ void hild_unstage(const double2 *hl, XS &Xs) {
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    Xs.a[k] = k ? hl[0].y : hl[0].x;
+    Xs.b[k] = k ? hl[64].y : hl[64].x;
+    Xs.c[k] = k ? hl[128].y : hl[128].x;
+  }
+#pragma unroll
+  for (int i = 0; i < 3 * NP; ++i) {
+    const double2 x = hl[(3 + i) * 64];
+    Xs.t[i][0] = x.x;
+    Xs.t[i][1] = x.y;
+  }
 }
 
-// One rank-2 sweep (orc_hildreth): H(i,:)*lambda = M(i,:)*v with v = X*lambda
-// recomputed at the sweep start and updated after every row.  CAREFUL = false is
-// the straight-line form (v += X(:,i)*d always, div_fast) that flags in `bad` a
-// non-finite d or an operand outside div_fast's domain; CAREFUL = true is the
-// exact rule for those cases (plain division; v recomputed from lambda after a
-// non-finite d).
-template <bool CAREFUL>
-__device__ __forceinline__ void sweep_rank2(const Cons &Cn, const XS &Xs, const double K[NCON], double L[NCON],
-                                            bool done, double tol, bool &conv, bool &bad) {
+// One rank-2 sweep (orc_hildreth, finite X and M): v = X*lambda from +0 at the sweep
+// start (fma, ascending j), t_i = fma(M_i1, v1, fma(M_i0, v0, K_i)),
+// w = fma(H_ii, lambda_i, -t_i) / H_ii, lambda_i = max(w, 0), v += X(:,i) * d by fma.
+// The fast form: straight line, no frozen lanes (the caller keeps a converged lane's
+// lambda aside), division by div_fast's last three steps.  It reports max |d| (the
+// reference's inf-norm test, hildreth.m:39), max / min |numerator| (div_fast's
+// dividend domain) and whether v ended finite (false once any d was not finite: inf
+// and NaN stay in v).
+__device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double K[NCON], double L[NCON],
+                                           double &dmax, double &xmax, double &xmin, bool &vfin) {
   ConsM Mf{Cn};
-  double v0, v1;
-  hild_v(Xs, L, v0, v1);
-  // domain / finiteness accumulators of the straight-line form, off the serial chain
-  double xmax = 0.0, xmin = 1.0, chk = 0.0;
+  asm volatile("" ::: "memory");  // reload the LDS slots each sweep (no hoisting)
+  double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NCON; ++j) {
+    const double2 x = hx(hl, j);
+    v0 = __builtin_fma(x.x, L[j], v0);
+    v1 = __builtin_fma(x.y, L[j], v1);
+  }
+  asm volatile("" ::: "memory");
+  // row i's slots are read one row ahead: ds_read latency (~76 cycles) stays off the chain
+  double2 xc = hx(hl, 0), hc = hh(hl, 0);
 #pragma unroll
   for (int i = 0; i < NCON; ++i) {
-    const double m0 = Mf(i, 0), m1 = Mf(i, 1);
-    const double hii = (0.0 + m0 * xval(Xs, i, 0)) + m1 * xval(Xs, i, 1);
-    const double sv = (0.0 + m0 * v0) + m1 * v1;
-    const double li = L[i];
-    const double num = -((K[i] + sv) - hii * li);
-    double w;
-    if (CAREFUL) {
-      w = num / hii;
-    } else {
-      w = div_fast(num, hii);
-      const double xa = fabs(num);
-      xmax = fmax(xmax, xa);
-      xmin = fmin(xmin, num == 0.0 ? 1.0 : xa);
+    double2 xn = xc, hn = hc;
+    if (i + 1 < NCON) {
+      xn = hx(hl, i + 1);
+      hn = hh(hl, i + 1);
     }
+    double t = __builtin_fma(Mf(i, 0), v0, K[i]);
+    t = __builtin_fma(Mf(i, 1), v1, t);
+    const double num = __builtin_fma(hc.x, L[i], -t);
+    const double q0 = num * hc.y;
+    const double e2 = __builtin_fma(-hc.x, q0, num);
+    const double wf = __builtin_fma(e2, hc.y, q0);
+    const double w = hzero_row(i) ? (hc.x == 0.0 ? q0 : wf) : wf;
+    xmax = fmax(xmax, fabs(num));
+    xmin = fmin(xmin, fabs(num));
+    const double nl = w > 0 ? w : 0.0;
+    const double d = nl - L[i];
+    dmax = fmax(dmax, fabs(d));
+    L[i] = nl;
+    v0 = __builtin_fma(xc.x, d, v0);
+    v1 = __builtin_fma(xc.y, d, v1);
+    xc = xn;
+    hc = hn;
+  }
+  vfin = isfinite(v0) && isfinite(v1);
+}
+
+// The exact form for lanes the fast form flagged: plain division, v recomputed from
+// lambda after a non-finite d (orc_hildreth), frozen lanes (done) keep lambda.
+__device__ __forceinline__ void sweep_careful(const Cons &Cn, const double2 *hl, const double K[NCON],
+                                              double L[NCON], bool done, double tol, bool &conv) {
+  ConsM Mf{Cn};
+  auto xv = [&](double &v0, double &v1) {
+    v0 = 0.0;
+    v1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < NCON; ++j) {
+      const double2 x = hx(hl, j);
+      v0 = __builtin_fma(x.x, L[j], v0);
+      v1 = __builtin_fma(x.y, L[j], v1);
+    }
+  };
+  asm volatile("" ::: "memory");
+  double v0, v1;
+  xv(v0, v1);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    const double2 x = hx(hl, i), hr = hh(hl, i);
+    double t = __builtin_fma(Mf(i, 0), v0, K[i]);
+    t = __builtin_fma(Mf(i, 1), v1, t);
+    const double li = L[i];
+    const double w = __builtin_fma(hr.x, li, -t) / hr.x;
     const double nl = w > 0 ? w : 0.0;
     if (!(fabs(nl - li) < tol)) conv = false;
     const double nli = done ? li : nl;
     const double d = nli - li;
     L[i] = nli;
-    if (CAREFUL && !isfinite(d)) {
-      hild_v(Xs, L, v0, v1);
+    if (!isfinite(d)) {
+      xv(v0, v1);
     } else {
-      v0 = v0 + xval(Xs, i, 0) * d;
-      v1 = v1 + xval(Xs, i, 1) * d;
+      v0 = __builtin_fma(x.x, d, v0);
+      v1 = __builtin_fma(x.y, d, v1);
     }
-    if (!CAREFUL) chk = chk + (d - d);  // NaN once any d is inf or NaN
   }
-  if (!CAREFUL) bad = !(chk == 0.0 && xmax <= 0x1p400 && xmin >= 0x1p-400);
 }
 
 // The dense sweep for lanes with a non-finite X or M entry (orc_hildreth): H(i,:)*lambda
@@ -1187,74 +1281,78 @@ __device__ __forceinline__ void sweep_dense(const Cons &Cn, const XS &Xs, const 
   }
 }
 
-// hildreth.m:32-44 for one lane; returns nexec.  Every lane of the wave stays in each
-// loop until all are done (a converged lane freezes lambda): on MI355X a wave whose
-// EXEC holds fewer than 16 lanes issues FP64 VALU up to 2.6x slower under full-chip
-// load (tools/micro/exec_micro.hip).  `done` = true makes a lane a passenger from the
-// start (no QP this step: a finite dummy problem, nothing kept).
+// hildreth.m:32-44, lane per problem, in two launches.  Every lane of a wave stays in
+// each loop until all are done: on MI355X a wave whose EXEC holds fewer than 16 lanes
+// issues FP64 VALU up to 2.6x slower under full-chip load (tools/micro/exec_micro.hip).
+// `done` = true makes a lane a passenger from the start (a finite dummy problem,
+// nothing kept).  hl = the lane's LDS slots (HILD_LDS_PER_WAVE per wave).
 //
-// Three loops, so the hot one carries nothing else (register pressure):
-//  1. the straight-line rank-2 sweep (sweep_rank2<false>) for lanes with finite X, M;
-//  2. lanes whose sweep flagged a non-finite d or an operand outside div_fast's
-//     domain restart from their warm start L0 (global) with the exact rules
-//     (sweep_rank2<true>): every sweep before the flag was bit-identical to the exact
-//     form, so the result is the exact form's;
-//  3. lanes with a non-finite X or M entry: the dense sweep.
-__device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
-                                              double tol, const double K[NCON], double Mtl[NC], bool done,
-                                              const double *L0, int64_t l0_stride) {
+// hild_fast (k_hild): the fast rank-2 sweep for lanes with finite X, M, every H_ii in
+// div_fast's divisor domain and a finite warm start.  Lanes keep sweeping after they
+// converge; the lambda they converged with goes to L0 (their warm start is no longer
+// needed) and comes back after the loop.  A lane whose sweep ends with a non-finite v
+// or a dividend outside div_fast's domain, and every lane outside the fast form's
+// domain, returns `slow` with its warm start intact in L0: every sweep before the
+// flag was bit-identical to the exact form, so restarting it with the exact rules
+// gives the exact form's result.
+// hild_slow (k_hild_slow, only waves holding a slow lane): sweep_careful for finite X
+// and M, the dense sweep otherwise.  Kept out of k_hild so that the fast loop's
+// register allocation carries none of their pressure (224 VGPRs, no AGPR traffic).
+__device__ __forceinline__ bool hild_fast(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
+                                          double tol, const double K[NCON], bool done, double2 *hl, double *L0,
+                                          int64_t l0_stride, int &nexec) {
   static_assert(NC == 2, "written for Nc = 2");
-  ConsM Mf{Cn};
-  XS Xs;
-  bool fin;
-  hild_x(Cn, E, Xs, fin);
-  int nexec = maxIter;
-  bool careful = false;
-  if (fin && !done) {
-    bool yok = true;
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) yok = yok && div_y_ok((0.0 + Mf(i, 0) * xval(Xs, i, 0)) + Mf(i, 1) * xval(Xs, i, 1));
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) yok = yok && isfinite(L[i]);
-    careful = !yok;
-  }
-  auto launder_x = [&]() {  // opaque per sweep: stops loop-invariant H entries being hoisted
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      launder(Xs.a[k]); launder(Xs.b[k]); launder(Xs.c[k]);
-#pragma unroll
-      for (int i = 0; i < 3 * NP; ++i) launder(Xs.t[i][k]);
-    }
-  };
+  bool fin, yok;
   {
-    bool fdone = done || !fin || careful;
-#pragma unroll 1
-    for (int it = 1; it <= maxIter; ++it) {
-      if (__all(fdone)) break;
-      launder_x();
-      bool conv = true, bad = false;
-      sweep_rank2<false>(Cn, Xs, K, L, fdone, tol, conv, bad);
-      if (!fdone && bad) {
-        fdone = true;
-        careful = true;
-      } else if (!fdone && conv) {
-        fdone = true;
-        nexec = it;
-      }
-    }
+    XS Xs;
+    hild_x(Cn, E, Xs, fin);
+    yok = hild_stage(Cn, Xs, hl);
   }
-  if (__any(careful)) {
-    bool cdone = !careful;
-    if (careful) {
+  nexec = maxIter;
+  bool lok = true;
 #pragma unroll
-      for (int j = 0; j < NCON; ++j) L[j] = L0[j * l0_stride];
+  for (int i = 0; i < NCON; ++i) lok = lok && isfinite(L[i]);
+  bool slow = !done && !(fin && yok && lok);
+  bool active = !done && !slow;  // still sweeping for itself
+#pragma unroll 1
+  for (int it = 1; it <= maxIter; ++it) {
+    if (__all(!active)) break;
+    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+    bool vfin;
+    sweep_fast(Cn, hl, K, L, dmax, xmax, xmin, vfin);
+    const bool bad = !(vfin && xmax <= 0x1p400 && xmin >= 0x1p-400);
+    const bool conv = dmax < tol;
+    const bool newconv = active && !bad && conv;
+    if (active && bad) slow = true;
+    if (newconv) {
+      nexec = it;
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) L0[i * l0_stride] = L[i];
     }
+    active = active && !bad && !conv;
+  }
+  // converged lanes take their lambda back; lanes at maxIter keep their last sweep's
+  if (!active && !done && !slow) {
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) L[i] = L0[i * l0_stride];
+  }
+  return slow;
+}
+
+__device__ __forceinline__ int hild_slow(const Cons &Cn, const double E[NC][NC], double L[NCON], int maxIter,
+                                         double tol, const double K[NCON], bool done, double2 *hl) {
+  bool fin;
+  XS Xs;
+  hild_x(Cn, E, Xs, fin);
+  (void)hild_stage(Cn, Xs, hl);
+  int nexec = maxIter;
+  if (__any(fin && !done)) {
+    bool cdone = done || !fin;
 #pragma unroll 1
     for (int it = 1; it <= maxIter; ++it) {
       if (__all(cdone)) break;
-      launder_x();
-      bool conv = true, bad = false;
-      sweep_rank2<true>(Cn, Xs, K, L, cdone, tol, conv, bad);
+      bool conv = true;
+      sweep_careful(Cn, hl, K, L, cdone, tol, conv);
       if (!cdone && conv) {
         cdone = true;
         nexec = it;
@@ -1266,7 +1364,12 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
 #pragma unroll 1
     for (int it = 1; it <= maxIter; ++it) {
       if (__all(ddone)) break;
-      launder_x();
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {  // opaque per sweep: no hoisting of the 529 H entries
+        launder(Xs.a[k]); launder(Xs.b[k]); launder(Xs.c[k]);
+#pragma unroll
+        for (int i = 0; i < 3 * NP; ++i) launder(Xs.t[i][k]);
+      }
       bool conv = true;
       sweep_dense(Cn, Xs, K, L, ddone, tol, conv);
       if (!ddone && conv) {
@@ -1275,14 +1378,19 @@ __device__ __forceinline__ int hildreth_sweep(const Cons &Cn, const double E[NC]
       }
     }
   }
+  return nexec;
+}
+
+// M'*lambda (hildreth.m:46; the caller adds F and solves -E\(.))
+__device__ __forceinline__ void hild_mtl(const Cons &Cn, const double L[NCON], double Mtl[NC]) {
+  ConsM Mf{Cn};
 #pragma unroll
   for (int k = 0; k < NC; ++k) {
     double s = 0.0;
 #pragma unroll
     for (int i = 0; i < NCON; ++i) s = s + Mf(i, k) * L[i];
-    Mtl[k] = s;  // M'*lambda; the caller adds F and solves -E\(.)
+    Mtl[k] = s;
   }
-  return nexec;
 }
 
 // ---------------------------------------------------------------------------
@@ -2138,12 +2246,12 @@ __device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int6
   }
 }
 
-// hildreth.m + iterMPC.m:68-95, lane per cell.
+// hildreth.m + iterMPC.m:68-95, lane per cell: the fast solve (hild_fast).
 __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
-  // every lane of the wave stays in the solve (see hildreth_sweep); cells without a
-  // QP this step ride along on a finite dummy problem and store nothing
+  // every lane of the wave stays in the solve; cells without a QP this step ride
+  // along on a finite dummy problem and store nothing
   const bool qp = s.hflag[c] != 0;
   const int64_t n = s.n;
   Cons Cn;
@@ -2157,11 +2265,47 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
 #pragma unroll
     for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
   }
-  double Mtl[NC];
-  const int nexec = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp, s.lam + c, n);
+  extern __shared__ double2 hlds[];
+  int nexec;
+  const bool slow = hild_fast(Cn, E, lam, cf.max_hild, cf.hild_tol, K, !qp, hild_lane_lds(hlds), s.lam + c, n, nexec);
   if (!qp) return;
+  if (slow) {  // k_hild_slow finishes it (warm start still in s.lam)
+    s.hflag[c] = 2;
+    return;
+  }
+  double Mtl[NC];
+  hild_mtl(Cn, lam, Mtl);
 #pragma unroll
   for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
+  hild_finish(s, io, c, Cn, Mtl, nexec);
+}
+
+// The exact-rule solve of the cells k_hild flagged (hflag 2); a wave without one leaves.
+__global__ void __launch_bounds__(64) k_hild_slow(const KCfg cf, const KState s, const KIO io) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  const bool slow = s.hflag[c] == 2;
+  if (!__any(slow)) return;
+  const int64_t n = s.n;
+  Cons Cn;
+  double E[NC][NC], K[NCON], lam[NCON];
+  if (!slow) {
+    hild_dummy(Cn, E, K);
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = 0.0;
+  } else {
+    hild_load(s, c, Cn, E, K);
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
+  }
+  extern __shared__ double2 hlds[];
+  const int nexec = hild_slow(Cn, E, lam, cf.max_hild, cf.hild_tol, K, !slow, hild_lane_lds(hlds));
+  if (!slow) return;
+  s.hflag[c] = 1;
+  double Mtl[NC];
+  hild_mtl(Cn, lam, Mtl);
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];
   hild_finish(s, io, c, Cn, Mtl, nexec);
 }
 
@@ -2240,14 +2384,15 @@ __global__ void __launch_bounds__(64) k_hildreth(int64_t n, const double *Ei, co
   nexec[c] = it;
 }
 
-// The fused solver (hildreth_sweep, as in k_hild) on constraintsMPC.m-structured
+// The fused solver (hild_fast + hild_slow, as k_hild + k_hild_slow) on constraintsMPC.m-structured
 // problems given by their Toeplitz rows: M = [Cu; -Cu; I; -I; G_v; -G_e; G_soc].
+template <bool SLOW>
 __global__ void __launch_bounds__(256) k_hildreth_structured(int64_t n, const double *Ei, const double *Fi,
                                                              const double *Hvi, const double *Hei,
                                                              const double *Hsi, const double *gi, double *lami,
                                                              int maxIter, double tol, double *DUo, int *nexec) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool real = c < n;  // lanes past n ride along (hildreth_sweep keeps the wave full)
+  const bool real = c < n;  // lanes past n ride along (hild_fast keeps the wave full)
   const int64_t cc = real ? c : 0;
   Cons Cn;
   double E[NC][NC], F[NC], K[NCON], lam[NCON];
@@ -2283,8 +2428,27 @@ __global__ void __launch_bounds__(256) k_hildreth_structured(int64_t n, const do
       lam[i] = lami[cc * NCON + i];
     }
   }
+  extern __shared__ double2 hlds[];
+  int it;
+  bool slow = false;
+  if (SLOW) {
+    slow = real && nexec[cc] < 0;
+    if (!__any(slow)) return;
+    if (!slow) {  // a finished problem rides along as a passenger
+      hild_dummy(Cn, E, K);
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) lam[i] = 0.0;
+    }
+    it = hild_slow(Cn, E, lam, maxIter, tol, K, !slow, hild_lane_lds(hlds));
+    if (!slow) return;
+  } else {
+    if (hild_fast(Cn, E, lam, maxIter, tol, K, !real, hild_lane_lds(hlds), lami + cc * NCON, 1, it)) {
+      if (real) nexec[cc] = -1;  // the second launch finishes it (warm start still in lambda)
+      return;
+    }
+  }
   double Mtl[NC];
-  const int it = hildreth_sweep(Cn, E, lam, maxIter, tol, K, Mtl, !real, lami + cc * NCON, 1);
+  hild_mtl(Cn, lam, Mtl);
   if (!real) return;
   double rhs[NC], mE[NC][NC], DU[NC];
 #pragma unroll
@@ -2416,9 +2580,20 @@ int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk
   return (int)hipGetLastError();
 }
 
+static int hild_lds_bytes() {  // 4 waves per block; one block per CU (147 KiB of 160)
+  static_assert(4 * HILD_LDS_PER_WAVE <= 160 * 1024, "Hildreth slots exceed the LDS");
+  return 4 * HILD_LDS_PER_WAVE;
+}
+
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
   if (s.n == 0) return 0;
-  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), 0, (hipStream_t)stream, c, s, io);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_hild, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), hild_lds_bytes(), (hipStream_t)stream, c, s, io);
+  hipLaunchKernelGGL(k_hild_slow, dim3(grid_for(s.n, 64)), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);
   return (int)hipGetLastError();
 }
 
@@ -2452,8 +2627,18 @@ int launch_hildreth_structured(int64_t n, const double *E, const double *F, cons
                                const double *Hs, const double *gam, double *lam, int max_iter, double tol,
                                double *DU, int *nexec, void *stream) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(k_hildreth_structured, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, n, E, F, Hv,
-                     He, Hs, gam, lam, max_iter, tol, DU, nexec);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_hildreth_structured<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_hildreth_structured<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_hildreth_structured<false>, dim3(grid_for(n, 256)), dim3(256), hild_lds_bytes(),
+                     (hipStream_t)stream, n, E, F, Hv, He, Hs, gam, lam, max_iter, tol, DU, nexec);
+  hipLaunchKernelGGL(k_hildreth_structured<true>, dim3(grid_for(n, 256)), dim3(256), hild_lds_bytes(),
+                     (hipStream_t)stream, n, E, F, Hv, He, Hs, gam, lam, max_iter, tol, DU, nexec);
   return (int)hipGetLastError();
 }
 

@@ -427,7 +427,7 @@ void orc_predmat(const double *a /*6*/, const double *C /*6*/, double D, int Np,
 static void hild_v(int Nc, int nC, const double *X, const double *lam, double *v) {
   for (int k = 0; k < Nc; ++k) {
     double a = 0.0;
-    for (int j = 0; j < nC; ++j) a = a + X[j * Nc + k] * lam[j];
+    for (int j = 0; j < nC; ++j) a = fma(X[j * Nc + k], lam[j], a);
     v[k] = a;
   }
 }
@@ -455,11 +455,12 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
   }
   /* H = M*X has rank Nc: H(i,:)*lambda = M(i,:)*v with v = X*lambda (an Nc-vector).
    * Defined evaluation (the kernels evaluate the same sequence):
-   *  - finite X and M: v recomputed from lambda at the start of every sweep (sums from
-   *    +0 in ascending j), s_i = M(i,:)*v, and after row i v += X(:,i)*(new - old
-   *    lambda(i)); when that change is not finite (a zero-diagonal row going to or
-   *    from +inf) v is recomputed from lambda instead, which reproduces the dense
-   *    form's inf/NaN propagation (0*inf terms) exactly in kind.
+   *  - finite X and M: v recomputed from lambda at the start of every sweep (fma
+   *    accumulation from +0 in ascending j), t_i = K_i + M(i,:)*v by fma in ascending k,
+   *    w = fma(H_ii, lambda_i, -t_i) / H_ii (= -(K_i + s_i - H_ii lambda_i) / H_ii), and
+   *    after row i v += X(:,i)*(new - old lambda(i)) by fma; when that change is not
+   *    finite (a zero-diagonal row going to or from +inf) v is recomputed from lambda
+   *    instead, which reproduces the dense form's inf/NaN propagation in kind.
    *  - otherwise the dense H(i,:)*lambda as 4 interleaved partial sums (terms j = q
    *    mod 4 from +0) combined as (p0+p1)+(p2+p3).
    * MATLAB's own BLAS order for H(i,:)*lambda is unpinned; the math is hildreth.m:35. */
@@ -471,23 +472,24 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
     double v[NCMAX];
     if (finite) hild_v(Nc, nC, X, lam, v);
     for (int i = 0; i < nC; ++i) {
-      double s;
+      double w, hii = H[i * HMAX + i];
       if (finite) {
-        s = 0.0;
-        for (int k = 0; k < Nc; ++k) s = s + M[i * Nc + k] * v[k];
+        double t = K[i];
+        for (int k = 0; k < Nc; ++k) t = fma(M[i * Nc + k], v[k], t);
+        w = fma(hii, lam[i], -t) / hii;
       } else {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];
-        s = (p[0] + p[1]) + (p[2] + p[3]);
+        double s = (p[0] + p[1]) + (p[2] + p[3]);
+        w = -((K[i] + s) - hii * lam[i]) / hii;
       }
-      double w = -((K[i] + s) - H[i * HMAX + i] * lam[i]) / H[i * HMAX + i];
       double nl = w > 0 ? w : 0.0;
       double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = 0;
       lam[i] = nl;
       if (finite) {
         if (isfinite(d))
-          for (int k = 0; k < Nc; ++k) v[k] = v[k] + X[i * Nc + k] * d;
+          for (int k = 0; k < Nc; ++k) v[k] = fma(X[i * Nc + k], d, v[k]);
         else
           hild_v(Nc, nC, X, lam, v);
       }

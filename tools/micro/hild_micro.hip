@@ -36,9 +36,12 @@ __global__ void __launch_bounds__(256) k_micro(const double *pr, int nprob, int 
       K[i] = sum + Cn.gam[i];
     }
   }
-  double Mtl[NC];
+
   long long t0 = clock64(), r0 = wall_clock64();
-  int it = hildreth_sweep(Cn, E, L, maxIter, tol, K, Mtl, false, p + 44, 1);
+  extern __shared__ double2 hlds[];
+  for (int i = 0; i < NCON; ++i) lam_out[c * NCON + i] = L[i];  // warm start (hild_fast's L0)
+  int it;
+  (void)hild_fast(Cn, E, L, maxIter, tol, K, false, hild_lane_lds(hlds), lam_out + c * NCON, 1, it);
   long long t1 = clock64(), r1 = wall_clock64();
   for (int i = 0; i < NCON; ++i) lam_out[c * NCON + i] = L[i];
   nexec[c] = it;
@@ -84,9 +87,11 @@ __global__ void __launch_bounds__(256) k_probe(const KCfg cf, const KState s, in
   double lam[NCON];
 #pragma unroll
   for (int i = 0; i < NCON; ++i) lam[i] = s.lam[(size_t)i * n + c];
-  double Mtl[NC];
+
   long long t0 = clock64(), r0 = wall_clock64();
-  int it = hildreth_sweep(Cn, E, lam, cf.max_hild, cf.hild_tol, K, Mtl, !qp, s.lam + c, n);
+  extern __shared__ double2 hlds[];
+  int it;
+  (void)hild_fast(Cn, E, lam, cf.max_hild, cf.hild_tol, K, !qp, hild_lane_lds(hlds), s.lam + c, n, it);
   long long t1 = clock64(), r1 = wall_clock64();
   if (!qp) return;
   it_out[c] = it;
@@ -165,7 +170,7 @@ static int ab_mode(int nfiles, char **files, int reps) {
     for (float x : t[i]) printf(" %.3f", x);
     printf(")\n");
     hipMemcpy(R[i].dlam, R[i].dlam0, (size_t)NCON * R[i].n * 8, hipMemcpyDeviceToDevice);
-    hipLaunchKernelGGL(k_probe, dim3((R[i].n + 255) / 256), dim3(256), 0, 0, cf, R[i].st, R[i].dit, R[i].dcyc,
+    hipLaunchKernelGGL(k_probe, dim3((R[i].n + 255) / 256), dim3(256), hild_lds_bytes(), 0, cf, R[i].st, R[i].dit, R[i].dcyc,
                        R[i].drt);
     hipDeviceSynchronize();
     int64_t n = R[i].n;
@@ -246,7 +251,7 @@ static int state_mode(const char *path, const char *out) {
   hipMemcpy(dlam, dlam0, lam.size() * 8, hipMemcpyDeviceToDevice);
   long long *drt;
   hipMalloc(&drt, n * 8);
-  hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), 0, 0, cf, st, dit, dcyc, drt);
+  hipLaunchKernelGGL(k_probe, dim3((n + 255) / 256), dim3(256), hild_lds_bytes(), 0, cf, st, dit, dcyc, drt);
   hipDeviceSynchronize();
   std::vector<int> it(n);
   std::vector<long long> cyc(n);
@@ -265,6 +270,8 @@ static int state_mode(const char *path, const char *out) {
 }
 
 int main(int argc, char **argv) {
+  hipFuncSetAttribute((const void *)k_micro, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipFuncSetAttribute((const void *)k_probe, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (argc > 3 && std::string(argv[1]) == "--state") return state_mode(argv[2], argv[3]);
   if (argc > 3 && std::string(argv[1]) == "--ab") return ab_mode(argc - 3, argv + 3, atoi(argv[2]));
   const char *path = argc > 1 ? argv[1] : "tools/micro/hild_problems.bin";
@@ -295,7 +302,7 @@ int main(int argc, char **argv) {
       // same problem in every lane: no divergence, the wave's own sweep latency
       for (int rep = 0; rep < 2; ++rep) {
         hipEventRecord(e0);
-        hipLaunchKernelGGL(k_micro, dim3((N + 255) / 256), dim3(N < 256 ? N : 256), 0, 0, dp + pid * PREC_M, 1, 100,
+        hipLaunchKernelGGL(k_micro, dim3((N + 255) / 256), dim3(N < 256 ? N : 256), hild_lds_bytes(), 0, dp + pid * PREC_M, 1, 100,
                            1e-6, dl, dn, dc, dr);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
