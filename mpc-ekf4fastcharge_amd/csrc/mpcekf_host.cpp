@@ -71,6 +71,9 @@ struct mpcekf_ctx {
   double *d_prob = nullptr;   // k_cell -> k_hild problem records
   double *d_zk = nullptr, *d_zbk = nullptr;
   double *d_bnd = nullptr;    // k_cell -> k_bounds records [NBND][n]
+  int *d_xm = nullptr;        // fused step: Xind hand-off iterEKF kernel -> EKFmatsHandler kernel
+  double *d_xg = nullptr;
+  bool split_cell = false;    // fused step: k_cell as two kernels (MPCEKF_SPLIT_CELL=1; slower, 0.125 vs 0.118 ms)
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
@@ -382,6 +385,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
     const int v = std::atoi(e);
     if (v >= 1 && v <= LAZY_H) X->flush_period = v;
   }
+  // MPCEKF_SPLIT_CELL=1: the fused step's k_cell as two kernels (results identical).
+  if (const char *e = std::getenv("MPCEKF_SPLIT_CELL")) X->split_cell = std::atoi(e) != 0;
   X->Tref = rom->Tref;
   X->Rgas = rom->R;
   const mpcekf_electrode *el[2] = {&rom->neg, &rom->pos};
@@ -398,7 +403,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
       (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
-      (rc = dalloc(&X->d_bnd, n * NBND)) ||
+      (rc = dalloc(&X->d_bnd, n * NBND)) || (rc = dalloc(&X->d_xg, n * 4)) ||
+      (rc = hipMalloc((void **)&X->d_xm, n * 4 * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) ||
       (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))
 #ifdef MPCEKF_STAMPS
       || (rc = dalloc(&X->d_stamps, n * NSTAMPS))
@@ -427,7 +433,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -548,7 +554,23 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.zk = X->d_zk;
     io.zbk = bounds ? X->d_zbk : nullptr;
     io.bnd = bounds ? X->d_bnd : nullptr;
-    if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+    if (X->split_cell) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
+      io.xm_out = X->d_xm;
+      io.xg_out = X->d_xg;
+      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) return rc;
+      KIO io2 = io;
+      io2.zk = nullptr;
+      io2.zbk = nullptr;
+      io2.bnd = nullptr;
+      io2.xm_out = nullptr;
+      io2.xg_out = nullptr;
+      io2.zk_in = X->d_zk;
+      io2.xm_in = X->d_xm;
+      io2.xg_in = X->d_xg;
+      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io2, X->stream, P_MPC), "cell"))) return rc;
+    } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) {
+      return rc;
+    }
     if (E) HIPCHK(hipEventRecord(E[2], X->stream));
     if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, X->d_zbk, X->stream), "bounds"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));

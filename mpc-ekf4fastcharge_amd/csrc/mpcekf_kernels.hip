@@ -220,15 +220,18 @@ __device__ __forceinline__ bool is_pd5(const double a[NPK]) {
   for (int j = 0; j < NX; ++j) {
     double s = a[pk(j, j)];
 #pragma unroll
-    for (int k = 0; k < j; ++k) s = s - (l[j][k] * l[j][k]) * d[k];
+    for (int k = 0; k < j; ++k) s = __builtin_fma(-(l[j][k] * l[j][k]), d[k], s);
     pd = pd && (s > 0);
     d[j] = s;
+    if (j + 1 < NX) {
+      const double inv = 1.0 / s;
 #pragma unroll
-    for (int i = j + 1; i < NX; ++i) {
-      double t = a[pk(j, i)];
+      for (int i = j + 1; i < NX; ++i) {
+        double t = a[pk(j, i)];
 #pragma unroll
-      for (int k = 0; k < j; ++k) t = t - (l[i][k] * l[j][k]) * d[k];
-      l[i][j] = t / s;
+        for (int k = 0; k < j; ++k) t = __builtin_fma(-(l[i][k] * l[j][k]), d[k], t);
+        l[i][j] = t * inv;
+      }
     }
   }
   return pd;
@@ -239,7 +242,7 @@ __device__ __forceinline__ bool is_pd5(const double a[NPK]) {
 __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], const double L[NX], double St,
                                                  double res) {
 #pragma unroll
-  for (int k = 0; k < NX; ++k) x[k] = x[k] + L[k] * res;
+  for (int k = 0; k < NX; ++k) x[k] = __builtin_fma(L[k], res, x[k]);
   double LS[NX];
 #pragma unroll
   for (int r = 0; r < NX; ++r) LS[r] = L[r] * St;
@@ -248,8 +251,8 @@ __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], co
   for (int r = 0; r < NX; ++r)
 #pragma unroll
     for (int c = r; c < NX; ++c) {
-      double prc = S[pk(r, c)] - LS[r] * L[c];
-      double pcr = S[pk(r, c)] - LS[c] * L[r];
+      double prc = __builtin_fma(-LS[r], L[c], S[pk(r, c)]);
+      double pcr = __builtin_fma(-LS[c], L[r], S[pk(r, c)]);
       Ps[pk(r, c)] = prc + pcr;
       a[pk(r, c)] = (prc + pcr) * 0.5;
     }
@@ -337,14 +340,29 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
     const double *Cm = cc.L + xi.m[j] * cc.stride;
     const double *Dm = Cm + NZ * NX;
     double g = xi.g[j];
+    // row q+1's C and D are read while row q computes (LDS latency off the chain)
+    double cr[NX + 1];
+#pragma unroll
+    for (int k = 0; k < NX; ++k) cr[k] = Cm[k];
+    cr[NX] = Dm[0];
 #pragma unroll
     for (int q = 0; q < NZ; ++q) {
+      double cn[NX + 1];
+      if (q + 1 < NZ) {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) cn[k] = Cm[(q + 1) * NX + k];
+        cn[NX] = Dm[q + 1];
+      }
       double acc = 0.0;
 #pragma unroll
-      for (int k = 0; k < NX; ++k) acc = acc + Cm[q * NX + k] * x[k];
-      double zj = acc + Dm[q] * ik;
-      Z[q] = Z[q] + zj * g;
+      for (int k = 0; k < NX; ++k) acc = __builtin_fma(cr[k], x[k], acc);
+      const double zj = __builtin_fma(cr[NX], ik, acc);
+      Z[q] = __builtin_fma(zj, g, Z[q]);
       launder(Z[q]);
+      if (q + 1 < NZ) {
+#pragma unroll
+        for (int k = 0; k <= NX; ++k) cr[k] = cn[k];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -1824,12 +1842,12 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int cI = 0; cI < NX; ++cI) {
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < NX; ++k) acc = acc + S1[pk(k, cI)] * ChatV[j][k];
+        for (int k = 0; k < NX; ++k) acc = __builtin_fma(S1[pk(k, cI)], ChatV[j][k], acc);
         row[cI] = acc;
       }
       double acc = 0.0;
 #pragma unroll
-      for (int cI = 0; cI < NX; ++cI) acc = acc + row[cI] * ChatV[j][cI];
+      for (int cI = 0; cI < NX; ++cI) acc = __builtin_fma(row[cI], ChatV[j][cI], acc);
       St[j] = acc + cf.SigmaV;
 #pragma unroll
       for (int k = 0; k < NX; ++k) Lg[j][k] = row[k] / St[j];
@@ -1868,7 +1886,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       __builtin_amdgcn_sched_barrier(0);
     }
     STAMP(6);
-    x0 = x0 + L0 * res;
+    x0 = __builtin_fma(L0, res, x0);
     S0 = S0 - L0 * St0 * L0;
     SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);

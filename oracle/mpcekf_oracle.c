@@ -329,13 +329,14 @@ int orc_is_pd(const double *a /*full, symmetric*/) {
   double l[NX][NX], d[NX];
   for (int j = 0; j < NX; ++j) {
     double s = a[j * NX + j];
-    for (int k = 0; k < j; ++k) s = s - (l[j][k] * l[j][k]) * d[k];
+    for (int k = 0; k < j; ++k) s = fma(-(l[j][k] * l[j][k]), d[k], s);
     if (!(s > 0)) return 0;
     d[j] = s;
+    double inv = 1.0 / s;
     for (int i = j + 1; i < NX; ++i) {
       double t = a[i * NX + j];
-      for (int k = 0; k < j; ++k) t = t - (l[i][k] * l[j][k]) * d[k];
-      l[i][j] = t / s;
+      for (int k = 0; k < j; ++k) t = fma(-(l[i][k] * l[j][k]), d[k], t);
+      l[i][j] = t * inv;
     }
   }
   return 1;
@@ -346,7 +347,7 @@ void orc_meas_cov(double *S /*packed*/, const double *L, double St, int bump) {
   double LS[NX];
   for (int r = 0; r < NX; ++r) LS[r] = L[r] * St;
   for (int r = 0; r < NX; ++r)
-    for (int c = 0; c < NX; ++c) P[r][c] = S[PK[r][c]] - LS[r] * L[c];
+    for (int c = 0; c < NX; ++c) P[r][c] = fma(-LS[r], L[c], S[PK[r][c]]);
   for (int r = 0; r < NX; ++r)
     for (int c = 0; c < NX; ++c) a[r * NX + c] = (P[r][c] + P[c][r]) * 0.5;
   /* HH = VV*SS*VV' of svd (iterEKF.m:145-146) is the polar factor of SigmaX; for the
@@ -667,9 +668,9 @@ static double get_variables(const orc_ctx *X, orc_cell *s, double ik, const orc_
     for (int q = 0; q < nz; ++q) {
       const double *c = Crow(r, xi->m[j], q);
       double acc = 0.0;
-      for (int k = 0; k < NX; ++k) acc = acc + c[k] * x[k];
-      double zj = acc + Dval(r, xi->m[j], q) * ik;
-      Z[q] = Z[q] + zj * xi->g[j];
+      for (int k = 0; k < NX; ++k) acc = fma(c[k], x[k], acc);
+      double zj = fma(Dval(r, xi->m[j], q), ik, acc);
+      Z[q] = fma(zj, xi->g[j], Z[q]);
     }
   }
   double If0 = Z[ix->If0], If3 = Z[ix->If3];
@@ -782,11 +783,11 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
     double row[NX];
     for (int c = 0; c < NX; ++c) {
       double acc = 0.0;
-      for (int k = 0; k < NX; ++k) acc = acc + S1[PK[k][c]] * ChatV[j][k];
+      for (int k = 0; k < NX; ++k) acc = fma(S1[PK[k][c]], ChatV[j][k], acc);
       row[c] = acc;
     }
     double acc = 0.0;
-    for (int c = 0; c < NX; ++c) acc = acc + row[c] * ChatV[j][c];
+    for (int c = 0; c < NX; ++c) acc = fma(row[c], ChatV[j][c], acc);
     St[j] = acc + cf->SigmaV;
     for (int k = 0; k < NX; ++k) L[j][k] = row[k] / St[j]; /* Sigma symmetric: Sigma*c == (c'*Sigma)' */
   }
@@ -796,10 +797,10 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
   for (int j = 0; j < 4; ++j) {
     double *x = s->xhat + (size_t)xi.m[j] * NX;
     double *S = s->S + (size_t)xi.m[j] * NPK;
-    for (int k = 0; k < NX; ++k) x[k] = x[k] + L[j][k] * res;
+    for (int k = 0; k < NX; ++k) x[k] = fma(L[j][k], res, x[k]);
     orc_meas_cov(S, L[j], St[j], res * res > 9 * St[j]);
   }
-  s->x0 = s->x0 + L0 * res;
+  s->x0 = fma(L0, res, s->x0);
   s->S0 = s->S0 - L0 * St0 * L0;
   SOC = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q));
   get_xind(X, Tk, SOC, &xi);
