@@ -401,7 +401,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.n = ncells;
   if ((rc = dalloc(&s.bigx, n * NM * 6)) || (rc = dalloc(&s.ekf, n * NM * REC)) ||
       (rc = dalloc(&X->d_scal, n * 10)) || (rc = dalloc(&s.lam, n * X->ncon)) ||
-      (rc = dalloc(&X->d_int, n * 4)) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
+      (rc = hipMalloc((void **)&X->d_int, (n * 4 + 1) * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) || (rc = dalloc(&X->d_prob, n * PROB_DOUBLES)) || (rc = dalloc(&X->d_const, n * 8)) ||
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
       (rc = dalloc(&X->d_bnd, n * NBND)) || (rc = dalloc(&X->d_xg, n * 4)) ||
       (rc = hipMalloc((void **)&X->d_xm, n * 4 * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) ||
@@ -417,6 +417,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.SOCn = sc; s.SOCp = sc + n; s.x0 = sc + 2 * n; s.S0 = sc + 3 * n; s.priorI = sc + 4 * n;
   s.uk_1 = sc + 5 * n; s.uk = sc + 6 * n; s.vk = sc + 7 * n; s.J_unc = sc + 8 * n; s.J_fin = sc + 9 * n;
   s.warn = X->d_int; s.status = X->d_int + n; s.nviol = X->d_int + 2 * n; s.hflag = X->d_int + 3 * n;
+  s.hslow = X->d_int + 4 * n;
+  HIPCHK(hipMemset(s.hslow, 0, sizeof(int)));
   s.prob = X->d_prob;
   s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;

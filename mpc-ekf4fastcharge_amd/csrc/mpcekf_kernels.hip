@@ -1433,6 +1433,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   const double *Tp = lds + r.plant_tab + 6 * r.ntab;
   const double *Zp = Tp + MAXT;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
   if (c >= s.n) return;
   if (lazy_t) {  // this step's inputs, for the deferred updates of every model (k_cell, k_flush)
     const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
@@ -2286,6 +2287,8 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
   extern __shared__ double2 hlds[];
   int nexec;
   const bool slow = hild_fast(Cn, E, lam, cf.max_hild, cf.hild_tol, K, !qp, hild_lane_lds(hlds), s.lam + c, n, nexec);
+  if (__any(slow) && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))
+    atomicAdd(s.hslow, 1);  // one add per wave: k_hild_slow has work
   if (!qp) return;
   if (slow) {  // k_hild_slow finishes it (warm start still in s.lam)
     s.hflag[c] = 2;
@@ -2298,9 +2301,14 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
   hild_finish(s, io, c, Cn, Mtl, nexec);
 }
 
-// The exact-rule solve of the cells k_hild flagged (hflag 2); a wave without one leaves.
+// The exact-rule solve of the cells k_hild flagged (hflag 2): one wave per block over a
+// grid-stride range of waves, gone at once when k_hild counted none.
+__device__ __forceinline__ void hild_slow_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c);
 __global__ void __launch_bounds__(64) k_hild_slow(const KCfg cf, const KState s, const KIO io) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (__builtin_amdgcn_readfirstlane(*s.hslow) == 0) return;
+  for (int64_t w = blockIdx.x; w * 64 < s.n; w += gridDim.x) hild_slow_cell(cf, s, io, w * 64 + threadIdx.x);
+}
+__device__ __forceinline__ void hild_slow_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c) {
   if (c >= s.n) return;
   const bool slow = s.hflag[c] == 2;
   if (!__any(slow)) return;
@@ -2611,7 +2619,8 @@ int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
     attr = true;
   }
   hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), hild_lds_bytes(), (hipStream_t)stream, c, s, io);
-  hipLaunchKernelGGL(k_hild_slow, dim3(grid_for(s.n, 64)), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);
+  const int gs = grid_for(s.n, 64) < 256 ? grid_for(s.n, 64) : 256;
+  hipLaunchKernelGGL(k_hild_slow, dim3(gs), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);
   return (int)hipGetLastError();
 }
 

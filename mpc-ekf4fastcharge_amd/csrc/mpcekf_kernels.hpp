@@ -59,7 +59,8 @@ struct KState {
   double *J_unc, *J_fin;
   int *nviol;
   // hand-off k_cell -> k_hild
-  int *hflag;      // [n] 1: hildreth.m must run this step
+  int *hflag;      // [n] 1: hildreth.m must run this step (2: k_hild_slow finishes it)
+  int *hslow;      // [1] waves of the current step with a k_hild_slow lane (k_plant zeroes it)
   double *prob;    // [PB_N][n] problem records (mpcekf_kernels.hip PB_*)
   // deferred all-model time update (fused mpcekf_step only): each local
   // model's record is current through step ts[c][m] of the running call; the inputs

@@ -890,7 +890,7 @@ void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, c
   L->Dsoc = 0.0;
   double TK = Tc + 273.15;
   double SOCavg = zk[r->nz + 1];
-  double SOCnAvg = fsoc(en, SOCavg), SOCpAvg = fsoc(ep, SOCavg);
+  double SOCnAvg = fsoc(en, SOCavg); /* EKFmatsHandler.m computes SOCpAvg too; unused on this path */
   double k0n = fk0(r, en, TK), k0p = fk0(r, ep, TK);
   double i0n = k0n * msqrt(zk[ix->Thetae1] * (1 - zk[ix->Thetass0]) * zk[ix->Thetass0]);
   double i0p = k0p * msqrt(zk[ix->ThetaeE] * (1 - zk[ix->Thetass3]) * zk[ix->Thetass3]);

@@ -55,9 +55,19 @@ def build(quiet=True):
 _lib = None
 
 
+def _host_has_fma():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return any(line.startswith("flags") and " fma " in line + " " for line in f)
+    except OSError:
+        return True
+
+
 def lib():
     global _lib
     if _lib is None:
+        if not _host_has_fma():
+            raise RuntimeError("the C oracle is built with -mfma (FMA3); this host CPU lacks it")
         if not os.path.exists(LIB_PATH):
             build()
         L = C.CDLL(LIB_PATH)

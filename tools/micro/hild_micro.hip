@@ -135,6 +135,8 @@ static bool load_state(const char *path, Replay &R) {
   KState st{};
   st.n = n; st.prob = R.dprob; st.lam = R.dlam; st.hflag = R.dhf; st.uk_1 = R.duk1; st.uk = R.duk; st.J_fin = R.djf;
   st.nviol = R.dnv; st.J_unc = R.djf;
+  hipMalloc(&st.hslow, sizeof(int));
+  hipMemset(st.hslow, 0, sizeof(int));
   R.st = st;
   return true;
 }
@@ -232,6 +234,8 @@ static int state_mode(const char *path, const char *out) {
   cf.hild_tol = 1e-6;
   KState st{};
   st.n = n; st.prob = dprob; st.lam = dlam; st.hflag = dhf; st.uk_1 = duk1; st.uk = duk; st.J_fin = djf;
+  hipMalloc(&st.hslow, sizeof(int));
+  hipMemset(st.hslow, 0, sizeof(int));
   st.nviol = dnv; st.J_unc = djf;
   KIO io{};
   io.mode = MODE_FUSED;

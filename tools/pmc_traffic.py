@@ -4,7 +4,7 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 exactly half the bytes of a wide (16 B/lane) coalesced streaming read
 (MI355X_MICROARCH.md §HBM), so reads are doubled; WRITE_SIZE is exact for
-16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,flush,cell,hild} (flush = the all-model
+16-B-per-lane stores.  Output: JSON with per_launch_bytes{plant,flush,cell,hild,bounds} (flush = the all-model
 time update of the fused path) and fp64_flops_per_launch.
 """
 import csv
@@ -16,8 +16,8 @@ from collections import defaultdict
 
 # kernel (exact name prefix) -> bench stage; a stage's per-step figure is the sum of
 # its kernels' per-dispatch averages (each launches once per step)
-KERNELS = {"k_plant(": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild2(": "hild",
-           "k_bulk(": "bulk"}
+KERNELS = {"k_plant(": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild_slow(": "hild",
+           "k_bounds<": "bounds", "k_bulk(": "bulk"}
 
 
 def read_counter(d, name):
