@@ -1594,57 +1594,85 @@ __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const
 // k_flush: brings every local model (EKF record and plant state) of every cell
 // from its timestamp to step t with the logged inputs, then stamps it new_ts.
 // Block per cell, the cell's input rings and timestamps staged in LDS.
+// Lane per model: a wave takes one cell at a time (grid-stride) with its lanes on
+// models m0 + lane; the model's coefficients (diag(A) for xhat, a_p a_q for Sigma, bigA
+// for the plant) stay in registers across cells, the record (26 doubles) is loaded once,
+// replayed step by step and stored once.  The step inputs come from the lane holding
+// that ring slot (readlane; k is wave-uniform), so a step is 26 FMAs and no memory.
+__device__ __forceinline__ double rl64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, const KState s, const int t,
                                                const int new_ts) {
-  extern __shared__ double lds[];
   const int NM = r.NM;
-  const int ne = NM * REC, np = NM * 6;
-  stage_lds(lds, r.bulk_tab, ne + np);
-  double *hp = lds + ne + np, *hu = hp + LAZY_H;
-  int *tse = reinterpret_cast<int *>(hu + LAZY_H), *tsp = tse + NM;
-  const double *cC = lds, *cP = lds + ne;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const double W = cf.SigmaW;
-  for (int64_t c = blockIdx.x; c < s.n; c += gridDim.x) {
-    __syncthreads();  // previous cell's LDS rings/timestamps fully consumed
-    for (int k = threadIdx.x; k < LAZY_H; k += blockDim.x) {
-      hp[k] = s.hist_p[(size_t)k * s.n + c];
-      hu[k] = s.hist_u[(size_t)k * s.n + c];
-    }
-    for (int m = threadIdx.x; m < NM; m += blockDim.x) {
-      tse[m] = s.ts_ekf[c * NM + m];
-      tsp[m] = s.ts_plant[c * NM + m];
-    }
-    __syncthreads();
-    double2 *be = reinterpret_cast<double2 *>(s.ekf + (size_t)c * ne);
-    for (int j = threadIdx.x; j < ne / 2; j += blockDim.x) {
-      const int e0 = 2 * j, m = e0 / REC;
-      const int ts = tse[m];
-      if (ts >= t) continue;
-      double2 v = be[j];
-      const bool x0 = (e0 % REC) < NX, x1 = ((e0 + 1) % REC) < NX;
-      for (int k = ts + 1; k <= t; ++k) {
-        const double p = hp[k % LAZY_H];
-        v.x = __builtin_fma(cC[e0], v.x, x0 ? p : W);
-        v.y = __builtin_fma(cC[e0 + 1], v.y, x1 ? p : W);
+  const double *cC = r.bulk_tab, *cP = r.bulk_tab + (size_t)NM * REC;
+  for (int m0 = 0; m0 < NM; m0 += 64) {
+    const int m = m0 + lane;
+    const bool act = m < NM;
+    const int mm = act ? m : NM - 1;
+    double ce[REC], cp[6];
+#pragma unroll
+    for (int e = 0; e < REC; ++e) ce[e] = cC[(size_t)mm * REC + e];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) cp[e] = cP[(size_t)mm * 6 + e];
+    for (int64_t c = w0; c < s.n; c += nw) {
+      const double hpl = s.hist_p[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+      const double hul = s.hist_u[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+      const int tse = act ? s.ts_ekf[c * NM + m] : t, tsp = act ? s.ts_plant[c * NM + m] : t;
+      double2 *re = reinterpret_cast<double2 *>(s.ekf + ((size_t)c * NM + mm) * REC);
+      double2 *rp = reinterpret_cast<double2 *>(s.bigx + ((size_t)c * NM + mm) * 6);
+      double xe[REC], xp[6];
+      if (tse < t) {
+#pragma unroll
+        for (int e = 0; e < REC / 2; ++e) {
+          const double2 v = re[e];
+          xe[2 * e] = v.x;
+          xe[2 * e + 1] = v.y;
+        }
       }
-      be[j] = v;
-    }
-    double2 *bp = reinterpret_cast<double2 *>(s.bigx + (size_t)c * np);
-    for (int j = threadIdx.x; j < np / 2; j += blockDim.x) {
-      const int e0 = 2 * j, m = e0 / 6;
-      const int ts = tsp[m];
-      if (ts >= t) continue;
-      double2 v = bp[j];
-      for (int k = ts + 1; k <= t; ++k) {
-        const double u = hu[k % LAZY_H];
-        v.x = __builtin_fma(cP[e0], v.x, u);
-        v.y = __builtin_fma(cP[e0 + 1], v.y, u);
+      if (tsp < t) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const double2 v = rp[e];
+          xp[2 * e] = v.x;
+          xp[2 * e + 1] = v.y;
+        }
       }
-      bp[j] = v;
-    }
-    for (int m = threadIdx.x; m < NM; m += blockDim.x) {
-      s.ts_ekf[c * NM + m] = new_ts;
-      s.ts_plant[c * NM + m] = new_ts;
+      int kmin = min(tse, tsp);
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) kmin = min(kmin, __shfl_xor(kmin, o));
+      for (int k = kmin + 1; k <= t; ++k) {  // k is wave-uniform
+        const int sl = k & (LAZY_H - 1);
+        const double p = rl64(hpl, sl), u = rl64(hul, sl);
+        if (k > tse) {
+#pragma unroll
+          for (int e = 0; e < NX; ++e) xe[e] = __builtin_fma(ce[e], xe[e], p);
+#pragma unroll
+          for (int e = NX; e < REC; ++e) xe[e] = __builtin_fma(ce[e], xe[e], W);
+        }
+        if (k > tsp) {
+#pragma unroll
+          for (int e = 0; e < 6; ++e) xp[e] = __builtin_fma(cp[e], xp[e], u);
+        }
+      }
+      if (tse < t) {
+#pragma unroll
+        for (int e = 0; e < REC / 2; ++e) re[e] = make_double2(xe[2 * e], xe[2 * e + 1]);
+      }
+      if (tsp < t) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) rp[e] = make_double2(xp[2 * e], xp[2 * e + 1]);
+      }
+      if (act) {
+        s.ts_ekf[c * NM + m] = new_ts;
+        s.ts_plant[c * NM + m] = new_ts;
+      }
     }
   }
 }
@@ -2534,9 +2562,10 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
 
 int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream) {
   if (s.n == 0) return 0;
-  int lds = (int)((r.NM * REC + r.NM * 6 + 2 * LAZY_H) * sizeof(double) + 2 * r.NM * sizeof(int));
-  int grid = (int)(s.n < 2048 ? s.n : 2048);
-  hipLaunchKernelGGL(k_flush, dim3(grid), dim3(256), lds, (hipStream_t)stream, r, c, s, t, new_ts);
+  static_assert((LAZY_H & (LAZY_H - 1)) == 0 && LAZY_H <= 64, "k_flush: ring slots live in lanes");
+  // persistent waves: 3 per SIMD (k_flush holds ~140 VGPRs), striding over cells
+  const int64_t waves = s.n < 3072 ? s.n : 3072;
+  hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts);
   return (int)hipGetLastError();
 }
 
