@@ -88,7 +88,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cells-per-gpu", type=int, default=65536)
     ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
-    ap.add_argument("--cpu-cells", type=int, default=4096)
+    ap.add_argument("--cpu-cells", type=int, default=32768)
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")

@@ -433,6 +433,25 @@ static void hild_v(int Nc, int nC, const double *X, const double *lam, double *v
   }
 }
 
+/* t_i = K_i + M(i,:)*v of the rank form.  Nc <= 2 (the lane-per-cell kernels): fma in
+ * ascending k.  Nc > 2 (the 16-lane-group kernels, lane k holding v_k): a_0 = fma(M_i0, v_0,
+ * K_i), a_k = M_ik*v_k for 0 < k < Nc, a_k = +0 for Nc <= k < 16, summed as the pairwise
+ * tree ((a0+a1)+(a2+a3)) + ((a4+a5)+(a6+a7)) ... over the 16 slots (the lane butterfly). */
+static double hild_row_t(int Nc, const double *Mi, const double *v, double Ki) {
+  if (Nc <= 2) {
+    double t = Ki;
+    for (int k = 0; k < Nc; ++k) t = fma(Mi[k], v[k], t);
+    return t;
+  }
+  double a[16];
+  a[0] = fma(Mi[0], v[0], Ki);
+  for (int k = 1; k < 16; ++k) a[k] = 0.0;
+  for (int k = 1; k < Nc && k < 16; ++k) a[k] = Mi[k] * v[k];
+  for (int w = 1; w < 16; w *= 2)
+    for (int k = 0; k < 16; k += 2 * w) a[k] = a[k] + a[k + w];
+  return a[0];
+}
+
 int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double *M /*nC x Nc*/,
                  const double *gam, double *lam /*in: warm start, out*/, int maxIter, double tol,
                  double *DU) {
@@ -457,7 +476,7 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
   /* H = M*X has rank Nc: H(i,:)*lambda = M(i,:)*v with v = X*lambda (an Nc-vector).
    * Defined evaluation (the kernels evaluate the same sequence):
    *  - finite X and M: v recomputed from lambda at the start of every sweep (fma
-   *    accumulation from +0 in ascending j), t_i = K_i + M(i,:)*v by fma in ascending k,
+   *    accumulation from +0 in ascending j), t_i = K_i + M(i,:)*v as hild_row_t,
    *    w = fma(H_ii, lambda_i, -t_i) / H_ii (= -(K_i + s_i - H_ii lambda_i) / H_ii), and
    *    after row i v += X(:,i)*(new - old lambda(i)) by fma; when that change is not
    *    finite (a zero-diagonal row going to or from +inf) v is recomputed from lambda
@@ -475,8 +494,7 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
     for (int i = 0; i < nC; ++i) {
       double w, hii = H[i * HMAX + i];
       if (finite) {
-        double t = K[i];
-        for (int k = 0; k < Nc; ++k) t = fma(M[i * Nc + k], v[k], t);
+        double t = hild_row_t(Nc, M + i * Nc, v, K[i]);
         w = fma(hii, lam[i], -t) / hii;
       } else {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
