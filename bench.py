@@ -30,7 +30,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32):
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32, Np=5, Nc=2):
     """Algorithmic HBM bytes each kernel moves per cell per launch:
     the state it must read and write once, with nothing re-read.
 
@@ -51,6 +51,13 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32):
     cell = 4 * 2 * 8 * 20 + 4 * 2 * 4 + 8 + 20 * 8 + 4 * 8 + zk + 51 * 8 + (14 * 8 if bounds else 0)
     plant = 4 * 2 * 6 * 8 + 4 * 2 * 4 + 2 * 8 + 12 * 8 + 8
     hild = 51 * 8 + 2 * 8 * ncon + 4 * 8
+    if (Np, Nc) != (5, 2):
+        # wide horizons (mpcekf_wide.hip): k_cell hands over the 35-double linearisation
+        # record + zk(end); the QP record E, F, Hv, He, Hs, gamma, e, Ru, uk_1 and the
+        # hildreth.m setup X (ncon x Nc), K, H_ii are written by k_mpc_wide and read back
+        prob = Nc * Nc + Nc + 4 * Np + ncon + 2
+        cell = cell - 51 * 8 + 36 * 8
+        hild = 2 * 8 * (36 + prob + ncon * (Nc + 2)) + 2 * 8 * ncon + 4 * 8
     out = dict(flush=flush, cell=cell, plant=plant, hild=hild)
     if bounds:
         out["bounds"] = 14 * 8 + 15 * 8 + 4 * 8 + 28 * 8
@@ -70,11 +77,11 @@ def batch_inputs(n, seed=0x5EED):
     return rng.uniform(5, 30, n), rng.uniform(20, 30, n)
 
 
-def cpu_baseline(rom, soc0, tc, cells, steps, threads):
+def cpu_baseline(rom, soc0, tc, cells, steps, threads, Np=5, Nc=2):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c
     t0 = time.perf_counter()
-    oracle_c.run(rom, soc0[:cells], tc[:cells], steps, nthreads=threads)
+    oracle_c.run(rom, soc0[:cells], tc[:cells], steps, nthreads=threads, Np=Np, Nc=Nc)
     dt = time.perf_counter() - t0
     return dict(value=cells * steps / dt, unit="cell-steps/s", cores=threads, kind="port",
                 sample=f"C oracle (oracle/mpcekf_oracle.c, -O3 fp64, OpenMP) on the first {cells} cells "
@@ -88,6 +95,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cells-per-gpu", type=int, default=65536)
     ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
+    ap.add_argument("--np", type=int, default=5, help="prediction horizon (configs[4]: 20)")
+    ap.add_argument("--nc", type=int, default=2, help="control horizon (configs[4]: 10)")
     ap.add_argument("--cpu-cells", type=int, default=32768)
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -111,7 +120,8 @@ def main():
     total = cpg * world
     soc0_all, tc_all = batch_inputs(total)
     sl = slice(rank * cpg, (rank + 1) * cpg)
-    cfg = M.make_config(bounds=bool(args.bounds))
+    cfg = M.make_config(bounds=bool(args.bounds), Np=args.np, Nc=args.nc)
+    ncon = 4 * args.nc + 3 * args.np
     ctx = M.Context(rom, cpg, cfg, device=local)
     ctx.init_cells(soc0_all[sl], tc_all[sl])
     dev = torch.device("cuda", local)
@@ -146,7 +156,7 @@ def main():
     if rank == 0:
         cell_steps = total * K
         value = cell_steps / dt if dt > 0 else 0.0
-        bpc = algorithmic_bytes_per_cell(rom.NM, 23, bool(args.bounds))
+        bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
         per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1], ms_total=tim[k][0])
                       for k in tim if tim[k][1] > 0}
         # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
@@ -169,7 +179,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps or (W + K),
-                               args.cpu_threads)
+                               args.cpu_threads, Np=args.np, Nc=args.nc)
         line = {
             "metric": METRIC,
             "value": value,
@@ -184,9 +194,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (synthetic NMC30-like ROM; SOC0~U[5,30]%, TC~U[20,30]C, seed 0x5EED)",
             "config": {
-                "workload": f"{cpg} cells per GPU ({total} total), Np=5 Nc=2, closed loop runMPC.m:84-111 "
+                "workload": f"{cpg} cells per GPU ({total} total), Np={args.np} Nc={args.nc}, closed loop runMPC.m:84-111 "
                             f"incl. plant, boundzk={'on' if args.bounds else 'off'}",
-                "cells_per_gpu": cpg, "total_cells": total, "Np": 5, "Nc": 2, "models_per_cell": rom.NM,
+                "cells_per_gpu": cpg, "total_cells": total, "Np": args.np, "Nc": args.nc, "models_per_cell": rom.NM,
                 "rom_outputs": rom.nz, "parallelism": f"cell-shard x{world} (no data-path collective)",
             },
             "roofline": {
@@ -195,8 +205,8 @@ def main():
                 "algorithmic_bytes_per_cell": bpc[dom],
                 "fp64": fp64,
                 "step_equivalent": {
-                    "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, 23),
-                    "achieved": value * survey_bytes_per_cell_step(rom.NM, 23) / 1e9, "unit": "GB/s",
+                    "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, ncon),
+                    "achieved": value * survey_bytes_per_cell_step(rom.NM, ncon) / 1e9, "unit": "GB/s",
                     "note": "SURVEY.md 8(d): whole-step state r+w per cell-step x cell-steps/s",
                 },
             },

@@ -41,7 +41,8 @@ int fail(int code, const char *fmt, ...) {
     if (e_ != hipSuccess) return fail(MPCEKF_E_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
   } while (0)
 
-constexpr int NCON_BUILT = 4 * 2 + 3 * 5;  // Np = 5, Nc = 2 compiled into the kernels
+constexpr int NCON_BUILT = 4 * 2 + 3 * 5;  // Np = 5, Nc = 2 compiled into the lane-per-cell kernels
+int ncon_of(int Np, int Nc) { return 4 * Nc + 3 * Np; }  // constraintsMPC.m, all switches on
 
 template <class T>
 int dalloc(T **p, size_t n) {
@@ -77,6 +78,10 @@ struct mpcekf_ctx {
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
+  // wide horizons (Np = 20, Nc = 10; mpcekf_wide.hip): k_cell hands the linearisation over
+  bool wide = false;
+  KWide w{};
+  double *d_lin = nullptr, *d_zsoc = nullptr;  // [n][35], [n]
   int flush_period = LAZY_H;      // steps between all-model flushes (<= LAZY_H)
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
@@ -336,8 +341,9 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
 }
 
 static int check_cfg(const mpcekf_config *c) {
-  if (c->Np != 5 || c->Nc != 2)
-    return fail(MPCEKF_E_UNSUPPORTED, "Np=%d Nc=%d: this build compiles the GPU step for Np=5, Nc=2", c->Np, c->Nc);
+  if (!(c->Np == 5 && c->Nc == 2) && !wide_supported(c->Np, c->Nc))
+    return fail(MPCEKF_E_UNSUPPORTED, "Np=%d Nc=%d: this build compiles the GPU step for Np/Nc = 5/2 and 20/10",
+                c->Np, c->Nc);
   if (!c->use_current || !c->use_voltage || !c->use_eta)
     return fail(MPCEKF_E_UNSUPPORTED, "constraint switches must all be on (runMPC.m:33) in this build");
   if (c->max_hild < 1) return fail(MPCEKF_E_ARG, "max_hild < 1");
@@ -376,7 +382,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   X->device = device;
   X->n = ncells;
   X->cfg = *cfg;
-  X->ncon = NCON_BUILT;
+  X->ncon = ncon_of(cfg->Np, cfg->Nc);
+  X->wide = wide_supported(cfg->Np, cfg->Nc);
   if ((rc = build_rom(X, rom))) { mpcekf_ctx_destroy(X); return rc; }
   fill_kcfg(cfg, rom->Q, X->k);
   // Diagnostic override (tests/test_gpu_parity.py shows results do not depend on it):
@@ -425,6 +432,22 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
   s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
+  if (X->wide) {
+    KWide &w = X->w;
+    w.Np = cfg->Np; w.Nc = cfg->Nc; w.ncon = X->ncon;
+    const size_t nc = (size_t)X->ncon;
+    if ((rc = dalloc(&w.prob, n * wide_prob_doubles(w.Np, w.Nc))) || (rc = dalloc(&w.X, nc * n * w.Nc)) ||
+        (rc = dalloc(&w.K, nc * n)) || (rc = dalloc(&w.hii, nc * n)) || (rc = dalloc(&w.it, n)) ||
+        (rc = dalloc(&w.smin, (size_t)w.Nc * w.Nc + 1)) || (rc = dalloc(&X->d_lin, n * MPCEKF_LIN_SIZE)) ||
+        (rc = dalloc(&X->d_zsoc, n))) {
+      mpcekf_ctx_destroy(X);
+      return rc;
+    }
+    // mpc_setup's sigma_min cache: GsocT*Gsoc for Csoc = [0 0 0 0 0 -Ts/(3600 Q)] (EKFmatsHandler.m:43-45)
+    rc = launch_wide_smin(w, -rom->Ts / (3600 * rom->Q), rom->A, X->stream);
+    if (rc) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "smin kernel: %s", hipGetErrorString((hipError_t)rc)); }
+    HIPCHK(hipStreamSynchronize(X->stream));
+  }
   *out = X;
   return MPCEKF_OK;
 }
@@ -435,7 +458,8 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->stream) (void)hipStreamSynchronize(X->stream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
-                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg};
+                  X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
+                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -556,7 +580,18 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.zk = X->d_zk;
     io.zbk = bounds ? X->d_zbk : nullptr;
     io.bnd = bounds ? X->d_bnd : nullptr;
-    if (X->split_cell) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
+    KIO iow{};  // wide horizons: iterMPC in mpcekf_wide.hip from the linearisation record
+    if (X->wide) {
+      io.lin_out = X->d_lin;
+      io.zsoc_out = X->d_zsoc;
+      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF | P_LIN), "cell"))) return rc;
+      iow.mode = MODE_FUSED;
+      iow.lin_in = X->d_lin;
+      iow.soc_k1_in = X->d_zsoc;
+      iow.u = io.u;
+      iow.nexec = io.nexec;
+      if ((rc = lerr(launch_mpc_wide(X->k, X->s, iow, X->w, X->stream), "mpc_wide"))) return rc;
+    } else if (X->split_cell) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
       io.xm_out = X->d_xm;
       io.xg_out = X->d_xg;
       if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) return rc;
@@ -576,7 +611,11 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     if (E) HIPCHK(hipEventRecord(E[2], X->stream));
     if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, X->d_zbk, X->stream), "bounds"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));
-    if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+    if (X->wide) {
+      if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
+    } else if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
+      return rc;
+    }
     if (E) HIPCHK(hipEventRecord(E[4], X->stream));
     if (t % X->flush_period == 0 || t == nsteps) {
       if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
@@ -739,8 +778,13 @@ int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, doub
   io.soc_k1_in = ds;
   io.uk_out = du;
   io.nexec = dn;
-  if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-  if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+  if (X->wide) {
+    if ((rc = lerr(launch_mpc_wide(X->k, X->s, io, X->w, X->stream), "mpc_wide"))) return rc;
+    if ((rc = lerr(launch_hild_wide(X->k, X->s, io, X->w, X->stream), "hild_wide"))) return rc;
+  } else {
+    if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
+    if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
+  }
   HIPCHK(hipMemcpyAsync(uk, du, n * 8, hipMemcpyDeviceToHost, X->stream));
   if (nexec) HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
@@ -765,7 +809,8 @@ extern "C" {
 int mpcekf_predmat(int device, int64_t n, int32_t Np, int32_t Nc, const double *a, const double *C, const double *D,
                    double *Phi, double *G) {
   if (n < 0 || (n && (!a || !C || !D || !Phi || !G))) return fail(MPCEKF_E_ARG, "predmat: bad argument");
-  if (Np != 5 || Nc != 2) return fail(MPCEKF_E_UNSUPPORTED, "predmat: built for Np=5, Nc=2");
+  const bool wide = wide_supported(Np, Nc);
+  if (!(Np == 5 && Nc == 2) && !wide) return fail(MPCEKF_E_UNSUPPORTED, "predmat: built for Np/Nc = 5/2 and 20/10");
   if (n == 0) return MPCEKF_OK;
   HIPCHK(hipSetDevice(device));
   DevScope d;
@@ -776,7 +821,8 @@ int mpcekf_predmat(int device, int64_t n, int32_t Np, int32_t Nc, const double *
   HIPCHK(hipMemcpyAsync(da, a, n * 6 * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(dC, C, n * 6 * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(dD, D, n * 8, hipMemcpyHostToDevice, d.st));
-  int rc = lerr(launch_predmat(n, Np, Nc, da, dC, dD, dP, dG, d.st), "predmat");
+  int rc = lerr(wide ? launch_predmat_wide(n, Np, Nc, da, dC, dD, dP, dG, d.st)
+                     : launch_predmat(n, Np, Nc, da, dC, dD, dP, dG, d.st), "predmat");
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(Phi, dP, n * Np * 7 * 8, hipMemcpyDeviceToHost, d.st));
   HIPCHK(hipMemcpyAsync(G, dG, n * Np * Nc * 8, hipMemcpyDeviceToHost, d.st));
@@ -796,14 +842,17 @@ int mpcekf_constraints(int device, const mpcekf_config *cfg, double Q, int64_t n
   HIPCHK(hipSetDevice(device));
   DevScope d;
   HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
-  const int ncon = NCON_BUILT;
-  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * (MPCEKF_LIN_SIZE + 2 + ncon * 2 + ncon) * 8 + 1024));
-  double *dl = (double *)d.buf, *du = dl + n * MPCEKF_LIN_SIZE, *ds = du + n, *dM = ds + n, *dg = dM + n * ncon * 2;
+  const int ncon = ncon_of(cfg->Np, cfg->Nc), Nc = cfg->Nc;
+  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * (MPCEKF_LIN_SIZE + 2 + ncon * Nc + ncon) * 8 + 1024));
+  double *dl = (double *)d.buf, *du = dl + n * MPCEKF_LIN_SIZE, *ds = du + n, *dM = ds + n, *dg = dM + n * ncon * Nc;
   HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(du, uk_1, n * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, d.st));
-  if ((rc = lerr(launch_constraints(k, n, dl, du, ds, dM, dg, d.st), "constraints"))) return rc;
-  HIPCHK(hipMemcpyAsync(M, dM, n * ncon * 2 * 8, hipMemcpyDeviceToHost, d.st));
+  if ((rc = lerr(wide_supported(cfg->Np, Nc) ? launch_constraints_wide(k, cfg->Np, Nc, n, dl, du, ds, dM, dg, d.st)
+                                               : launch_constraints(k, n, dl, du, ds, dM, dg, d.st),
+                 "constraints")))
+    return rc;
+  HIPCHK(hipMemcpyAsync(M, dM, n * ncon * Nc * 8, hipMemcpyDeviceToHost, d.st));
   HIPCHK(hipMemcpyAsync(gamma, dg, n * ncon * 8, hipMemcpyDeviceToHost, d.st));
   HIPCHK(hipStreamSynchronize(d.st));
   return MPCEKF_OK;
@@ -877,6 +926,7 @@ int mpcekf_get_hild_problems(mpcekf_ctx *X, double *prob, int32_t *hflag) {
   int rc = need_init(X);
   if (rc) return rc;
   static_assert(MPCEKF_PROB_DOUBLES == PROB_DOUBLES, "problem record size");
+  if (X->wide) return fail(MPCEKF_E_UNSUPPORTED, "get_hild_problems: Np = 5 / Nc = 2 records only");
   const size_t n = (size_t)X->n;
   if (prob) HIPCHK(hipMemcpyAsync(prob, X->s.prob, n * PROB_DOUBLES * 8, hipMemcpyDeviceToHost, X->stream));
   if (hflag) HIPCHK(hipMemcpyAsync(hflag, X->s.hflag, n * 4, hipMemcpyDeviceToHost, X->stream));

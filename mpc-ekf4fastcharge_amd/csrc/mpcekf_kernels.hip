@@ -1567,7 +1567,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
     }
   }
-  if (!(PARTS & P_MPC)) return;
+  if (!(PARTS & (P_MPC | P_LIN))) return;
   // The fused step's second kernel: cells the iterEKF kernel failed are finished.
   if (!(PARTS & P_EKF) && fused) {
     if (st & ST_ERROR) return;
@@ -1592,6 +1592,18 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
   }
   STAMP(10);
+  if (PARTS & P_LIN) {  // iterMPC runs in the wide-horizon kernels (mpcekf_wide.hip) from lin_out / zsoc_out
+    if (fused) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc = acc + L.Cphi[k] * L.xhat[k];
+      if (io.phise) io.phise[c] = acc + s.uk[c] * L.Dphi + L.bphi;  // runMPC.m:94-95
+      if (io.v) io.v[c] = vk;
+      if (io.soc) io.soc[c] = Zsoc;
+      if (io.zsoc_out) io.zsoc_out[c] = Zsoc;
+    }
+    return;
+  }
 
 #ifndef PROBE_NO_MPC
   if (io.mode & (MODE_MPC | MODE_FUSED)) {
@@ -2199,6 +2211,7 @@ static int launch_cell_nz(const KRom &r, const KCfg &c, const KState &s, const K
     case P_EKF: launch_cell_t<NZ, P_EKF>(r, c, s, io, st); return 0;
     case P_MPC: launch_cell_t<NZ, P_MPC>(r, c, s, io, st); return 0;
     case P_ALL: launch_cell_t<NZ, P_ALL>(r, c, s, io, st); return 0;
+    case P_EKF | P_LIN: launch_cell_t<NZ, P_EKF | P_LIN>(r, c, s, io, st); return 0;
     default: return -1;
   }
 }

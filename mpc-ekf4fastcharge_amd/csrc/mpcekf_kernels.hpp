@@ -86,6 +86,7 @@ struct KIO {
   int lazy_t;             // > 0: fused step t of the running call with deferred time update
   double *bnd;            // [NBND][n] boundzk hand-off k_cell -> k_bounds (with zbk)
   long long *stamps;      // [MPCEKF_NSTAMPS][n] s_memtime per k_cell section (-DMPCEKF_STAMPS builds only)
+  double *zsoc_out;       // [n] zk(end) for the wide-horizon MPC kernels (P_LIN, fused)
 };
 constexpr int NSTAMPS = 12;
 // k_cell -> k_bounds record: g[4], m[4], Z(te1, th0, tee, th3), x0, S0.  k_bounds reads
@@ -96,7 +97,18 @@ enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 // Which blocks of k_cell an instantiation compiles: the fused step launches the iterEKF
 // part and the EKFmatsHandler + iterMPC part as two kernels (each with its own register
 // allocation), handing over zk and Xind through HBM; the stage entry points use both.
-enum { P_EKF = 1, P_MPC = 2, P_ALL = 3 };
+enum { P_EKF = 1, P_MPC = 2, P_ALL = 3, P_LIN = 4 };  // P_EKF | P_LIN: iterEKF + EKFmatsHandler only (wide MPC)
+
+// Scratch of the wide-horizon MPC stage (mpcekf_wide.hip; Np = 20, Nc = 10): the
+// Hildreth problem, X = E\M', K = M*(E\F) + gamma and H_ii per constraint row.
+struct KWide {
+  int Np, Nc, ncon;
+  double *prob;    // [wide_prob_doubles][n]: E, F, Hv, He, Hs, gamma, e, Ru, uk_1
+  double *X;       // [ncon][n][Nc]  X(:,i) = E\M(i,:)'
+  double *K, *hii; // [ncon][n]
+  int *it;         // [n] hildreth.m sweeps (nexec)
+  double *smin;    // [Nc*Nc + 1] GsocT*Gsoc of the configuration and its sigma_min
+};
 
 // host-side launchers (defined in mpcekf_kernels.hip)
 // lazy_t > 0: deferred mode (corners replayed/advanced in place, inputs logged to the rings)
@@ -122,6 +134,21 @@ int launch_hildreth_structured(int64_t n, const double *E, const double *F, cons
                                double *DU, int *nexec, void *stream);
 int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream);
 bool cell_kernel_supported(int nzp);
+
+// wide-horizon MPC stage (mpcekf_wide.hip)
+bool wide_supported(int Np, int Nc);
+int wide_prob_doubles(int Np, int Nc);
+// GsocT*Gsoc + sigma_min cache for mpc_setup (rr = -Ts/(3600 Q), a = diag(A) of one model)
+int launch_wide_smin(const KWide &w, double rr, const double *a6, void *stream);
+// iterMPC setup from the linearisation records io.lin_in [n][35] and io.soc_k1_in [n]
+int launch_mpc_wide(const KCfg &c, const KState &s, const KIO &io, const KWide &w, void *stream);
+// hildreth.m (16-lane groups, exact lane-per-cell path for the rest) and iterMPC.m:75-95
+int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide &w, void *stream);
+// context-free predMat / constraintsMPC / hildreth at the wide horizons
+int launch_predmat_wide(int64_t n, int Np, int Nc, const double *a, const double *C, const double *D, double *Phi,
+                        double *G, void *stream);
+int launch_constraints_wide(const KCfg &c, int Np, int Nc, int64_t n, const double *lin, const double *uk_1,
+                            const double *soc_k1, double *M, double *gam, void *stream);
 int cell_lds_bytes(const KRom &r);
 int plant_lds_bytes(const KRom &r);
 

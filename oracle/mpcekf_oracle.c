@@ -888,6 +888,7 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
 typedef struct {
   double a[NX + 1], Csoc[NX + 1], Dsoc, Cv[NX + 1], Dv, Cphi[NX + 1], Dphi, bv, bphi, xhat[NX + 1];
 } orc_lin;
+_Static_assert(sizeof(orc_lin) == 35 * sizeof(double), "orc_lin is the 35-double record");
 
 /* EKFmatsHandler.m:26-114 */
 void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, const double *zk, double Tc,
@@ -1086,6 +1087,30 @@ void orc_mpc_step(const orc_rom *r, const orc_cfg *cf, orc_cell *s, const orc_li
     Jq = Jq + acc * DU[c];
   }
   o->J_fin = J + Jq;
+}
+
+/* iterMPC.m:17-95 on given EKFmatsHandler records (the 35-double layout of orc_lin,
+ * include/mpcekf.h MPCEKF_LIN_*): open-loop parity of the MPC stage.  uk_1 and lam
+ * ([n][nC]) are the mpcData state in and out. */
+int orc_mpc_lin(const orc_rom *r, const orc_cfg *c, int n, const double *lin, const double *soc_k1, double *uk_1,
+                double *lam, double *uk, int32_t *nexec) {
+  if (c->Np > NPMAX || c->Nc > NCMAX) return -10;
+  const int nC = (c->use_cur ? 4 * c->Nc : 0) + (c->use_v ? c->Np : 0) + (c->use_eta ? c->Np : 0) + c->Np;
+  for (int i = 0; i < n; ++i) {
+    orc_cell s;
+    memset(&s, 0, sizeof s);
+    s.uk_1 = uk_1[i];
+    for (int j = 0; j < nC; ++j) s.lam[j] = lam[(size_t)i * nC + j];
+    orc_lin L;
+    memcpy(&L, lin + (size_t)i * 35, sizeof L);
+    orc_mpc_out o;
+    orc_mpc_step(r, c, &s, &L, soc_k1[i], &o);
+    uk[i] = o.uk;
+    nexec[i] = o.nexec;
+    uk_1[i] = s.uk_1;
+    for (int j = 0; j < nC; ++j) lam[(size_t)i * nC + j] = s.lam[j];
+  }
+  return 0;
 }
 
 /* ----------------------------------------------------------------------- */

@@ -77,6 +77,8 @@ def lib():
         L.orc_predmat.argtypes = [_dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp]
         L.orc_hildreth.restype = C.c_int
         L.orc_hildreth.argtypes = [C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_int, C.c_double, _dp]
+        L.orc_mpc_lin.restype = C.c_int
+        L.orc_mpc_lin.argtypes = [C.POINTER(_Rom), C.POINTER(_Cfg), C.c_int, _dp, _dp, _dp, _dp, _dp, _ip]
         L.orc_sigma_min.restype = C.c_double
         L.orc_sigma_min.argtypes = [C.c_int, _dp]
         L.orc_meas_cov.argtypes = [_dp, _dp, C.c_double, C.c_int]
@@ -162,6 +164,24 @@ def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, **cfg):
     if want_zk:
         out["zk"], out["zbk"] = zk, zbk
     return out
+
+
+def mpc_lin(rom, lin, soc_k1, uk_1, lam, **cfg):
+    """iterMPC.m on given linearisation records [n, 35]; uk_1 [n] and lam [n, ncon] are the
+    mpcData state (copied).  Returns uk, nexec, uk_1 after, lam after."""
+    lin = np.ascontiguousarray(lin, dtype=np.float64)
+    n = lin.shape[0]
+    pr = PackedRom(rom)
+    c = make_cfg(**cfg)
+    u1 = np.array(uk_1, dtype=np.float64)
+    lm = np.array(lam, dtype=np.float64, order="C")
+    uk = np.empty(n)
+    ne = np.empty(n, dtype=np.int32)
+    rc = lib().orc_mpc_lin(C.byref(pr.s), C.byref(c), n, _p(lin), _p(np.ascontiguousarray(soc_k1, dtype=np.float64)),
+                           _p(u1), _p(lm), _p(uk), ne.ctypes.data_as(_ip))
+    if rc:
+        raise RuntimeError(f"orc_mpc_lin failed: {rc}")
+    return uk, ne, u1, lm
 
 
 def predmat(a, Cr, D, Np, Nc):

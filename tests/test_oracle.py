@@ -199,3 +199,47 @@ def test_numpy_and_c_oracle_agree_short(rom, oc):
     r = oc.run(rom, [17.0], [23.0], 120, nthreads=1)
     for k in ("u", "v", "soc", "phise"):
         assert rel(r[k][:, 0], out[k]).max() <= 1e-13
+
+
+def test_c_oracle_wide_horizon_matches_numpy(rom, oc):
+    """Np = 20 / Nc = 10 (BASELINE.json configs[4]): the C restatement (rank-Nc Hildreth
+    with the lane-tree row order, Jacobi polar) against the MATLAB-faithful numpy one
+    (dense H, LAPACK svd) on two cells x 30 closed-loop steps."""
+    onp = importlib.import_module("oracle_np")
+    soc0, tc = np.array([10.0, 27.0]), np.array([25.0, 21.0])
+    r = oc.run(rom, soc0, tc, 30, nthreads=2, Np=20, Nc=10)
+    for i in range(2):
+        g = onp.run_cell(rom, soc0[i], tc[i], 30, cfg=dict(Np=20, Nc=10))
+        for k in ("u", "v", "soc", "phise"):
+            assert rel(r[k][:, i], g[k]).max() <= 1e-12, (i, k)
+        np.testing.assert_array_equal(r["nexec"][:, i], g["nexec"])
+
+
+def test_oracle_mpc_lin_matches_numpy_iter_mpc(rom, oc):
+    """orc_mpc_lin (the open-loop MPC entry of the GPU tests) against oracle_np.iter_mpc on
+    the numpy restatement's own linearisations along a closed loop (Np = 20, Nc = 10)."""
+    onp = importlib.import_module("oracle_np")
+    c = dict(onp.RUNMPC_DEFAULTS)
+    c.update(Np=20, Nc=10)
+    soc0, tc = 20.0, 25.0
+    ekf = onp.init_kf(rom, soc0, tc, np.diag([1.0] * rom.n + [2e6]), c["SigmaV"], c["SigmaW"])
+    mpc = onp.init_mpc(rom, soc0, c["Np"], c["Nc"], c["targetSOC"], c)
+    cs = onp.ob_step_init(rom, soc0, tc)
+    uk = 0.0
+    onp.ob_step(uk, tc, cs)
+    with np.errstate(all="ignore"):
+        for k in range(12):
+            V = onp.ob_step(uk, tc, cs)
+            zk, _, Xind = onp.iter_ekf(ekf, V, uk, tc)
+            MPC, xhat = onp.ekf_mats_handler(ekf, Xind, zk, tc)
+            mpc["SOCk_1"] = zk[-1]
+            lin = np.concatenate([MPC["a"], MPC["Csoc"], [MPC["Dsoc"]], MPC["Cv"], [MPC["Dv"]], MPC["Cphi"],
+                                  [MPC["Dphi"], MPC["bv"], MPC["bphi"]], xhat])[None, :]
+            lam_in = np.zeros(100) if mpc["lam"] is None else np.array(mpc["lam"], dtype=float)
+            u1, lam0 = np.array([mpc["uk_1"]]), lam_in[None, :]
+            uk, info = onp.iter_mpc(xhat, MPC, mpc)
+            uk_c, ne_c, _, lam_c = oc.mpc_lin(rom, lin, np.array([zk[-1]]), u1, lam0, Np=20, Nc=10)
+            assert rel(uk_c, [uk]).max() <= 1e-12, k
+            assert ne_c[0] == info["nexec"], k
+            lam_np = lam_in if mpc["lam"] is None else np.asarray(mpc["lam"], dtype=float)
+            assert rel(lam_c[0], lam_np).max() <= 1e-9, k
