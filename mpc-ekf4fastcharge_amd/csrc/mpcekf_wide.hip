@@ -3,15 +3,18 @@
 //
 // The fused step runs k_cell as iterEKF + EKFmatsHandler only (P_EKF | P_LIN) and
 // hands the linearisation record to:
-//   k_mpc_wide        lane per cell   iterMPC.m:17-66 (predMat.m x3, adaptive Ru,
-//                                     unconstrained LS, constraintsMPC.m, violation
-//                                     test) and, when hildreth.m must run, its setup
-//                                     (hildreth.m:17-29): X = E\M', K, H_ii
-//   k_hild_wide       16-lane group   hildreth.m:32-42 sweeps; lane k holds v_k and
-//                     per cell        column k of X in registers, row values are
-//                                     summed by a DPP butterfly (oracle hild_row_t)
-//   k_hild_wide_slow  lane per cell   the exact rules (inf/NaN rows, non-finite X or
-//                                     M, non-SPD E) from the warm start
+//   k_mpc_wide        lane per cell   iterMPC.m:17-66: predMat.m x3, adaptive Ru, the
+//                                     unconstrained LS solve, constraintsMPC.m and the
+//                                     violation test, streamed row by row (no M or
+//                                     gamma arrays live); finishes cells that need no QP
+//   k_hild_prep       lane per cell   hildreth.m:17-29: R = chol(E), X(:,i) = E\M(i,:)'
+//                                     for the 80 distinct rows, K = M*(E\F) + gamma, H_ii
+//   k_hild_wide       16-lane group   hildreth.m:32-42 sweeps: lane k holds v_k and
+//                     per cell        column k of X in registers; row values are summed
+//                                     by a DPP butterfly (oracle hild_row_t)
+//   k_hild_wide_slow  lane per cell   the exact rules (inf/NaN rows, non-finite X or M,
+//                                     non-SPD E, divisions outside the fast form's
+//                                     domain) from the warm start
 //   k_mpc_wide_finish lane per cell   hildreth.m:46 DU = -E\(F + M'*lambda) and
 //                                     iterMPC.m:75-95
 // A cell's QP has nC = 4 Nc + 3 Np = 100 rows and rank-Nc H = M E^-1 M' (SURVEY.md
@@ -36,25 +39,59 @@ struct W {
   // problem record, SoA [field][n]
   static constexpr int E = 0, F = E + NC * NC, HV = F + NC, HE = HV + NP, HS = HE + NP, GAM = HS + NP,
                        ERR = GAM + NCON, RU = ERR + NP, UK1 = RU + 1, N = UK1 + 1;
-  static constexpr int HPW = NC - 1 + NP;          // one Toeplitz block, NC - 1 leading zeros
-  static constexpr int CELL_LDS = 3 * NCON + 3 * HPW;  // doubles per cell in k_hild_wide
-  static constexpr int GROUPS = 16;                // cells per 256-thread block
+  // X is kept for the distinct rows only: [Cu (NC); I (NC); G_v, -G_e, G_soc (3 NP)];
+  // the -Cu / -I rows use -X (E\(-b) = -(E\b) up to the sign of zero entries, which
+  // never reaches a result: every sum they enter starts from +0).
+  static constexpr int NX_ROWS = 2 * NC + 3 * NP;
+  static constexpr int HPW = NC - 1 + NP;             // one Toeplitz block, NC - 1 leading zeros
+  static constexpr int CELL_LDS = 4 * NCON + 3 * HPW;  // k_hild_wide doubles per cell
+  static constexpr int GROUPS = 16;                   // cells per 256-thread block
 };
 
+// distinct-row slot of constraint row i, and whether row i is the negated copy
 template <int NP, int NC>
-__device__ __forceinline__ void load_cons(const double *pb, int64_t n, int64_t c, ConsT<NP, NC> &Cn,
-                                          bool with_gam) {
-  using T = W<NP, NC>;
+__device__ __forceinline__ constexpr int xslot(int i) {
+  return i < NC ? i : i < 2 * NC ? i - NC : i < 3 * NC ? i - NC : i < 4 * NC ? i - 2 * NC : i - 2 * NC;
+}
+template <int NC>
+__device__ __forceinline__ constexpr bool xneg(int i) {
+  return (i >= NC && i < 2 * NC) || (i >= 3 * NC && i < 4 * NC);
+}
+
+// One step k of predmat_s's recurrence: H(k) and row k of Phi.
+__device__ __forceinline__ void pred_step(const double a[6], const double Cb[7], double S[6], double P[6], double &H,
+                                          double row[7]) {
+  double acc = 0.0;
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    Cn.Hv[i] = pb[(T::HV + i) * n + c];
-    Cn.He[i] = pb[(T::HE + i) * n + c];
-    Cn.Hs[i] = pb[(T::HS + i) * n + c];
-  }
-  if (with_gam) {
+  for (int j = 0; j < 6; ++j) acc = acc + Cb[j] * S[j];
+  acc = acc + Cb[6] * 1.0;
+  H = acc;
 #pragma unroll
-    for (int i = 0; i < T::NCON; ++i) Cn.gam[i] = pb[(T::GAM + i) * n + c];
+  for (int j = 0; j < 6; ++j) {
+    S[j] = a[j] * S[j] + 1.0;
+    P[j] = a[j] * P[j];
   }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) row[j] = 0.0 + Cb[j] * P[j];
+  double acc2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) acc2 = acc2 + Cb[j] * S[j];
+  row[6] = acc2 + Cb[6] * 1.0;
+}
+__device__ __forceinline__ double rowdot(const double row[7], const double dx[7]) {
+  double acc = 0.0;
+#pragma unroll
+  for (int k = 0; k < NA; ++k) acc = acc + row[k] * dx[k];
+  return acc;
+}
+
+// M(i, j) of the constant rows [Cu; -Cu; I; -I] (constraintsMPC.m:23-42), mval's literals
+template <int NC>
+__device__ __forceinline__ double mconst(int i, int j) {
+  if (i < NC) return j <= i ? 1.0 : 0.0;
+  if (i < 2 * NC) return -((j <= i - NC) ? 1.0 : 0.0);
+  if (i < 3 * NC) return (i - 2 * NC) == j ? 1.0 : 0.0;
+  return -((i - 3 * NC) == j ? 1.0 : 0.0);
 }
 
 template <int NP, int NC>
@@ -66,13 +103,25 @@ __device__ __forceinline__ void load_E(const double *pb, int64_t n, int64_t c, d
     for (int b = 0; b < NC; ++b) E[a][b] = pb[(T::E + a * NC + b) * n + c];
 }
 
+// sigma_min of GsocT*Gsoc out of line, from the copy k_mpc_wide left in the record's E
+// slots: GsocT*Gsoc is a batch constant (the cached value hits), so the Jacobi runs only
+// for foreign linearisations and must not add to k_mpc_wide's registers.
+template <int NC>
+__device__ __noinline__ double sigma_min_cold(const double *g, int64_t n) {
+  double G[NC][NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) G[a][b] = g[(size_t)(a * NC + b) * n];
+  return sigma_min_n<NC>(G);
+}
+
 // ---------------------------------------------------------------------------
-// k_mpc_wide: iterMPC.m:17-66 per cell, then hildreth.m:17-29 when it must run
+// k_mpc_wide: iterMPC.m:17-66 per cell (mpc_setup's arithmetic, streamed)
 // ---------------------------------------------------------------------------
 template <int NP, int NC>
 __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, const KIO io, const KWide w) {
   using T = W<NP, NC>;
-  constexpr int NCON = T::NCON;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
   if (c >= n) return;
@@ -85,72 +134,224 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
     }
     return;
   }
+  double *pb = w.prob;
   Lin L;
   lin_load(io.lin_in + c * 35, L);
   const double SOCk_1 = io.soc_k1_in[c];
-  double uk_1 = s.uk_1[c];
-  MpcSetupT<NP, NC> P;
-  MpcOut o;
-  const bool need = mpc_setup<NP, NC>(cf, L, uk_1, SOCk_1, P, o, w.smin);
-  if (s.J_unc) s.J_unc[c] = o.J_unc;
-  if (!need) {
-    mpc_finish<NP, NC>(P.Cn, P.e, P.Ru, P.DU, uk_1, o);
-    s.uk_1[c] = uk_1;
-    if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
-    if (io.uk_out) io.uk_out[c] = o.uk;
+  const double uk_1 = s.uk_1[c];
+  double dx[NA];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dx[k] = L.xhat[k];
+  dx[6] = uk_1;
+  // predMat(Csoc): Hs, e = Ref - Phi_soc*dx (iterMPC.m:20-35); the SOC constraint rows'
+  // gamma (constraintsMPC.m:89-101) from the same Phi_soc*dx
+  double Hs[NP], e[NP], gs[NP];
+  {
+    double S[6], P[6], Cb[7], row[7];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; Cb[j] = L.Csoc[j]; }
+    Cb[6] = L.Dsoc;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      pred_step(L.a, Cb, S, P, Hs[k], row);
+      const double acc = rowdot(row, dx);
+      e[k] = cf.ref * 1.0 - acc;
+      gs[k] = cf.zmax * 1.0 - (acc + SOCk_1 * 1.0);
+    }
+  }
+  double F[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) acc = acc + (-2 * (j <= i ? Hs[i - j] : 0.0)) * e[i];
+    F[j] = acc;
+  }
+  // E = 2(G'G + Ru I), Ru = ||F|| / (2 du_max sqrt(Nc)) - sigma_min(G'G) (iterMPC.m:38-47).
+  // G'G is formed twice (for the sigma_min cache test, then for E) rather than kept live.
+  auto gtg = [&](int a, int b) {
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) acc = acc + (a <= i ? Hs[i - a] : 0.0) * (b <= i ? Hs[i - b] : 0.0);
+    return acc;
+  };
+  bool hit = true;
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+      const double gab = gtg(a, b);
+      hit = hit && __double_as_longlong(gab) == __double_as_longlong(w.smin[a * NC + b]);
+      pb[(T::E + a * NC + b) * n + c] = gab;
+    }
+  const double smin = hit ? w.smin[NC * NC] : sigma_min_cold<NC>(pb + T::E * n + c, n);
+  double nF = 0.0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) nF = nF + F[j] * F[j];
+  nF = sqrt(nF);
+  const double Ru = (nF / (2 * cf.du_max * sqrt((double)NC))) - smin;
+  double mE[NC][NC], DU[NC];
+#pragma unroll
+  for (int a = 0; a < NC; ++a) {
+    pb[(T::F + a) * n + c] = F[a];
+#pragma unroll
+    for (int b = 0; b < NC; ++b) {
+      const double eab = 2 * (gtg(a, b) + Ru * (a == b ? 1.0 : 0.0));
+      pb[(T::E + a * NC + b) * n + c] = eab;
+      mE[a][b] = -eab;
+    }
+  }
+  lu_solve_n<NC>(mE, F, DU);  // DU = -E\F (iterMPC.m:48)
+  const double J_unc = mpc_cost<NP, NC>(Hs, e, Ru, DU);
+  if (s.J_unc) s.J_unc[c] = J_unc;
+  // constraintsMPC.m rows: gamma to the record, M*DU - gamma tested as each row is formed
+  int nv = 0, nviol = 0;
+#pragma unroll
+  for (int i = 0; i < 4 * NC; ++i) {
+    const double g = i < NC ? (cf.u_max - uk_1) * 1.0 : i < 2 * NC ? -(cf.u_min - uk_1) * 1.0
+                   : i < 3 * NC ? cf.du_max * 1.0 : -cf.du_min * 1.0;
+    pb[(T::GAM + i) * n + c] = g;
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc = acc + mconst<NC>(i, j) * DU[j];
+    if (acc - g > 0) nv++;
+    if (acc - g > 1e-9) nviol++;
+  }
+  {  // G_v rows: predMat(Cv, Dv), gamma = v_max - (Phi_v*dx + bv)
+    double S[6], P[6], Cb[7], row[7], Hv[NP];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; Cb[j] = L.Cv[j]; }
+    Cb[6] = L.Dv;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      pred_step(L.a, Cb, S, P, Hv[k], row);
+      const double g = cf.v_max - (rowdot(row, dx) + L.bv * 1.0);
+      pb[(T::GAM + 4 * NC + k) * n + c] = g;
+      pb[(T::HV + k) * n + c] = Hv[k];
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc = acc + (j <= k ? Hv[k - j] : 0.0) * DU[j];
+      if (acc - g > 0) nv++;
+      if (acc - g > 1e-9) nviol++;
+    }
+  }
+  {  // -G_e rows: predMat(Cphi, Dphi), gamma = -phise_min + (Phi_e*dx + bphi)
+    double S[6], P[6], Cb[7], row[7], He[NP];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; Cb[j] = L.Cphi[j]; }
+    Cb[6] = L.Dphi;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      pred_step(L.a, Cb, S, P, He[k], row);
+      const double g = -cf.phise_min + (rowdot(row, dx) + L.bphi * 1.0);
+      pb[(T::GAM + 4 * NC + NP + k) * n + c] = g;
+      pb[(T::HE + k) * n + c] = He[k];
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) acc = acc + (-(j <= k ? He[k - j] : 0.0)) * DU[j];
+      if (acc - g > 0) nv++;
+      if (acc - g > 1e-9) nviol++;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {  // G_soc rows
+    const double g = gs[k];
+    pb[(T::GAM + 4 * NC + 2 * NP + k) * n + c] = g;
+    pb[(T::HS + k) * n + c] = Hs[k];
+    pb[(T::ERR + k) * n + c] = e[k];
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) acc = acc + (j <= k ? Hs[k - j] : 0.0) * DU[j];
+    if (acc - g > 0) nv++;
+    if (acc - g > 1e-9) nviol++;
+  }
+  pb[T::RU * n + c] = Ru;
+  pb[T::UK1 * n + c] = uk_1;
+  if (nv == 0) {  // iterMPC.m:66-95 without hildreth.m: J_fin = J_unc (same DU)
+    const double uk = DU[0] + uk_1;
+    s.uk_1[c] = uk;
+    if (s.J_fin) { s.J_fin[c] = J_unc; s.nviol[c] = nviol; }
+    if (io.uk_out) io.uk_out[c] = uk;
     if (io.nexec) io.nexec[c] = 0;
     if (fused) {
-      s.uk[c] = o.uk;
-      if (io.u) io.u[c] = o.uk;
+      s.uk[c] = uk;
+      if (io.u) io.u[c] = uk;
     }
     return;
   }
-  double *pb = w.prob;
+  s.hflag[c] = 1;
+}
+
+// M(i, :) of row i as a vector (constant rows by mconst, Toeplitz rows from H)
+template <int NP, int NC>
+__device__ __forceinline__ void mrow_vec(int i, const double *Hb, double b[NC]) {
 #pragma unroll
-  for (int a = 0; a < NC; ++a) {
-    pb[(T::F + a) * n + c] = P.F[a];
-#pragma unroll
-    for (int b = 0; b < NC; ++b) pb[(T::E + a * NC + b) * n + c] = P.E[a][b];
-  }
-#pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    pb[(T::HV + i) * n + c] = P.Cn.Hv[i];
-    pb[(T::HE + i) * n + c] = P.Cn.He[i];
-    pb[(T::HS + i) * n + c] = P.Cn.Hs[i];
-    pb[(T::ERR + i) * n + c] = P.e[i];
-  }
-#pragma unroll
-  for (int i = 0; i < NCON; ++i) pb[(T::GAM + i) * n + c] = P.Cn.gam[i];
-  pb[T::RU * n + c] = P.Ru;
-  pb[T::UK1 * n + c] = uk_1;
-  // hildreth.m:28-29 as orc_hildreth: X(:,i) = E\M(i,:)' by Cholesky, H_ii = M(i,:)*X(:,i),
-  // K = M*(E\F) + gamma.  A non-SPD E (LU fallback) or a non-finite X / M goes to the
-  // exact lane-per-cell kernel, which builds all of this itself.
-  double R[NC][NC];
-  const bool ok = chol_n<NC>(P.E, R);
-  bool fin = ok;
-  if (ok) {
-    double y[NC];
-    chol_apply<NC>(R, P.F, y);
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) {
-      double b[NC], x[NC];
-#pragma unroll
-      for (int k = 0; k < NC; ++k) b[k] = mval(P.Cn, i, k);
-      chol_apply<NC>(R, b, x);
-      double h = 0.0, kk = 0.0;
-#pragma unroll
-      for (int k = 0; k < NC; ++k) {
-        h = h + b[k] * x[k];
-        kk = kk + b[k] * y[k];
-        fin = fin && isfinite(x[k]) && isfinite(b[k]);
-        w.X[((size_t)i * n + c) * NC + k] = x[k];
-      }
-      w.hii[(size_t)i * n + c] = h;
-      w.K[(size_t)i * n + c] = kk + P.Cn.gam[i];
+  for (int k = 0; k < NC; ++k) {
+    if (i < 4 * NC) {
+      b[k] = mconst<NC>(i, k);
+    } else {
+      const int blk = (i - 4 * NC) / NP, r = (i - 4 * NC) % NP;
+      const double h = k <= r ? Hb[r - k] : 0.0;
+      b[k] = blk == 1 ? -h : h;
     }
   }
-  s.hflag[c] = fin ? 1 : 2;
+}
+
+// ---------------------------------------------------------------------------
+// k_hild_prep: hildreth.m:28-29 for the cells that run it (hflag == 1)
+// ---------------------------------------------------------------------------
+// hflag after: 1 = k_hild_wide, 2 = exact path with X/K/H_ii ready, 3 = exact path
+// that must build them (E not SPD: MATLAB's \ falls back to LU).
+template <int NP, int NC>
+__global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w) {
+  using T = W<NP, NC>;
+  constexpr int NCON = T::NCON;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = s.n;
+  if (c >= n || s.hflag[c] != 1) return;
+  const double *pb = w.prob;
+  double E[NC][NC], R[NC][NC], F[NC], y[NC];
+  load_E<NP, NC>(pb, n, c, E);
+  if (!chol_n<NC>(E, R)) {
+    s.hflag[c] = 3;
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < NC; ++a) F[a] = pb[(T::F + a) * n + c];
+  chol_apply<NC>(R, F, y);
+  bool fin = true;
+  double Hb[NP];
+#pragma unroll
+  for (int i = 0; i < NCON; ++i) {
+    if (i >= 4 * NC && (i - 4 * NC) % NP == 0) {  // next Toeplitz block
+      const int blk = (i - 4 * NC) / NP;
+#pragma unroll
+      for (int r = 0; r < NP; ++r) Hb[r] = pb[(T::HV + blk * NP + r) * n + c];
+    }
+    double b[NC];
+    mrow_vec<NP, NC>(i, Hb, b);
+    double kk = 0.0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      kk = kk + b[k] * y[k];
+      fin = fin && isfinite(b[k]);
+    }
+    w.K[(size_t)c * NCON + i] = kk + pb[(T::GAM + i) * n + c];
+    if (xneg<NC>(i)) continue;  // H_ii of -b equals that of b (stored with the b row)
+    double x[NC];
+    chol_apply<NC>(R, b, x);
+    double h = 0.0;
+    const int u = xslot<NP, NC>(i);
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      h = h + b[k] * x[k];
+      fin = fin && isfinite(x[k]);
+      w.X[((size_t)u * n + c) * NC + k] = x[k];
+    }
+    w.hii[(size_t)c * NCON + i] = h;
+    if (i < NC || (i >= 2 * NC && i < 3 * NC)) w.hii[(size_t)c * NCON + i + NC] = h;
+  }
+  if (!fin) s.hflag[c] = 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -175,78 +376,142 @@ __device__ __forceinline__ double tree16(double a) {
   return a;
 }
 
-// M(i, k) of the constraintsMPC.m pattern for lane k (i compile-time); the Toeplitz
-// rows read the cell's padded impulse responses hp (exact zeros in front).
+__device__ __forceinline__ double rcp_refined_w(double y) {
+  double r = __builtin_amdgcn_rcp(y);
+  double e = __builtin_fma(-y, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-y, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// The row term a_k of hild_row_t for lane k: a_0 = fma(M_i0, v_0, K_i), a_k = M_ik v_k,
+// as fma(M_ik, v_k, kz) with kz = K_i in lane 0 and +0 elsewhere.  fma(m, v, +0) differs
+// from m*v only in the sign of a zero product, which cannot reach t: the lanes >= Nc add
+// +0, so the butterfly never returns -0.  Constant rows (M entries +-1 / +-0) become an
+// add or a select: fma(+-0, v, kz) = kz up to the sign of a zero for finite v (a
+// non-finite v ends the sweep on the exact path).
 template <int NP, int NC>
-__device__ __forceinline__ double mrow(int i, int k, const double *hp) {
-  using T = W<NP, NC>;
-  if (i < NC) return k <= i ? 1.0 : 0.0;                     // Cu
-  if (i < 2 * NC) return -((k <= i - NC) ? 1.0 : 0.0);       // -Cu
-  if (i < 3 * NC) return (i - 2 * NC) == k ? 1.0 : 0.0;      // I
-  if (i < 4 * NC) return -((i - 3 * NC) == k ? 1.0 : 0.0);   // -I
-  const int b = (i - 4 * NC) / NP, r = (i - 4 * NC) % NP;
-  const int kk = k < NC ? k : NC - 1;
-  const double h = hp[b * T::HPW + (NC - 1) + r - kk];
-  return b == 1 ? -h : h;                                    // G_v, -G_e, G_soc
+__device__ __forceinline__ double row_term(int i, int k, double v, double kz, double m) {
+  if (i < NC) return k <= i ? v + kz : kz;
+  if (i < 2 * NC) return k <= i - NC ? kz - v : kz;
+  if (i < 3 * NC) return k == i - 2 * NC ? v + kz : kz;
+  if (i < 4 * NC) return k == i - 3 * NC ? kz - v : kz;
+  const int blk = (i - 4 * NC) / NP;
+  return blk == 1 ? __builtin_fma(-m, v, kz) : __builtin_fma(m, v, kz);
+}
+// lane k's M entry of Toeplitz row i (0 for the constant rows, which row_term builds)
+template <int NP, int NC>
+__device__ __forceinline__ double row_m(int i, const double *mp) {
+  if (i < 4 * NC) return 0.0;
+  const int blk = (i - 4 * NC) / NP, r = (i - 4 * NC) % NP;
+  return mp[blk * W<NP, NC>::HPW + r];
 }
 
 template <int NP, int NC>
-__global__ void __launch_bounds__(256) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
+__global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
   using T = W<NP, NC>;
-  constexpr int NCON = T::NCON;
+  constexpr int NCON = T::NCON, HPW = T::HPW;
   extern __shared__ double lds[];
+  double *zero = lds;  // NCON zeros: lanes that add no K_i / no M entry read these
   const int g = threadIdx.x >> 4, k = threadIdx.x & 15;
   const int64_t n = s.n, c = (int64_t)blockIdx.x * T::GROUPS + g;
-  double *lam = lds + g * T::CELL_LDS, *Kl = lam + NCON, *hl = Kl + NCON, *hp = hl + NCON;
+  double *base = lds + NCON + g * T::CELL_LDS;
+  double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
+  double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
+  for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
   const bool act = c < n && s.hflag[c] == 1;
+  bool ok = true;
   if (act) {
     for (int i = k; i < NCON; i += 16) {
-      lam[i] = s.lam[(size_t)i * n + c];
-      Kl[i] = w.K[(size_t)i * n + c];
-      hl[i] = w.hii[(size_t)i * n + c];
+      const double li = s.lam[(size_t)i * n + c];
+      const double hii = w.hii[(size_t)c * NCON + i];
+      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
+      const double ay = fabs(hii);
+      ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
+      lam[i] = li;
+      Kl[i] = w.K[(size_t)c * NCON + i];
+      hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
     }
-    for (int j = k; j < 3 * T::HPW; j += 16) {
-      const int b = j / T::HPW, q = j % T::HPW;
+    for (int j = k; j < 3 * HPW; j += 16) {
+      const int b = j / HPW, q = j % HPW;
       hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
     }
   }
   __syncthreads();
   if (!act) return;
-  const int kx = k < NC ? k : 0;
-  double X[NCON];
-#pragma unroll
-  for (int i = 0; i < NCON; ++i) {
-    const double x = w.X[((size_t)i * n + c) * NC + kx];
-    X[i] = k < NC ? x : 0.0;
+  const int gshift = 16 * (g & 3);
+  if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
+    if (k == 0) s.hflag[c] = 2;
+    return;
   }
+  const double *kp = k == 0 ? Kl : zero;
+  const double *mp = k < NC ? hp + (NC - 1) - k : zero;
+  double X[T::NX_ROWS];
+#pragma unroll
+  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
   int it;
   bool slow = false;
   for (it = 1; it <= maxIter; ++it) {
+    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
+    // of the loop they would need ~400 more registers
+    asm volatile("" ::: "memory");
     double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
 #pragma unroll
-    for (int j = 0; j < NCON; ++j) v = __builtin_fma(X[j], lam[j], v);
-    bool conv = true;
+    for (int j = 0; j < NCON; ++j) {
+      if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
+      const double x = X[xslot<NP, NC>(j)];
+      v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
+    }
+    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+    // row i's LDS operands are read one row ahead (ds_read latency off the chain)
+    double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
+    double2 h = hr[0];
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
-      const double m = mrow<NP, NC>(i, k, hp);
-      const double a = k == 0 ? __builtin_fma(m, v, Kl[i]) : (k < NC ? m * v : 0.0);
-      const double t = tree16(a);
-      const double hii = hl[i], li = lam[i];
-      const double wv = __builtin_fma(hii, li, -t) / hii;
+      asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
+      double kzn = kz, lin = li, mn = m;
+      double2 hn = h;
+      if (i + 1 < NCON) {
+        kzn = kp[i + 1];
+        lin = lam[i + 1];
+        hn = hr[i + 1];
+        mn = row_m<NP, NC>(i + 1, mp);
+      }
+      const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
+      // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
+      // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
+      // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
+      const double num = __builtin_fma(h.x, li, -t);
+      const double q0 = num * h.y;
+      const double e2 = __builtin_fma(-h.x, q0, num);
+      const double wf = __builtin_fma(e2, h.y, q0);
+      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
+      const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
+      xmax = fmax(xmax, fabs(num));
+      xmin = fmin(xmin, fabs(num));
       const double nl = wv > 0 ? wv : 0.0;
       const double d = nl - li;
-      conv = conv && fabs(d) < tol;
-      slow = slow || !isfinite(d);
+      dmax = fmax(dmax, fabs(d));
       lam[i] = nl;
-      v = __builtin_fma(X[i], d, v);
+      const double x = X[xslot<NP, NC>(i)];
+      v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
+      kz = kzn;
+      li = lin;
+      h = hn;
+      m = mn;
     }
-    if (slow || conv) break;
+    // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
+    // the fast division's domain: the exact path redoes this cell from its warm start,
+    // still in s.lam (every sweep before was bit-identical to the exact form)
+    const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
+    if ((__ballot(bad) >> gshift) & 0xFFFFull) {
+      slow = true;
+      break;
+    }
+    if (dmax < tol) break;
   }
-  // A non-finite step (a zero-diagonal row going to or from +inf) switches the reference
-  // evaluation to recomputing v from lambda: k_hild_wide_slow redoes this cell from its
-  // warm start, which is still in s.lam (every sweep before was bit-identical).
   if (slow) {
     if (k == 0) s.hflag[c] = 2;
     return;
@@ -257,20 +522,39 @@ __global__ void __launch_bounds__(256) k_hild_wide(const KCfg cf, const KState s
 }
 
 // ---------------------------------------------------------------------------
-// k_hild_wide_slow: orc_hildreth with every rule, lane per cell (hflag == 2)
+// k_hild_wide_slow: orc_hildreth with every rule, lane per cell (hflag 2 / 3)
 // ---------------------------------------------------------------------------
 template <int NP, int NC>
-__device__ __forceinline__ double row_t(const ConsT<NP, NC> &Cn, int i, const double v[NC], double Ki) {
+__device__ __forceinline__ double xval_g(const double *X, int64_t n, int64_t c, int i, int k) {
+  const double x = X[((size_t)xslot<NP, NC>(i) * n + c) * NC + k];
+  return xneg<NC>(i) ? -x : x;
+}
+
+template <int NP, int NC>
+__device__ __forceinline__ double mval_rt(const double *Hall, int i, int k) {  // runtime i
+  if (i < 4 * NC) {
+    if (i < NC) return k <= i ? 1.0 : 0.0;
+    if (i < 2 * NC) return -((k <= i - NC) ? 1.0 : 0.0);
+    if (i < 3 * NC) return (i - 2 * NC) == k ? 1.0 : 0.0;
+    return -((i - 3 * NC) == k ? 1.0 : 0.0);
+  }
+  const int blk = (i - 4 * NC) / NP, r = (i - 4 * NC) % NP;
+  const double h = k <= r ? Hall[blk * NP + r - k] : 0.0;
+  return blk == 1 ? -h : h;
+}
+
+template <int NP, int NC>
+__device__ __forceinline__ double row_t_rt(const double *Hall, int i, const double v[NC], double Ki) {
   if (NC <= 2) {
     double t = Ki;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) t = __builtin_fma(mval(Cn, i, k), v[k], t);
+    for (int k = 0; k < NC; ++k) t = __builtin_fma(mval_rt<NP, NC>(Hall, i, k), v[k], t);
     return t;
   }
   double a[16];
-  a[0] = __builtin_fma(mval(Cn, i, 0), v[0], Ki);
+  a[0] = __builtin_fma(mval_rt<NP, NC>(Hall, i, 0), v[0], Ki);
 #pragma unroll
-  for (int k = 1; k < 16; ++k) a[k] = k < NC ? mval(Cn, i, k) * v[k] : 0.0;
+  for (int k = 1; k < 16; ++k) a[k] = k < NC ? mval_rt<NP, NC>(Hall, i, k) * v[k] : 0.0;
 #pragma unroll
   for (int wd = 1; wd < 16; wd *= 2)
 #pragma unroll
@@ -285,7 +569,7 @@ __device__ __forceinline__ void hild_v_g(const double *X, int64_t n, int64_t c, 
   for (int k = 0; k < NC; ++k) {
     double a = 0.0;
 #pragma unroll 1
-    for (int j = 0; j < NCON; ++j) a = __builtin_fma(X[((size_t)j * n + c) * NC + k], lam[(size_t)j * n + c], a);
+    for (int j = 0; j < NCON; ++j) a = __builtin_fma(xval_g<NP, NC>(X, n, c, j, k), lam[(size_t)j * n + c], a);
     v[k] = a;
   }
 }
@@ -296,33 +580,44 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
   constexpr int NCON = T::NCON;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
-  if (c >= n || s.hflag[c] != 2) return;
-  ConsT<NP, NC> Cn;
-  load_cons<NP, NC>(w.prob, n, c, Cn, true);
-  double E[NC][NC], F[NC], R[NC][NC], y[NC];
-  load_E<NP, NC>(w.prob, n, c, E);
+  if (c >= n || s.hflag[c] < 2) return;
+  const double *pb = w.prob;
+  double Hall[3 * NP];
 #pragma unroll
-  for (int a = 0; a < NC; ++a) F[a] = w.prob[(T::F + a) * n + c];
-  const bool ok = chol_n<NC>(E, R);
-  mldiv_spd<NC>(E, R, ok, F, y);
+  for (int r = 0; r < 3 * NP; ++r) Hall[r] = pb[(T::HV + r) * n + c];
   bool fin = true;
+  if (s.hflag[c] == 3) {  // E not SPD: X(:,i) = E\M(i,:)' by LU (MATLAB's \ fallback)
+    double E[NC][NC], F[NC], y[NC];
+    load_E<NP, NC>(pb, n, c, E);
+#pragma unroll
+    for (int a = 0; a < NC; ++a) F[a] = pb[(T::F + a) * n + c];
+    lu_solve_n<NC>(E, F, y);
 #pragma unroll 1
-  for (int i = 0; i < NCON; ++i) {
-    double b[NC], x[NC];
+    for (int i = 0; i < NCON; ++i) {
+      double b[NC], x[NC];
+      double kk = 0.0;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) b[k] = mval(Cn, i, k);
-    mldiv_spd<NC>(E, R, ok, b, x);
-    double h = 0.0, kk = 0.0;
+      for (int k = 0; k < NC; ++k) {
+        b[k] = mval_rt<NP, NC>(Hall, i, k);
+        kk = kk + b[k] * y[k];
+      }
+      w.K[(size_t)c * NCON + i] = kk + pb[(T::GAM + i) * n + c];
+      lu_solve_n<NC>(E, b, x);
+      double h = 0.0;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      h = h + b[k] * x[k];
-      kk = kk + b[k] * y[k];
-      fin = fin && isfinite(x[k]) && isfinite(b[k]);
-      w.X[((size_t)i * n + c) * NC + k] = x[k];
+      for (int k = 0; k < NC; ++k) h = h + b[k] * x[k];
+      w.hii[(size_t)c * NCON + i] = h;
+      if (!xneg<NC>(i)) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) w.X[((size_t)xslot<NP, NC>(i) * n + c) * NC + k] = x[k];
+      }
     }
-    w.hii[(size_t)i * n + c] = h;
-    w.K[(size_t)i * n + c] = kk + Cn.gam[i];
   }
+#pragma unroll 1
+  for (int i = 0; i < NCON; ++i)
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+      fin = fin && isfinite(xval_g<NP, NC>(w.X, n, c, i, k)) && isfinite(mval_rt<NP, NC>(Hall, i, k));
   double *lam = s.lam;
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
@@ -333,18 +628,18 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
     if (fin) hild_v_g<NP, NC>(w.X, n, c, lam, v);
 #pragma unroll 1
     for (int i = 0; i < NCON; ++i) {
-      const double hii = w.hii[(size_t)i * n + c], Ki = w.K[(size_t)i * n + c];
+      const double hii = w.hii[(size_t)c * NCON + i], Ki = w.K[(size_t)c * NCON + i];
       const double li = lam[(size_t)i * n + c];
       double wv;
       if (fin) {
-        wv = __builtin_fma(hii, li, -row_t<NP, NC>(Cn, i, v, Ki)) / hii;
+        wv = __builtin_fma(hii, li, -row_t_rt<NP, NC>(Hall, i, v, Ki)) / hii;
       } else {  // dense H(i,:)*lambda, 4 interleaved partial sums (orc_hildreth)
         double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
         for (int j = 0; j < NCON; ++j) {
           double h = 0.0;
 #pragma unroll
-          for (int k = 0; k < NC; ++k) h = h + mval(Cn, i, k) * w.X[((size_t)j * n + c) * NC + k];
+          for (int k = 0; k < NC; ++k) h = h + mval_rt<NP, NC>(Hall, i, k) * xval_g<NP, NC>(w.X, n, c, j, k);
           p[j & 3] = p[j & 3] + h * lam[(size_t)j * n + c];
         }
         const double sm = (p[0] + p[1]) + (p[2] + p[3]);
@@ -357,7 +652,7 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       if (fin) {
         if (isfinite(d)) {
 #pragma unroll
-          for (int k = 0; k < NC; ++k) v[k] = __builtin_fma(w.X[((size_t)i * n + c) * NC + k], d, v[k]);
+          for (int k = 0; k < NC; ++k) v[k] = __builtin_fma(xval_g<NP, NC>(w.X, n, c, i, k), d, v[k]);
         } else {
           hild_v_g<NP, NC>(w.X, n, c, lam, v);
         }
@@ -376,53 +671,83 @@ template <int NP, int NC>
 __global__ void __launch_bounds__(64) k_mpc_wide_finish(const KCfg cf, const KState s, const KIO io,
                                                         const KWide w) {
   using T = W<NP, NC>;
-  constexpr int NCON = T::NCON;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
   if (c >= n || s.hflag[c] == 0) return;
   const double *pb = w.prob;
-  ConsT<NP, NC> Cn;
-  load_cons<NP, NC>(pb, n, c, Cn, false);
+  // M'*lambda, summed over the rows in ascending order from +0 (orc_hildreth)
   double Mtl[NC];
 #pragma unroll
   for (int k = 0; k < NC; ++k) Mtl[k] = 0.0;
 #pragma unroll
-  for (int i = 0; i < NCON; ++i) {
+  for (int i = 0; i < 4 * NC; ++i) {
+    if (i % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
     const double li = s.lam[(size_t)i * n + c];
 #pragma unroll
-    for (int k = 0; k < NC; ++k) Mtl[k] = Mtl[k] + mval(Cn, i, k) * li;
+    for (int k = 0; k < NC; ++k) Mtl[k] = Mtl[k] + mconst<NC>(i, k) * li;
   }
-  double E[NC][NC], mE[NC][NC], rhs[NC], DU[NC];
-  load_E<NP, NC>(pb, n, c, E);
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    double Hb[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) Hb[r] = pb[(T::HV + blk * NP + r) * n + c];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+      if (r % 8 == 0) asm volatile("" ::: "memory");
+      const double li = s.lam[(size_t)(4 * NC + blk * NP + r) * n + c];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        const double h = k <= r ? Hb[r - k] : 0.0;
+        Mtl[k] = Mtl[k] + (blk == 1 ? -h : h) * li;
+      }
+    }
+  }
+  double mE[NC][NC], rhs[NC], DU[NC];
 #pragma unroll
   for (int a = 0; a < NC; ++a) {
     rhs[a] = pb[(T::F + a) * n + c] + Mtl[a];
 #pragma unroll
-    for (int b = 0; b < NC; ++b) mE[a][b] = -E[a][b];
+    for (int b = 0; b < NC; ++b) mE[a][b] = -pb[(T::E + a * NC + b) * n + c];
   }
   lu_solve_n<NC>(mE, rhs, DU);
-  double uk_1 = pb[T::UK1 * n + c];
+  const double uk_1 = pb[T::UK1 * n + c];
   const double uk = DU[0] + uk_1;
-  uk_1 = uk;
   int nviol = 0;
 #pragma unroll
-  for (int i = 0; i < NCON; ++i) {
+  for (int i = 0; i < 4 * NC; ++i) {
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) acc = acc + mval(Cn, i, j) * DU[j];
+    for (int j = 0; j < NC; ++j) acc = acc + mconst<NC>(i, j) * DU[j];
     if (acc - pb[(T::GAM + i) * n + c] > 1e-9) nviol++;
+  }
+  double Hs[NP];
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    double Hb[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) Hb[r] = pb[(T::HV + blk * NP + r) * n + c];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const double h = j <= r ? Hb[r - j] : 0.0;
+        acc = acc + (blk == 1 ? -h : h) * DU[j];
+      }
+      if (acc - pb[(T::GAM + 4 * NC + blk * NP + r) * n + c] > 1e-9) nviol++;
+      if (blk == 2) Hs[r] = Hb[r];
+    }
   }
   double e[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) e[i] = pb[(T::ERR + i) * n + c];
-  const int it = w.it[c];
-  s.uk_1[c] = uk_1;
+  s.uk_1[c] = uk;
   if (s.J_fin) {
-    s.J_fin[c] = mpc_cost<NP, NC>(Cn.Hs, e, pb[T::RU * n + c], DU);
+    s.J_fin[c] = mpc_cost<NP, NC>(Hs, e, pb[T::RU * n + c], DU);
     s.nviol[c] = nviol;
   }
   if (io.uk_out) io.uk_out[c] = uk;
-  if (io.nexec) io.nexec[c] = it;
+  if (io.nexec) io.nexec[c] = w.it[c];
   if (io.mode & MODE_FUSED) {
     s.uk[c] = uk;
     if (io.u) io.u[c] = uk;
@@ -430,7 +755,7 @@ __global__ void __launch_bounds__(64) k_mpc_wide_finish(const KCfg cf, const KSt
 }
 
 // GsocT*Gsoc and its sigma_min, as mpc_setup forms them for Csoc = [0 0 0 0 0 rr],
-// Dsoc = 0 (EKFmatsHandler.m:43-45): the cache mpc_setup compares bitwise.
+// Dsoc = 0 (EKFmatsHandler.m:43-45): the cache k_mpc_wide compares bitwise.
 template <int NP, int NC>
 __global__ void k_wide_smin(double rr, double a0, double a1, double a2, double a3, double a4, double *out) {
   const double a[6] = {a0, a1, a2, a3, a4, 1.0};
@@ -501,7 +826,7 @@ int grid(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
 template <int NP, int NC>
 int hild_lds_bytes_w() {
-  return W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS * (int)sizeof(double);
+  return (W<NP, NC>::NCON + W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS) * (int)sizeof(double);
 }
 
 }  // namespace
@@ -535,6 +860,13 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
   if (s.n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   const int lds = hild_lds_bytes_w<WIDE_NP, WIDE_NC>();
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_hild_wide<WIDE_NP, WIDE_NC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_hild_prep<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, s, w);
   hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)), dim3(256), lds,
                      st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
