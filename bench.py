@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--timing-every", type=int, default=8,
+                    help="per-kernel HIP-event timing on every N-th step of the timed region (N | 32)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
 
@@ -131,7 +133,7 @@ def main():
     ptrs = [t.data_ptr() for t in outs] + [nex.data_ptr()]
     if W:
         ctx.step_device(W, *ptrs)
-    ctx.set_timing(True)
+    ctx.set_timing(args.timing_every)
     ctx.get_timing()
     if dist:
         dist.barrier()
@@ -157,8 +159,14 @@ def main():
         cell_steps = total * K
         value = cell_steps / dt if dt > 0 else 0.0
         bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
-        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches=tim[k][1], ms_total=tim[k][0])
+        # HIP-event averages over the sampled launches (--timing-every); every flush step is
+        # sampled, so a kernel's share of a step is its average x its launches per step
+        n_flush = K // 32 + (1 if K % 32 else 0)
+        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches_timed=tim[k][1],
+                              launches=(n_flush if k == "flush" else K))
                       for k in tim if tim[k][1] > 0}
+        for v in per_kernel.values():
+            v["ms_total"] = v["ms_per_launch"] * v["launches"]
         # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
         dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
         ms = per_kernel[dom]["ms_per_launch"]
@@ -211,6 +219,7 @@ def main():
                 },
             },
             "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
+                                launches_timed=v["launches_timed"],
                                 ms_per_step=round(v["ms_total"] / K, 5) if K else None,
                                 gbs_algorithmic=round(bpc[k] * cpg / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
                                 if v["ms_per_launch"] > 0 else None)

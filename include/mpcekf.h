@@ -15,6 +15,8 @@
  *   mpcekf_hildreth     <- [DU,lambda,nexec] = hildreth(E,F,M,gamma,lambda0,maxIter) hildreth.m:1
  *   mpcekf_init_cells   <- initKF.m:30, initMPC.m:29, first OB_step call (runMPC.m:20,52,74)
  *   mpcekf_step         <- the fused loop body runMPC.m:84-111, nsteps times
+ *   mpcekf_step_ex      <- the same, with every runMPC.m store (zkEst, zkBound, x_store,
+ *                          mpcData.cost) per step
  *
  * Conventions
  *  - Plain C types only; no exceptions cross the ABI.  Every function returns an
@@ -144,6 +146,23 @@ int mpcekf_init_cells(mpcekf_ctx *ctx, const double *soc0_pct, const double *tc_
 int mpcekf_step(mpcekf_ctx *ctx, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
                 double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device);
 
+/* Per-step outputs of mpcekf_step_ex (runMPC.m:55-69 stores, filled at runMPC.m:94-111
+ * and iterMPC.m:89-95).  Every pointer may be NULL.  Step-major arrays, host pointers
+ * (device pointers when outputs_on_device != 0):
+ *   [nsteps][ncells]       u, v, soc, phise, nexec, J_unc, J_fin, norm_du, nviol
+ *   [nsteps][ncells][6]    x    (x_store: the EKFmatsHandler xhat, integrator state last)
+ *   [nsteps][ncells][nz+2] zk, zbk (zkEst / zkBound; zbk needs MPCEKF_CF_BOUNDS)
+ * A cell in error has NaN floating outputs and zero nexec / nviol from its failing step on. */
+typedef struct {
+  double *u, *v, *soc, *phise;     /* u_store, voltage_store, SOC_store, phise_store    */
+  int32_t *nexec;                  /* mpcData.cost.nexec                                */
+  double *x;                       /* x_store                                           */
+  double *zk, *zbk;                /* zkEst, zkBound                                    */
+  double *J_unc, *J_fin, *norm_du; /* mpcData.cost.J_uncon / J_final / norm_DU          */
+  int32_t *nviol;                  /* mpcData.cost.viol                                 */
+} mpcekf_traj;
+int mpcekf_step_ex(mpcekf_ctx *ctx, int32_t nsteps, const mpcekf_traj *traj, int32_t outputs_on_device);
+
 /* Optional per-step EKF output of the LAST mpcekf_step call: zk and boundzk
  * ([ncells][nz+2], boundzk only with MPCEKF_CF_BOUNDS). */
 int mpcekf_get_zk(mpcekf_ctx *ctx, double *zk, double *boundzk);
@@ -186,7 +205,9 @@ int mpcekf_hildreth_structured(int device, int64_t n, const double *E, const dou
 
 /* ---- instrumentation (not part of the reference interface) ---- */
 /* When enabled, mpcekf_step brackets every kernel launch with HIP events on the
- * context's stream.  mpcekf_get_timing returns the summed milliseconds and launch
+ * context's stream; enable = N > 1 samples steps N-1, 2N-1, ... and the last only (the
+ * events then perturb the timed stream N times less; with N dividing 32 the sampled steps
+ * include every flush).  mpcekf_get_timing returns the summed milliseconds and launch
  * counts of [plant, flush, cell, hild, bounds] (arrays of MPCEKF_NKERNELS) since the
  * last call and resets them.  "flush" is the all-model time update (k_flush, every
  * 32 steps and at the end of each call); "bounds" is boundzk (k_bounds, when

@@ -53,13 +53,20 @@ class State(C.Structure):
     _fields_ = [("bigX", _dp), ("ekf", _dp), ("scal", _dp), ("lam", _dp), ("warn", _ip), ("status", _ip)]
 
 
+class Traj(C.Structure):
+    """mpcekf_traj: per-step output pointers of mpcekf_step_ex (any may be NULL)."""
+    _fields_ = [("u", C.c_void_p), ("v", C.c_void_p), ("soc", C.c_void_p), ("phise", C.c_void_p),
+                ("nexec", C.c_void_p), ("x", C.c_void_p), ("zk", C.c_void_p), ("zbk", C.c_void_p),
+                ("J_unc", C.c_void_p), ("J_fin", C.c_void_p), ("norm_du", C.c_void_p), ("nviol", C.c_void_p)]
+
+
 class MpcekfError(RuntimeError):
     pass
 
 
 EXPORTS = [
     "mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_ctx_create",
-    "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_get_zk",
+    "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_step_ex", "mpcekf_get_zk",
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
@@ -86,6 +93,7 @@ def load():
     L.mpcekf_ctx_info.argtypes = [vp, C.POINTER(C.c_int64), _ip, _ip, _ip]
     L.mpcekf_init_cells.argtypes = [vp, _dp, _dp]
     L.mpcekf_step.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32]
+    L.mpcekf_step_ex.argtypes = [vp, C.c_int32, C.POINTER(Traj), C.c_int32]
     L.mpcekf_get_zk.argtypes = [vp, _dp, _dp]
     L.mpcekf_plant_step.argtypes = [vp, _dp, _dp]
     L.mpcekf_ekf_step.argtypes = [vp, _dp, _dp, _dp, _dp, _ip, _dp]

@@ -88,6 +88,7 @@ struct mpcekf_ctx {
   size_t tmp_bytes = 0;
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
+  int timing_every = 1;  // sample every timing_every-th step (1 = every step)
   std::vector<hipEvent_t> ev;
   double t_ms[MPCEKF_NKERNELS] = {};
   int64_t t_n[MPCEKF_NKERNELS] = {};
@@ -527,29 +528,38 @@ static int lerr(int rc, const char *what) {
 
 // runMPC.m:84-111, nsteps times: OB_step -> (all-model advance + EKF time
 // update) -> iterEKF measurement update -> EKFmatsHandler -> iterMPC.
-int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
-                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device) {
+int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const mpcekf_traj *tr, int32_t outputs_on_device) {
   int rc = need_init(X);
   if (rc) return rc;
   if (nsteps < 0) return fail(MPCEKF_E_ARG, "nsteps < 0");
-  const size_t n = (size_t)X->n, per = n * (size_t)nsteps;
-  double *outs[4] = {traj_u, traj_v, traj_soc, traj_phise};
-  double *dev[4] = {nullptr, nullptr, nullptr, nullptr};
-  int *dnex = nullptr;
+  mpcekf_traj none{};
+  if (!tr) tr = &none;
+  const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
+  if (tr->zbk && !bounds) return fail(MPCEKF_E_ARG, "step_ex: a boundzk trajectory needs MPCEKF_CF_BOUNDS");
+  const size_t n = (size_t)X->n, per = n * (size_t)nsteps, nzz = (size_t)X->nz + 2;
+  // the output fields, their element size and elements per cell-step
+  struct F {
+    void *host;
+    size_t esz, width;
+    char *dev;
+  } f[] = {{tr->u, 8, 1, nullptr},       {tr->v, 8, 1, nullptr},      {tr->soc, 8, 1, nullptr},
+           {tr->phise, 8, 1, nullptr},   {tr->nexec, 4, 1, nullptr},  {tr->x, 8, 6, nullptr},
+           {tr->zk, 8, nzz, nullptr},    {tr->zbk, 8, nzz, nullptr},  {tr->J_unc, 8, 1, nullptr},
+           {tr->J_fin, 8, 1, nullptr},   {tr->norm_du, 8, 1, nullptr}, {tr->nviol, 4, 1, nullptr}};
+  constexpr int NF = sizeof(f) / sizeof(f[0]);
   if (outputs_on_device) {
-    for (int i = 0; i < 4; ++i) dev[i] = outs[i];
-    dnex = traj_nexec;
+    for (F &e : f) e.dev = (char *)e.host;
   } else {
     size_t need = 0;
-    for (int i = 0; i < 4; ++i) need += outs[i] ? per * 8 : 0;
-    need += traj_nexec ? per * 4 + 16 : 0;
-    if ((rc = X->tmp(need))) return rc;
+    for (F &e : f) need += e.host ? ((per * e.width * e.esz + 255) & ~(size_t)255) : 0;
+    if ((rc = X->tmp(need + 256))) return rc;
     char *p = (char *)X->d_tmp;
-    for (int i = 0; i < 4; ++i)
-      if (outs[i]) { dev[i] = (double *)p; p += per * 8; }
-    if (traj_nexec) dnex = (int *)p;
+    for (F &e : f)
+      if (e.host) { e.dev = p; p += (per * e.width * e.esz + 255) & ~(size_t)255; }
   }
-  const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
+  auto row = [&](int i, int k) -> char * {  // step k's [ncells][width] block of field i
+    return f[i].dev ? f[i].dev + (size_t)k * n * f[i].width * f[i].esz : nullptr;
+  };
   constexpr int NEV = 6;  // events per step: plant | cell | bounds | hild | flush |
   if (X->timing && X->ev.size() < (size_t)nsteps * NEV) {
     size_t old = X->ev.size();
@@ -562,9 +572,11 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
   // points, get/set_state) every model is current, exactly as after eager updates.
   std::vector<char> flushed((size_t)nsteps, 0);
   for (int k = 0; k < nsteps; ++k) {
-    const size_t o = (size_t)k * n;
     const int t = k + 1;
-    hipEvent_t *E = X->timing ? &X->ev[(size_t)k * NEV] : nullptr;
+    // sampled steps: every timing_every-th (k = every-1, 2 every-1, ...: with every dividing
+    // the flush period these include the flush steps) and the last
+    const bool sample = X->timing && ((k + 1) % X->timing_every == 0 || k == nsteps - 1);
+    hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
     if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, X->stream), "plant"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[1], X->stream));
@@ -572,14 +584,20 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     io.mode = MODE_FUSED;
     io.lazy_t = t;
     io.stamps = X->d_stamps;
-    io.u = dev[0] ? dev[0] + o : nullptr;
-    io.v = dev[1] ? dev[1] + o : nullptr;
-    io.soc = dev[2] ? dev[2] + o : nullptr;
-    io.phise = dev[3] ? dev[3] + o : nullptr;
-    io.nexec = dnex ? dnex + o : nullptr;
-    io.zk = X->d_zk;
-    io.zbk = bounds ? X->d_zbk : nullptr;
+    io.u = (double *)row(0, k);
+    io.v = (double *)row(1, k);
+    io.soc = (double *)row(2, k);
+    io.phise = (double *)row(3, k);
+    io.nexec = (int *)row(4, k);
+    io.x_out = (double *)row(5, k);
+    io.zk = f[6].dev ? (double *)row(6, k) : X->d_zk;
+    double *zbk_k = f[7].dev ? (double *)row(7, k) : X->d_zbk;
+    io.zbk = bounds ? zbk_k : nullptr;
     io.bnd = bounds ? X->d_bnd : nullptr;
+    io.junc_out = (double *)row(8, k);
+    io.jfin_out = (double *)row(9, k);
+    io.normdu_out = (double *)row(10, k);
+    io.nviol_out = (int *)row(11, k);
     KIO iow{};  // wide horizons: iterMPC in mpcekf_wide.hip from the linearisation record
     if (X->wide) {
       io.lin_out = X->d_lin;
@@ -590,6 +608,10 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
       iow.soc_k1_in = X->d_zsoc;
       iow.u = io.u;
       iow.nexec = io.nexec;
+      iow.junc_out = io.junc_out;
+      iow.jfin_out = io.jfin_out;
+      iow.normdu_out = io.normdu_out;
+      iow.nviol_out = io.nviol_out;
       if ((rc = lerr(launch_mpc_wide(X->k, X->s, iow, X->w, X->stream), "mpc_wide"))) return rc;
     } else if (X->split_cell) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
       io.xm_out = X->d_xm;
@@ -609,7 +631,7 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
       return rc;
     }
     if (E) HIPCHK(hipEventRecord(E[2], X->stream));
-    if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, X->d_zbk, X->stream), "bounds"))) return rc;
+    if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));
     if (X->wide) {
       if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
@@ -623,16 +645,21 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
     }
     if (E) HIPCHK(hipEventRecord(E[5], X->stream));
   }
-  if (!outputs_on_device) {
-    for (int i = 0; i < 4; ++i)
-      if (outs[i]) HIPCHK(hipMemcpyAsync(outs[i], dev[i], per * 8, hipMemcpyDeviceToHost, X->stream));
-    if (traj_nexec) HIPCHK(hipMemcpyAsync(traj_nexec, dnex, per * 4, hipMemcpyDeviceToHost, X->stream));
-  }
+  if (!outputs_on_device)
+    for (int i = 0; i < NF; ++i)
+      if (f[i].host)
+        HIPCHK(hipMemcpyAsync(f[i].host, f[i].dev, per * f[i].width * f[i].esz, hipMemcpyDeviceToHost, X->stream));
+  // mpcekf_get_zk returns the last step's zk / boundzk whichever buffers the steps wrote
+  if (nsteps > 0 && f[6].dev)
+    HIPCHK(hipMemcpyAsync(X->d_zk, row(6, nsteps - 1), n * nzz * 8, hipMemcpyDeviceToDevice, X->stream));
+  if (nsteps > 0 && f[7].dev)
+    HIPCHK(hipMemcpyAsync(X->d_zbk, row(7, nsteps - 1), n * nzz * 8, hipMemcpyDeviceToDevice, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   if (X->timing) {
     static const int slot[NEV - 1] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_BOUNDS, MPCEKF_K_HILD, MPCEKF_K_FLUSH};
     for (int k = 0; k < nsteps; ++k)
       for (int j = 0; j < NEV - 1; ++j) {
+        if ((k + 1) % X->timing_every != 0 && k != nsteps - 1) continue;
         if ((j == 4 && !flushed[k]) || (j == 2 && !bounds)) continue;
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + j], X->ev[(size_t)k * NEV + j + 1]));
@@ -643,9 +670,21 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, d
   return MPCEKF_OK;
 }
 
+int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
+                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device) {
+  mpcekf_traj tr{};
+  tr.u = traj_u;
+  tr.v = traj_v;
+  tr.soc = traj_soc;
+  tr.phise = traj_phise;
+  tr.nexec = traj_nexec;
+  return mpcekf_step_ex(X, nsteps, &tr, outputs_on_device);
+}
+
 int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {
   if (!X) return fail(MPCEKF_E_ARG, "null ctx");
   X->timing = enable != 0;
+  X->timing_every = enable > 1 ? enable : 1;
   return MPCEKF_OK;
 }
 

@@ -1389,6 +1389,12 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int q = 0; q < nz + 2; ++q) io.zbk[c * (nz + 2) + q] = NaN;
     if (io.bnd) io.bnd[BD_M * s.n + c] = -1.0;  // no boundzk record: k_bounds leaves zbk NaN
     if (io.uk_out) io.uk_out[c] = NaN;
+    if (io.x_out)
+      for (int q = 0; q < 6; ++q) io.x_out[c * 6 + q] = NaN;
+    if (io.junc_out) io.junc_out[c] = NaN;
+    if (io.jfin_out) io.jfin_out[c] = NaN;
+    if (io.normdu_out) io.normdu_out[c] = NaN;
+    if (io.nviol_out) io.nviol_out[c] = 0;
     if (io.lin_out)
       for (int q = 0; q < 35; ++q) io.lin_out[c * 35 + q] = NaN;
     if (io.xm_out)
@@ -1590,6 +1596,9 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
     mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
+    if (io.x_out)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) io.x_out[c * 6 + q] = L.xhat[q];  // x_store (runMPC.m:108)
   }
   STAMP(10);
   if (PARTS & P_LIN) {  // iterMPC runs in the wide-horizon kernels (mpcekf_wide.hip) from lin_out / zsoc_out
@@ -1630,6 +1639,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       if (io.phise) io.phise[c] = phise;
     }
     if (s.J_unc) s.J_unc[c] = o.J_unc;
+    if (io.junc_out) io.junc_out[c] = o.J_unc;
     STAMP(11);
     s.hflag[c] = need ? 1 : 0;
     if (need) {  // hildreth.m runs in k_hild
@@ -1657,6 +1667,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       mpc_finish(Pm.Cn, Pm.e, Pm.Ru, Pm.DU, uk_1, o);
       s.uk_1[c] = uk_1;
       if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
+      cost_out(io, c, o.J_fin, o.nviol, norm_du<NC>(Pm.DU));
       if (io.uk_out) io.uk_out[c] = o.uk;
       if (io.nexec) io.nexec[c] = 0;
       if (fused) {
@@ -1900,6 +1911,7 @@ __device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int6
   mpc_finish(P.Cn, P.e, P.Ru, P.DU, uk_1, o);
   s.uk_1[c] = uk_1;
   if (s.J_fin) { s.J_fin[c] = o.J_fin; s.nviol[c] = o.nviol; }
+  cost_out(io, c, o.J_fin, o.nviol, norm_du<NC>(P.DU));
   if (io.uk_out) io.uk_out[c] = o.uk;
   if (io.nexec) io.nexec[c] = o.nexec;
   if (io.mode & MODE_FUSED) {

@@ -87,6 +87,10 @@ struct KIO {
   double *bnd;            // [NBND][n] boundzk hand-off k_cell -> k_bounds (with zbk)
   long long *stamps;      // [MPCEKF_NSTAMPS][n] s_memtime per k_cell section (-DMPCEKF_STAMPS builds only)
   double *zsoc_out;       // [n] zk(end) for the wide-horizon MPC kernels (P_LIN, fused)
+  // per-step diagnostics of the fused step (runMPC.m:106-111, mpcData.cost iterMPC.m:89-95)
+  double *x_out;          // [n][6] x_store: the EKFmatsHandler xhat
+  double *junc_out, *jfin_out, *normdu_out;  // [n] J_uncon, J_final, norm_DU
+  int *nviol_out;         // [n] viol
 };
 constexpr int NSTAMPS = 12;
 // k_cell -> k_bounds record: g[4], m[4], Z(te1, th0, tee, th3), x0, S0.  k_bounds reads

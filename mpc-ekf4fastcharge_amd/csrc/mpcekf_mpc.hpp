@@ -334,6 +334,22 @@ __device__ __forceinline__ double mpc_cost(const double (&Hs)[NP], const double 
   return J + Jq;
 }
 
+// mpcData.cost.norm_DU = norm(DU,2) (iterMPC.m:92): square root of the sequential sum
+template <int NC>
+__device__ __forceinline__ double norm_du(const double (&DU)[NC]) {
+  double s2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) s2 = s2 + DU[j] * DU[j];
+  return sqrt(s2);
+}
+
+// Per-step mpcData.cost outputs (runMPC.m:63-69 / iterMPC.m:89-95) of a finished iterMPC
+__device__ __forceinline__ void cost_out(const KIO &io, int64_t c, double J_fin, int nviol, double ndu) {
+  if (io.jfin_out) io.jfin_out[c] = J_fin;
+  if (io.nviol_out) io.nviol_out[c] = nviol;
+  if (io.normdu_out) io.normdu_out[c] = ndu;
+}
+
 template <int NP, int NC>
 struct MpcSetupT {
   ConsT<NP, NC> Cn;

@@ -204,6 +204,7 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
   lu_solve_n<NC>(mE, F, DU);  // DU = -E\F (iterMPC.m:48)
   const double J_unc = mpc_cost<NP, NC>(Hs, e, Ru, DU);
   if (s.J_unc) s.J_unc[c] = J_unc;
+  if (io.junc_out) io.junc_out[c] = J_unc;
   // constraintsMPC.m rows: gamma to the record, M*DU - gamma tested as each row is formed
   int nv = 0, nviol = 0;
 #pragma unroll
@@ -271,6 +272,7 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
     const double uk = DU[0] + uk_1;
     s.uk_1[c] = uk;
     if (s.J_fin) { s.J_fin[c] = J_unc; s.nviol[c] = nviol; }
+    cost_out(io, c, J_unc, nviol, norm_du<NC>(DU));
     if (io.uk_out) io.uk_out[c] = uk;
     if (io.nexec) io.nexec[c] = 0;
     if (fused) {
@@ -742,10 +744,12 @@ __global__ void __launch_bounds__(64) k_mpc_wide_finish(const KCfg cf, const KSt
 #pragma unroll
   for (int i = 0; i < NP; ++i) e[i] = pb[(T::ERR + i) * n + c];
   s.uk_1[c] = uk;
+  const double J_fin = mpc_cost<NP, NC>(Hs, e, pb[T::RU * n + c], DU);
   if (s.J_fin) {
-    s.J_fin[c] = mpc_cost<NP, NC>(Hs, e, pb[T::RU * n + c], DU);
+    s.J_fin[c] = J_fin;
     s.nviol[c] = nviol;
   }
+  cost_out(io, c, J_fin, nviol, norm_du<NC>(DU));
   if (io.uk_out) io.uk_out[c] = uk;
   if (io.nexec) io.nexec[c] = w.it[c];
   if (io.mode & MODE_FUSED) {

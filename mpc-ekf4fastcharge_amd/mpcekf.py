@@ -128,21 +128,28 @@ class Context:
         check(self.L.mpcekf_init_cells(self.h, dptr(s), dptr(t)))
 
     # -- fused loop (runMPC.m:83-112) ------------------------------------
+    # runMPC.m stores per step: name -> (dtype, trailing shape); see mpcekf_traj
+    TRAJ_FIELDS = dict(u=(np.float64, ()), v=(np.float64, ()), soc=(np.float64, ()), phise=(np.float64, ()),
+                       nexec=(np.int32, ()), x=(np.float64, (6,)), zk=(np.float64, None),
+                       zbk=(np.float64, None), J_unc=(np.float64, ()), J_fin=(np.float64, ()),
+                       norm_du=(np.float64, ()), nviol=(np.int32, ()))
+
     def step(self, nsteps, outputs=("u", "v", "soc", "phise", "nexec")):
+        """nsteps fused closed-loop steps (runMPC.m:83-112).  ``outputs`` names the per-step
+        stores to return as [nsteps, ncells(, k)] arrays: u, v, soc, phise, nexec, and the
+        diagnostics x (x_store), zk / zbk (zkEst / zkBound), J_unc, J_fin, norm_du, nviol
+        (mpcData.cost)."""
         n = self.n
         out = {}
-        ptr = []
-        for k in ("u", "v", "soc", "phise"):
-            if k in outputs:
-                out[k] = np.empty((nsteps, n))
-                ptr.append(out[k].ctypes.data_as(C.c_void_p))
-            else:
-                ptr.append(None)
-        nex = None
-        if "nexec" in outputs:
-            out["nexec"] = nex = np.empty((nsteps, n), dtype=np.int32)
-        check(self.L.mpcekf_step(self.h, int(nsteps), *ptr,
-                                 nex.ctypes.data_as(C.c_void_p) if nex is not None else None, 0))
+        tr = _lib.Traj()
+        for k in outputs:
+            if k not in self.TRAJ_FIELDS:
+                raise KeyError(f"unknown output {k}")
+            dt, tail = self.TRAJ_FIELDS[k]
+            tail = (self.nz + 2,) if tail is None else tail
+            out[k] = np.empty((nsteps, n) + tail, dtype=dt)
+            setattr(tr, k, out[k].ctypes.data_as(C.c_void_p).value)
+        check(self.L.mpcekf_step_ex(self.h, int(nsteps), C.byref(tr), 0))
         return out
 
     def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
@@ -151,7 +158,8 @@ class Context:
         check(self.L.mpcekf_step(self.h, int(nsteps), *p, 1))
 
     def set_timing(self, enable=True):
-        check(self.L.mpcekf_set_timing(self.h, int(bool(enable))))
+        """enable: True/1 = every step; N > 1 = sample every N-th step (less perturbation)."""
+        check(self.L.mpcekf_set_timing(self.h, int(enable)))
 
     def get_timing(self):
         """{kernel: (ms_sum, launches)} since the last call (HIP events on the ctx stream)."""

@@ -994,7 +994,7 @@ int orc_constraints(const orc_rom *r, const orc_cfg *cf, const orc_lin *L, const
 }
 
 typedef struct {
-  double uk, J_unc, J_fin;
+  double uk, J_unc, J_fin, norm_du; /* mpcData.cost (iterMPC.m:89-95) */
   int nexec, nviol;
 } orc_mpc_out;
 
@@ -1087,6 +1087,9 @@ void orc_mpc_step(const orc_rom *r, const orc_cfg *cf, orc_cell *s, const orc_li
     Jq = Jq + acc * DU[c];
   }
   o->J_fin = J + Jq;
+  double s2 = 0.0; /* norm(DU,2) (iterMPC.m:92) as the square root of the sequential sum */
+  for (int j = 0; j < Nc; ++j) s2 = s2 + DU[j] * DU[j];
+  o->norm_du = sqrt(s2);
 }
 
 /* iterMPC.m:17-95 on given EKFmatsHandler records (the 35-double layout of orc_lin,
@@ -1154,10 +1157,21 @@ static void init_cell(const orc_ctx *X, orc_cell *s, double soc0, double tc) {
 }
 
 /* One closed-loop step of runMPC.m:84-111 for one cell. */
+/* Per-step diagnostics of runMPC.m:106-111 and mpcData.cost (iterMPC.m:89-95). */
+typedef struct {
+  double *x;                       /* [nsteps][ncells][6]    x_store (EKFmatsHandler xhat) */
+  double *zk, *zbk;                /* [nsteps][ncells][nz+2] zkEst, zkBound                */
+  double *J_unc, *J_fin, *norm_du; /* [nsteps][ncells]       J_uncon, J_final, norm_DU     */
+  int32_t *nviol;                  /* [nsteps][ncells]       viol                          */
+} orc_traj;
+
 static void cell_step(const orc_ctx *X, orc_cell *s, double *u, double *v, double *soc, double *phise, int *nexec,
-                      double *zk_out, double *zbk_out) {
+                      double *zk_out, double *zbk_out, orc_mpc_out *mo, double *x_out) {
   const orc_rom *r = X->r;
   int nz = r->nz;
+  mo->J_unc = mo->J_fin = mo->norm_du = mo->uk = NAN;
+  mo->nviol = 0;
+  if (x_out) for (int q = 0; q <= NX; ++q) x_out[q] = NAN;
   if (s->status & ST_ERROR) {
     *u = *v = *soc = *phise = NAN;
     *nexec = 0;
@@ -1184,6 +1198,8 @@ static void cell_step(const orc_ctx *X, orc_cell *s, double *u, double *v, doubl
   double ph = acc + ukin * L.Dphi + L.bphi;
   orc_mpc_out o;
   orc_mpc_step(r, X->c, s, &L, zk[nz + 1], &o);
+  *mo = o;
+  if (x_out) for (int q = 0; q <= NX; ++q) x_out[q] = L.xhat[q];
   s->uk = o.uk;
   *u = o.uk;
   *v = V;
@@ -1196,9 +1212,9 @@ static void cell_step(const orc_ctx *X, orc_cell *s, double *u, double *v, doubl
 
 /* Batched closed loop: outputs are [nsteps][ncells]; zk/zbk (optional) are
  * the LAST step's [ncells][nz+2].  Returns 0 on success. */
-int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, const double *tc, int nsteps,
-            double *u, double *v, double *soc, double *phise, int32_t *nexec, int32_t *status, double *zk,
-            double *zbk, int nthreads) {
+int orc_run_traj(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, const double *tc, int nsteps,
+                 double *u, double *v, double *soc, double *phise, int32_t *nexec, int32_t *status, double *zk,
+                 double *zbk, const orc_traj *tr, int nthreads) {
   orc_ctx X;
   int rc = ctx_init(&X, r, c);
   if (rc) return rc;
@@ -1217,9 +1233,18 @@ int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, 
       size_t o = (size_t)k * ncells + i;
       int ne;
       int last = k == nsteps - 1;
-      cell_step(&X, &s, &u[o], &v[o], &soc[o], &phise[o], &ne,
-                (zk && last) ? zk + (size_t)i * (r->nz + 2) : NULL,
-                (zbk && last) ? zbk + (size_t)i * (r->nz + 2) : NULL);
+      const size_t nzz = (size_t)r->nz + 2;
+      double *zko = (tr && tr->zk) ? tr->zk + o * nzz : (zk && last) ? zk + (size_t)i * nzz : NULL;
+      double *zbo = (tr && tr->zbk) ? tr->zbk + o * nzz : (zbk && last) ? zbk + (size_t)i * nzz : NULL;
+      orc_mpc_out mo;
+      cell_step(&X, &s, &u[o], &v[o], &soc[o], &phise[o], &ne, zko, zbo, &mo,
+                (tr && tr->x) ? tr->x + o * (NX + 1) : NULL);
+      if (tr && tr->zk && zk && last) memcpy(zk + (size_t)i * nzz, zko, nzz * sizeof(double));
+      if (tr && tr->zbk && zbk && last) memcpy(zbk + (size_t)i * nzz, zbo, nzz * sizeof(double));
+      if (tr && tr->J_unc) tr->J_unc[o] = mo.J_unc;
+      if (tr && tr->J_fin) tr->J_fin[o] = mo.J_fin;
+      if (tr && tr->norm_du) tr->norm_du[o] = mo.norm_du;
+      if (tr && tr->nviol) tr->nviol[o] = mo.nviol;
       nexec[o] = ne;
     }
     status[i] = s.status;
@@ -1228,6 +1253,14 @@ int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, 
     free(s.S);
   }
   return 0;
+}
+
+/* Batched closed loop: outputs are [nsteps][ncells]; zk/zbk (optional) are the LAST
+ * step's [ncells][nz+2]. */
+int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, const double *tc, int nsteps,
+            double *u, double *v, double *soc, double *phise, int32_t *nexec, int32_t *status, double *zk,
+            double *zbk, int nthreads) {
+  return orc_run_traj(r, c, ncells, soc0, tc, nsteps, u, v, soc, phise, nexec, status, zk, zbk, NULL, nthreads);
 }
 
 int orc_version(void) { return 1; }

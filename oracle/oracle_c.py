@@ -77,6 +77,9 @@ def lib():
         L.orc_predmat.argtypes = [_dp, _dp, C.c_double, C.c_int, C.c_int, _dp, _dp]
         L.orc_hildreth.restype = C.c_int
         L.orc_hildreth.argtypes = [C.c_int, C.c_int, _dp, _dp, _dp, _dp, _dp, C.c_int, C.c_double, _dp]
+        L.orc_run_traj.restype = C.c_int
+        L.orc_run_traj.argtypes = [C.POINTER(_Rom), C.POINTER(_Cfg), C.c_int, _dp, _dp, C.c_int,
+                                   _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, C.POINTER(_Traj), C.c_int]
         L.orc_mpc_lin.restype = C.c_int
         L.orc_mpc_lin.argtypes = [C.POINTER(_Rom), C.POINTER(_Cfg), C.c_int, _dp, _dp, _dp, _dp, _dp, _ip]
         L.orc_sigma_min.restype = C.c_double
@@ -143,8 +146,16 @@ def make_cfg(**kw):
     return c
 
 
-def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, **cfg):
-    """Batched closed loop on the CPU. Returns dict of [nsteps, ncells] arrays."""
+class _Traj(C.Structure):
+    _fields_ = [("x", _dp), ("zk", _dp), ("zbk", _dp), ("J_unc", _dp), ("J_fin", _dp), ("norm_du", _dp),
+                ("nviol", _ip)]
+
+
+def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, **cfg):
+    """Batched closed loop on the CPU. Returns dict of [nsteps, ncells] arrays.
+
+    traj=True adds the per-step diagnostics of runMPC.m:106-111 / mpcData.cost:
+    x [nsteps, n, 6], zk_traj / zbk_traj [nsteps, n, nz+2], J_unc, J_fin, norm_du, nviol."""
     soc0 = np.ascontiguousarray(soc0, dtype=np.float64)
     tc = np.ascontiguousarray(tc, dtype=np.float64)
     n = soc0.shape[0]
@@ -155,10 +166,21 @@ def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, **cfg):
     out["status"] = np.zeros(n, dtype=np.int32)
     zk = np.zeros((n, rom.nz + 2)) if want_zk else None
     zbk = np.zeros((n, rom.nz + 2)) if want_zk else None
-    rc = lib().orc_run(C.byref(pr.s), C.byref(c), n, _p(soc0), _p(tc), nsteps, _p(out["u"]),
-                       _p(out["v"]), _p(out["soc"]), _p(out["phise"]),
-                       out["nexec"].ctypes.data_as(_ip), out["status"].ctypes.data_as(_ip),
-                       _p(zk) if want_zk else None, _p(zbk) if want_zk else None, nthreads)
+    tr = None
+    if traj:
+        out["x"] = np.zeros((nsteps, n, 6))
+        out["zk_traj"] = np.zeros((nsteps, n, rom.nz + 2))
+        out["zbk_traj"] = np.zeros((nsteps, n, rom.nz + 2))
+        for k in ("J_unc", "J_fin", "norm_du"):
+            out[k] = np.zeros((nsteps, n))
+        out["nviol"] = np.zeros((nsteps, n), dtype=np.int32)
+        tr = _Traj(_p(out["x"]), _p(out["zk_traj"]), _p(out["zbk_traj"]), _p(out["J_unc"]), _p(out["J_fin"]),
+                   _p(out["norm_du"]), out["nviol"].ctypes.data_as(_ip))
+    rc = lib().orc_run_traj(C.byref(pr.s), C.byref(c), n, _p(soc0), _p(tc), nsteps, _p(out["u"]),
+                            _p(out["v"]), _p(out["soc"]), _p(out["phise"]),
+                            out["nexec"].ctypes.data_as(_ip), out["status"].ctypes.data_as(_ip),
+                            _p(zk) if want_zk else None, _p(zbk) if want_zk else None,
+                            C.byref(tr) if tr is not None else None, nthreads)
     if rc:
         raise RuntimeError(f"orc_run failed: {rc}")
     if want_zk:

@@ -271,3 +271,31 @@ def test_structured_hildreth_edge_paths_match_oracle(oc, M):
         assert ne[i] == ne_r, (i, g[i])
         np.testing.assert_array_equal(lam[i], lam_r, err_msg=f"cell {i} group {g[i]}")
         np.testing.assert_array_equal(DU[i], du_r, err_msg=f"cell {i} group {g[i]}")
+
+
+@pytest.mark.parametrize("Np,Nc", [(5, 2), (20, 10)])
+def test_step_diagnostics_match_oracle(rom, oc, M, Np, Nc):
+    """Every runMPC.m store per step (mpcekf_step_ex): x_store, zkEst, zkBound and
+    mpcData.cost (J_uncon, J_final, norm_DU, viol) against the oracle; the lock-out cell
+    gives NaN / 0 from its failing step on.  Tolerance as the short closed loops (1e-9:
+    asinh differs by ulps upstream); the integer viol count must match exactly."""
+    n, steps = 24, 40
+    soc0, tc = batch_inputs(n, seed=13)
+    soc0[3] = 130.0  # lock-out
+    ref = oc.run(rom, soc0, tc, steps, nthreads=4, traj=True, Np=Np, Nc=Nc)
+    cfg = M.make_config(bounds=True, Np=Np, Nc=Nc)
+    names = ("u", "v", "soc", "phise", "nexec", "x", "zk", "zbk", "J_unc", "J_fin", "norm_du", "nviol")
+    with M.Context(rom, n, cfg) as ctx:
+        ctx.init_cells(soc0, tc)
+        out = ctx.step(steps, outputs=names)
+        zk_last, zb_last = ctx.get_zk()
+    pairs = dict(x="x", zk="zk_traj", zbk="zbk_traj", J_unc="J_unc", J_fin="J_fin", norm_du="norm_du")
+    for k, rk in pairs.items():
+        assert np.array_equal(np.isnan(out[k]), np.isnan(ref[rk])), k
+        r = _rel(out[k], ref[rk])
+        assert r.max() <= RTOL_TIGHT, (k, r.max())
+    np.testing.assert_array_equal(out["nviol"], ref["nviol"])
+    np.testing.assert_array_equal(out["nexec"], ref["nexec"])
+    assert np.isnan(out["zk"][-1, 3]).all() and (out["nviol"][-1, 3] == 0)
+    np.testing.assert_array_equal(zk_last, out["zk"][-1])
+    np.testing.assert_array_equal(zb_last, out["zbk"][-1])
