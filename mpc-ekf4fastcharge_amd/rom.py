@@ -17,8 +17,9 @@ iterEKF.m:282-283,362-363,392-407, EKFmatsHandler.m:53-92).  This module
 * resolves the output-row roles (iterEKF.m:610-735) and packs everything into
   the flat arrays the C-ABI ``mpcekf_rom`` struct expects (include/mpcekf.h).
 
-A real ROM exported from MATLAB can be loaded with :func:`ROM.load_npz` as long as
-its cellData functions are tabulated in the same format.
+A real ROM is exported on a MATLAB machine by ``matlab/mpcekf_export_rom.m`` (it
+tabulates the cellData handles) and loaded with :func:`ROM.load_json` (SURVEY.md
+§8(f) rank 1); :func:`ROM.load_npz` reads this module's own ``save_npz`` files.
 """
 from __future__ import annotations
 
@@ -331,6 +332,98 @@ class ROM:
                    xloc=np.array(z["xloc"], float), F=float(z["F"]), R=float(z["R"]),
                    Q=float(z["Q"]), Rc=float(z["Rc"]), Tref=float(z["Tref"]),
                    neg=el("neg"), pos=el("pos"))
+
+
+    # ---- JSON exchange format (matlab/mpcekf_export_rom.m) ------------------
+    JSON_FORMAT = "mpcekf-rom-v1"
+
+    def to_json_dict(self):
+        """The dict ``matlab/mpcekf_export_rom.m`` writes: every array as
+        ``{"shape", "order": "F", "data"}`` (MATLAB column-major), scalars bare."""
+        def arr(x):
+            x = np.asarray(x, dtype=float)
+            shape = list(x.shape) if x.ndim >= 2 else [1, int(x.size)]
+            return {"shape": shape, "order": "F", "data": [_json_num(v) for v in x.ravel(order="F")]}
+
+        def el(e):
+            d = {k: float(getattr(e, k)) for k in _EL_SCALARS}
+            d.update({k: arr(getattr(e, k)) for k in ("U", "dUdT", "dU")})
+            return d
+
+        return {"format": self.JSON_FORMAT, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
+                "Ts": float(self.Ts), "A": arr(self.A), "C": arr(self.C), "D": arr(self.D),
+                "names": list(self.names), "xloc": arr(self.xloc), "F": float(self.F), "R": float(self.R),
+                "Q": float(self.Q), "Rc": float(self.Rc), "Tref": float(self.Tref),
+                "neg": el(self.neg), "pos": el(self.pos)}
+
+    def save_json(self, path):
+        import json
+        with open(path, "w") as f:
+            json.dump(self.to_json_dict(), f)
+
+    @staticmethod
+    def from_json_dict(d):
+        """Inverse of :meth:`to_json_dict`; accepts what MATLAB's ``jsonencode`` makes of
+        the exporter's struct (1-element arrays as bare numbers, NaN as null, a lone
+        name as a string).  Raises ValueError on a wrong format tag or shape."""
+        if d.get("format") != ROM.JSON_FORMAT:
+            raise ValueError(f"ROM json: format {d.get('format')!r}, expected {ROM.JSON_FORMAT!r}")
+
+        def arr(a, ndim):
+            if a.get("order", "F") != "F":
+                raise ValueError("ROM json: arrays must be column-major ('F')")
+            data = np.array([np.nan if v is None else v for v in np.atleast_1d(a["data"])], dtype=float)
+            shape = [int(v) for v in np.atleast_1d(a["shape"])]
+            if int(np.prod(shape)) != data.size:
+                raise ValueError(f"ROM json: shape {shape} does not hold {data.size} values")
+            x = data.reshape(shape, order="F")
+            if ndim == 1:
+                return x.ravel(order="F")
+            # MATLAB drops trailing singleton dimensions (e.g. nz = 1); restore them
+            if x.ndim < ndim:
+                x = x.reshape(list(x.shape) + [1] * (ndim - x.ndim), order="F")
+            if x.ndim != ndim:
+                raise ValueError(f"ROM json: expected {ndim}-D array, got shape {shape}")
+            return x
+
+        def el(e):
+            kw = {k: float(e[k]) for k in _EL_SCALARS}
+            kw.update({k: arr(e[k], 1) for k in ("U", "dUdT", "dU")})
+            return Electrode(**kw)
+
+        names = d["names"]
+        names = [names] if isinstance(names, str) else [str(s) for s in names]
+        rom = ROM(T_degC=arr(d["T_degC"], 1), SOC_pct=arr(d["SOC_pct"], 1), Ts=float(d["Ts"]),
+                  A=arr(d["A"], 3), C=arr(d["C"], 4), D=arr(d["D"], 3), names=names,
+                  xloc=arr(d["xloc"], 1), F=float(d["F"]), R=float(d["R"]), Q=float(d["Q"]),
+                  Rc=float(d["Rc"]), Tref=float(d["Tref"]), neg=el(d["neg"]), pos=el(d["pos"]),
+                  meta={k: d[k] for k in ("source", "tab_error") if k in d})
+        nT, nZ = rom.T_degC.size, rom.SOC_pct.size
+        if rom.A.shape[:2] != (nT, nZ) or rom.C.shape[:2] != (nT, nZ) or rom.D.shape[:2] != (nT, nZ):
+            raise ValueError("ROM json: A/C/D set-point grid does not match xraData.T x xraData.SOC")
+        if rom.C.shape[2] != len(names) or rom.D.shape[2] != len(names) or rom.xloc.size != len(names):
+            raise ValueError("ROM json: C/D/xloc rows do not match tfData.names")
+        return rom
+
+    @staticmethod
+    def load_json(path):
+        import json
+        with open(path) as f:
+            return ROM.from_json_dict(json.load(f))
+
+    @staticmethod
+    def load(path):
+        """Load a ROM exported by matlab/mpcekf_export_rom.m (.json) or saved by
+        :meth:`save_npz` (.npz)."""
+        return ROM.load_json(path) if str(path).endswith(".json") else ROM.load_npz(path)
+
+
+_EL_SCALARS = ("theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL")
+
+
+def _json_num(v):
+    v = float(v)
+    return None if v != v else v   # MATLAB jsonencode writes NaN as null
 
 
 # --------------------------------------------------------------------------

@@ -61,3 +61,93 @@ def test_tabulated_functions(rom):
     assert f.Uocp(-1.0) == f.Uocp(0.0) and f.Uocp(2.0) == f.Uocp(1.0)
     assert f.Uocp(0.3) == f.Uocp(0.3, rom.Tref)          # 1-arg call = Tref (EKFmatsHandler.m:96)
     assert f.soc(0.0) == rom.neg.theta0 and f.soc(1.0) == rom.neg.theta100
+
+
+def _matlab_jsonencode_quirks(d):
+    """What MATLAB's jsonencode does to the exporter's struct that Python's json does
+    not: 1-element arrays become bare numbers, trailing singleton dims vanish from
+    size(), NaN becomes null."""
+    d = copy.deepcopy(d)
+    d["neg"]["U"]["data"][0] = None               # NaN entry -> null
+    one = {"shape": [1, 1], "order": "F", "data": 2.5}
+    d["neg"]["Rf_tab_probe"] = one                # unknown keys are ignored
+    return d
+
+
+def test_rom_json_roundtrip_bit_exact(rom, tmp_path, P):
+    """matlab/mpcekf_export_rom.m's format -> ROM.load_json is lossless and keeps the
+    MATLAB column-major order: A(t,z,k) in MATLAB is rom.A[t-1, z-1, k-1] here."""
+    p = tmp_path / "rom.json"
+    rom.save_json(p)
+    q = type(rom).load(str(p))
+    for k in ("T_degC", "SOC_pct", "A", "C", "D", "xloc"):
+        assert np.array_equal(getattr(rom, k), getattr(q, k)), k
+    for side in ("neg", "pos"):
+        for k, v in getattr(rom, side).__dict__.items():
+            assert np.array_equal(np.asarray(v), np.asarray(getattr(getattr(q, side), k))), (side, k)
+    assert q.names == rom.names and (q.F, q.R, q.Q, q.Rc, q.Tref, q.Ts) == (rom.F, rom.R, rom.Q, rom.Rc, rom.Tref, rom.Ts)
+    lay_a, lay_b = rom.device_layout(), q.device_layout()
+    for k in lay_a:
+        assert np.array_equal(np.asarray(lay_a[k]), np.asarray(lay_b[k])), k
+    # column-major check on one hand-placed entry, as MATLAB would flatten it
+    d = rom.to_json_dict()
+    nT, nZ, nz, n1 = rom.C.shape
+    t, z, r, c = 2, 17, 13, 5
+    assert d["C"]["data"][t + nT * (z + nZ * (r + nz * c))] == rom.C[t, z, r, c]
+
+
+def test_rom_json_matlab_quirks_and_errors(rom):
+    ROMc = type(rom)
+    d = _matlab_jsonencode_quirks(rom.to_json_dict())
+    q = ROMc.from_json_dict(d)
+    assert np.isnan(q.neg.U[0]) and np.array_equal(q.neg.U[1:], rom.neg.U[1:])
+    # nz = 1: MATLAB reports size(D) as [nT nZ] (trailing 1 dropped)
+    d1 = rom.to_json_dict()
+    nT, nZ = rom.nT, rom.nZ
+    d1["D"] = {"shape": [nT, nZ], "order": "F", "data": d1["D"]["data"][: nT * nZ]}
+    d1["C"] = {"shape": [nT, nZ, 1, rom.n + 1], "order": "F",
+               "data": list(np.asarray(rom.C[:, :, :1, :]).ravel(order="F"))}
+    d1["names"], d1["xloc"] = rom.names[0], {"shape": [1, 1], "order": "F", "data": float(rom.xloc[0])}
+    q1 = ROMc.from_json_dict(d1)
+    assert q1.D.shape == (nT, nZ, 1) and q1.names == [rom.names[0]] and q1.xloc.shape == (1,)
+    bad = rom.to_json_dict()
+    bad["format"] = "something-else"
+    with pytest.raises(ValueError, match="format"):
+        ROMc.from_json_dict(bad)
+    bad = rom.to_json_dict()
+    bad["A"]["shape"] = [rom.nT, rom.nZ + 1, rom.n + 1]
+    with pytest.raises(ValueError, match="shape"):
+        ROMc.from_json_dict(bad)
+    bad = rom.to_json_dict()
+    bad["names"] = rom.names[:-1]
+    with pytest.raises(ValueError, match="tfData.names"):
+        ROMc.from_json_dict(bad)
+
+
+def test_json_rom_drives_oracle_identically(rom, tmp_path, oc):
+    """A ROM that went through the exchange format gives bit-identical closed-loop
+    trajectories in the C oracle (the same property holds for the GPU path, whose
+    inputs are the same packed arrays: ROM.device_layout)."""
+    p = tmp_path / "rom.json"
+    rom.save_json(p)
+    q = type(rom).load_json(str(p))
+    soc0, tc = np.array([8.0, 22.0]), np.array([21.0, 29.0])
+    a = oc.run(rom, soc0, tc, 40, nthreads=1)
+    b = oc.run(q, soc0, tc, 40, nthreads=1)
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+
+
+def test_matlab_exporter_writes_every_loaded_key():
+    """The MATLAB exporter (not runnable here: no MATLAB) must write every key
+    ROM.from_json_dict reads; checked on the script text."""
+    import pathlib
+    root = pathlib.Path(__file__).resolve().parents[1] / "matlab"
+    src = (root / "mpcekf_export_rom.m").read_text()
+    for k in ("T_degC", "SOC_pct", "Ts", "A", "C", "D", "names", "xloc", "F", "R", "Q", "Rc", "Tref",
+              "neg", "pos"):
+        assert f"out.{k} " in src or f"out.{k}=" in src or f"out.{k} =" in src, k
+    for k in ("theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL", "U", "dUdT", "dU"):
+        assert f"e.{k} " in src, k
+    assert "'mpcekf-rom-v1'" in src and "'order', 'F'" in src
+    assert (root / "mpcekf_pack_models.m").exists() and (root / "mpcekf_check_tables.m").exists()
