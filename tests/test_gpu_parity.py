@@ -299,3 +299,17 @@ def test_step_diagnostics_match_oracle(rom, oc, M, Np, Nc):
     assert np.isnan(out["zk"][-1, 3]).all() and (out["nviol"][-1, 3] == 0)
     np.testing.assert_array_equal(zk_last, out["zk"][-1])
     np.testing.assert_array_equal(zb_last, out["zbk"][-1])
+
+
+def test_json_exchanged_rom_is_bit_identical_on_gpu(rom, M, tmp_path):
+    """A ROM that went through matlab/mpcekf_export_rom.m's JSON format (ROM.load_json)
+    drives the GPU path to bit-identical trajectories: the exchange loses nothing the
+    kernels read."""
+    p = tmp_path / "rom.json"
+    rom.save_json(p)
+    q = type(rom).load_json(str(p))
+    soc0, tc = batch_inputs(64)
+    a = M.runMPC(rom, soc0, tc, 60)
+    b = M.runMPC(q, soc0, tc, 60)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
