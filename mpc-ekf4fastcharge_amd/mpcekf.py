@@ -45,6 +45,16 @@ def make_config(**kw) -> _lib.Config:
         elif k == "SigmaX0":
             for i in range(6):
                 c.SigmaX0[i] = float(v[i])
+        elif k == "method":
+            # initKF.m:44-49 blend selector.  Only the output blend ('OB', runMPC.m's choice)
+            # is built into the library; the model blend ('MB') exists in the oracle only
+            # (oracle/oracle_np.py) -- refuse it loudly rather than run something else.
+            m = str(v).upper()
+            if m not in ("OB", "OUTB", "MB", "MDLB"):
+                raise ValueError(f"method {v!r}: expected 'OB' or 'MB' (initKF.m:44-49)")
+            if m in ("MB", "MDLB"):
+                raise NotImplementedError("model-blend EKF ('MB', iterEKF.m:90-102) is not built into "
+                                          "libmpcekf yet (DESIGN.md §7)")
         elif k == "bounds":
             c.flags = (c.flags | _lib.CF_BOUNDS) if v else (c.flags & ~_lib.CF_BOUNDS)
         else:

@@ -361,8 +361,10 @@ def ob_step(Iapp, Tc, cs):
 # ---------------------------------------------------------------------------
 # initKF (initKF.m:30-136) and iterEKF 'OB' (iterEKF.m:30-210)
 # ---------------------------------------------------------------------------
-def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW):
+def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW, method="OB"):
+    """initKF.m:30-136.  method 'OB' (output blend) or 'MB' (model blend, initKF.m:44-49)."""
     n = rom.n
+    method = {"OUTB": "OB", "OB": "OB", "MDLB": "MB", "MB": "MB"}[method.upper()]
     if SigmaX0.shape != (n + 1, n + 1):
         raise ValueError("SigmaX0 has wrong dimension (initKF.m:66-69)")
     if T0 > 100:
@@ -378,7 +380,8 @@ def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW):
     return dict(rom=rom, cell=Cell(rom), ind=setup_inds(rom), M=M, n=n, nz=rom.nz,
                 x0=0.0, SigmaX0=float(SigmaX0[n, n]), xhat=np.zeros(n + 1),
                 SigmaV=SigmaV, SigmaW=SigmaW, priorI=0.0, Ts=rom.Ts, SOC0=SOC0 / 100,
-                Q=rom.Q, Tpts=np.unique(TK), Zpts=np.unique(ZS), warnCount=0, status=0)
+                Q=rom.Q, Tpts=np.unique(TK), Zpts=np.unique(ZS), warnCount=0, status=0,
+                method=method, SigmaX=np.array(SigmaX0, dtype=float))   # initKF.m:100-101 (MB)
 
 
 def get_xind(ekf, Tk, SOC):
@@ -417,7 +420,8 @@ def get_variables(ekf, ik, Xind, T):
     cell, ind = ekf["cell"], ekf["ind"]
     F, R = cell.F, cell.R
     mdl = [ekf["M"][(Xind["theT"][j], Xind["theZ"][j])] for j in range(4)]
-    x0 = ekf["x0"]
+    mb = ekf["method"] == "MB"
+    x0 = ekf["xhat"][-1] if mb else ekf["x0"]                   # iterEKF.m:265-275
     xSOC = ekf["SOC0"] - x0 * (ekf["Ts"] / (3600 * ekf["Q"]))
     SOCnAvg = cell.soc("neg", xSOC, T)
     SOCpAvg = cell.soc("pos", xSOC, T)
@@ -435,7 +439,8 @@ def get_variables(ekf, ik, Xind, T):
         SOCpAvg = 0.998
     Z = np.zeros(ekf["nz"])
     for j in range(4):                                          # iterEKF.m:312-313
-        zj = mv(mdl[j]["C"], mdl[j]["xhat"]) + mdl[j]["D"] * ik
+        xj = ekf["xhat"][:-1] if mb else mdl[j]["xhat"]         # MB: iterEKF.m:314-315
+        zj = mv(mdl[j]["C"], xj) + mdl[j]["D"] * ik
         Z = Z + zj * Xind["gamma"][j]
     If0 = Z[ind["If0"]]
     If3 = Z[ind["If3"]]
@@ -501,6 +506,8 @@ def get_chat_v(ekf, Xind, Z, Tk):
     cell, ind = ekf["cell"], ekf["ind"]
     F, R = cell.F, cell.R
     Cs = [Xind["gamma"][j] * ekf["M"][(Xind["theT"][j], Xind["theZ"][j])]["C"] for j in range(4)]
+    if ekf["method"] == "MB":
+        return _get_chat_v_mb(ekf, Cs, Z, Tk)
     x0 = ekf["x0"]
     xSOC = ekf["SOC0"] - x0 * (ekf["Ts"] / (3600 * ekf["Q"]))
     SOCnAvg = cell.soc("neg", xSOC, Tk)
@@ -527,10 +534,48 @@ def get_chat_v(ekf, Xind, Z, Tk):
     return Chat, Chat0
 
 
+def _sum4(rows):
+    """MATLAB sum([r1; r2; r3; r4]) down the columns, in row order."""
+    return ((rows[0] + rows[1]) + rows[2]) + rows[3]
+
+
+def _get_chat_v_mb(ekf, Cs, Z, Tk):
+    """getChatV 'MB' branches (iterEKF.m:448-459, 475-479, 489-491, 512-517): one blended
+    voltage row over the shared state, augmented with the integrator term -> (Chat[n+1], Chat0)."""
+    cell, ind = ekf["cell"], ekf["ind"]
+    F, R = cell.F, cell.R
+    Ts, Q = ekf["Ts"], ekf["Q"]
+    x0 = ekf["xhat"][-1]
+    xSOC = ekf["SOC0"] - x0 * (Ts / (3600 * Q))
+    SOCnAvg = cell.soc("neg", xSOC, Tk)
+    SOCpAvg = cell.soc("pos", xSOC, Tk)
+    Rfn = cell.Rf("neg", SOCnAvg, Tk)
+    Rfp = cell.Rf("pos", SOCpAvg, Tk)
+    rows = lambda r: _sum4([C[r] for C in Cs])
+    Chat = Rfp * rows(ind["Ifdl3"]) - Rfn * rows(ind["Ifdl0"])
+    k0n = cell.k0("neg", SOCnAvg, Tk)
+    k0p = cell.k0("pos", SOCpAvg, Tk)
+    i0n = k0n * _sqrt(Z[ind["Thetae"][0]] * (1 - Z[ind["Thetass0"]]) * Z[ind["Thetass0"]])
+    i0p = k0p * _sqrt(Z[ind["Thetae"][-1]] * (1 - Z[ind["Thetass3"]]) * Z[ind["Thetass3"]])
+    Rctn = R * Tk / (F * i0n)
+    Rctp = R * Tk / (F * i0p)
+    Chat = Chat + Rctp * rows(ind["If3"]) - Rctn * rows(ind["If0"])
+    Chat = Chat + rows(ind["Phie"][-1])
+    dUocpn0 = cell.dUocp("neg", Z[ind["Thetass0"]], Tk)
+    dUocpp3 = cell.dUocp("pos", Z[ind["Thetass3"]], Tk)
+    res0n = -dUocpn0 * Ts * (cell.soc("neg", 1, Tk) - cell.soc("neg", 0, Tk)) / (3600 * Q)
+    res0p = -dUocpp3 * Ts * (cell.soc("pos", 1, Tk) - cell.soc("pos", 0, Tk)) / (3600 * Q)
+    Chat0 = res0p - res0n
+    Chat = Chat + dUocpp3 * rows(ind["Thetass3"]) - dUocpn0 * rows(ind["Thetass0"])
+    return np.concatenate([Chat, [Chat0]]), Chat0
+
+
 def get_chat_z(ekf, Xind, Z, Tk):
-    """iterEKF.m:523-602 ('OB')."""
+    """iterEKF.m:523-602 ('OB'; 'MB' in _get_chat_z_mb)."""
     cell, ind = ekf["cell"], ekf["ind"]
     Cs = [Xind["gamma"][j] * ekf["M"][(Xind["theT"][j], Xind["theZ"][j])]["C"] for j in range(4)]
+    if ekf["method"] == "MB":
+        return _get_chat_z_mb(ekf, Xind, Cs, Z, Tk)
     Chat = [C.copy() for C in Cs]
     Chat0 = np.zeros(ekf["nz"])
     ChatV, ChatV0 = get_chat_v(ekf, Xind, Z, Tk)
@@ -562,8 +607,92 @@ def get_chat_z(ekf, Xind, Z, Tk):
     return Chat, ChatV, Chat0, ChatV0
 
 
+def _get_chat_z_mb(ekf, Xind, Cs, Z, Tk):
+    """getChatZ 'MB' branches (iterEKF.m:537-538, 554-558, 575-576, 596-600) -> (Chat nz x (n+1),
+    ChatV n+1, Chat0 nz, ChatV0)."""
+    cell, ind = ekf["cell"], ekf["ind"]
+    Chat = ((Cs[0] + Cs[1]) + Cs[2]) + Cs[3]
+    Chat0 = np.zeros(ekf["nz"])
+    ChatV, ChatV0 = get_chat_v(ekf, Xind, Z, Tk)
+    for r in ind["posPhis"]:
+        Chat[r] = Chat[r] + ChatV[:-1]
+    Chat0[ind["posPhis"]] = ChatV[-1]
+    Ts, Q = ekf["Ts"], ekf["Q"]
+    res0n = -Ts * (cell.soc("neg", 1, Tk) - cell.soc("neg", 0, Tk)) / (3600 * Q)
+    res0p = -Ts * (cell.soc("pos", 1, Tk) - cell.soc("pos", 0, Tk)) / (3600 * Q)
+    Chat0[ind["negThetass"]] = res0n
+    Chat0[ind["posThetass"]] = res0p
+    xSOC = ekf["SOC0"] - ekf["xhat"][-1] * (Ts / (3600 * Q))
+    dUocpn = cell.dUocp("neg", cell.soc("neg", xSOC, Tk), Tk)
+    dUocpp = cell.dUocp("pos", cell.soc("pos", xSOC, Tk), Tk)
+    Chat0[ind["negPhise"]] = dUocpn * res0n
+    Chat0[ind["posPhise"]] = dUocpp * res0p
+    Chat0[ind["Phie"]] = -dUocpn * res0n
+    for r in ind["Phie"]:
+        Chat[r] = Chat[r] - Chat[ind["Phise0"]]
+    return np.concatenate([Chat, Chat0[:, None]], axis=1), ChatV, Chat0, ChatV0
+
+
+def _symmetrise_bump(S, residual, St):
+    """iterEKF.m:142-154 / 164-173: svd symmetrisation, then the Q-bump."""
+    _, SS, VVh = np.linalg.svd(S)
+    VV = VVh.T
+    HH = (VV * SS[None, :]) @ VV.T
+    S = (S + S.T + HH + HH.T) / 4
+    if residual ** 2 > 9 * St:
+        S = S * 2
+    return S
+
+
+def _iter_ekf_mb(ekf, vk, ik, Tk):
+    """iterEKF.m:30-210 with method 'MB': one blended model over one (n+1) state and one
+    (n+1)x(n+1) covariance per cell (iterEKF.m:90-102, 125-128, 160-176, 199-203)."""
+    nz, n = ekf["nz"], ekf["n"]
+    r = ekf["Ts"] / (3600 * ekf["Q"])
+    W = ekf["SigmaW"]
+    SOC = ekf["SOC0"] - ekf["xhat"][-1] * r                     # iterEKF.m:92-93
+    Xind = get_xind(ekf, Tk, SOC)
+    As = [ekf["M"][(Xind["theT"][j], Xind["theZ"][j])]["A"] for j in range(4)]
+    g = Xind["gamma"]
+    AMB = np.concatenate([((As[0] * g[0] + As[1] * g[1]) + As[2] * g[2]) + As[3] * g[3], [1.0]])
+    ekf["xhat"] = AMB * ekf["xhat"] + ekf["priorI"]
+    ekf["SigmaX"] = (AMB[:, None] * ekf["SigmaX"]) * AMB[None, :] + W
+    SOC = ekf["SOC0"] - ekf["xhat"][-1] * r
+    Xind = get_xind(ekf, Tk, SOC)
+    vhat, Z, _ = get_variables(ekf, ik, Xind, Tk)
+    if ekf["status"] & ST_ERROR:
+        return np.full(nz + 2, NAN), np.full(nz + 2, NAN), None
+    ChatV, _ = get_chat_v(ekf, Xind, Z, Tk)                     # iterEKF.m:125-128
+    S = ekf["SigmaX"]
+    St = dot(mv(S.T, ChatV), ChatV) + ekf["SigmaV"]
+    L = mv(S, ChatV) / St
+    residual = vk - vhat
+    ekf["xhat"] = ekf["xhat"] + L * residual                     # iterEKF.m:160-173
+    LS = L * St
+    ekf["SigmaX"] = _symmetrise_bump(S - LS[:, None] * L[None, :], residual, St)
+    SOC = ekf["SOC0"] - ekf["xhat"][-1] * r
+    Xind = get_xind(ekf, Tk, SOC)
+    vhat, Z, Zsoc = get_variables(ekf, ik, Xind, Tk)
+    if ekf["status"] & ST_ERROR:
+        return np.full(nz + 2, NAN), np.full(nz + 2, NAN), None
+    zk = np.concatenate([Z, [vhat, Zsoc]])
+    res = -r
+    ChatZ, ChatVz, _, _ = get_chat_z(ekf, Xind, zk, Tk)         # iterEKF.m:199-203 (diag only)
+    S = ekf["SigmaX"]
+    P = mm(ChatZ, S)
+    SigZ = np.zeros(nz)
+    for c in range(n + 1):
+        SigZ = SigZ + P[:, c] * ChatZ[:, c]
+    SigV = dot(mv(S.T, ChatVz), ChatVz)
+    SigSOC = res * S[-1, -1] * res
+    with np.errstate(invalid="ignore"):
+        boundzk = 3 * np.sqrt(np.concatenate([SigZ, [SigV, SigSOC]]))
+    ekf["priorI"] = ik
+    return zk, boundzk, Xind
+
+
 def iter_ekf(ekf, vk, ik, Tk):
-    """iterEKF.m:30-210 with method 'OB'. Returns (zk, boundzk, Xind)."""
+    """iterEKF.m:30-210 with method 'OB' ('MB' in _iter_ekf_mb). Returns (zk, boundzk, Xind)."""
     nz = ekf["nz"]
     if ekf["status"] & ST_ERROR:
         return np.full(nz + 2, NAN), np.full(nz + 2, NAN), None
@@ -574,6 +703,8 @@ def iter_ekf(ekf, vk, ik, Tk):
         pass
     else:
         Tk = Tk + 273.15
+    if ekf["method"] == "MB":
+        return _iter_ekf_mb(ekf, vk, ik, Tk)
     W = ekf["SigmaW"]
     for key, m in ekf["M"].items():                             # iterEKF.m:73-84
         A = m["A"]
@@ -840,7 +971,7 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state):
     if cfg:
         c.update(cfg)
     SigmaX0 = np.diag([1.0] * rom.n + [2e6])
-    ekf = init_kf(rom, SOC0, TC, SigmaX0, c["SigmaV"], c["SigmaW"])
+    ekf = init_kf(rom, SOC0, TC, SigmaX0, c["SigmaV"], c["SigmaW"], c.get("method", "OB"))
     mpc = init_mpc(rom, SOC0, c["Np"], c["Nc"], c["targetSOC"], c)
     cs = ob_step_init(rom, SOC0, TC)
     uk = 0.0
