@@ -95,3 +95,16 @@ def test_gpu_library_refuses_mb(P):
         M.make_config(method="MB")
     with pytest.raises(ValueError):
         M.make_config(method="UKF")
+
+
+def test_mb_golden_fixture(rom):
+    """tests/golden/mb_batch4_200.npz (tools/make_golden.py: make_mb) stays reproducible:
+    the pin the C oracle's and the kernel's MB variants will be held to."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "mb_batch4_200.npz"))
+    for c in range(len(g["soc0"])):
+        o = O.run_cell(rom, float(g["soc0"][c]), float(g["tc"][c]), g["u"].shape[0], {"method": "MB"})
+        for k in ("u", "v", "soc", "phise"):   # rtol: LAPACK svd rounding may differ by build
+            np.testing.assert_allclose(o[k], g[k][:, c], rtol=1e-10, atol=0, err_msg=k)
+        np.testing.assert_array_equal(o["nexec"], g["nexec"][:, c])
+        assert o["status"][-1] == g["status"][c] == 0

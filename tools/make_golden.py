@@ -31,8 +31,8 @@ def rom_hash(rom):
     return h.hexdigest()
 
 
-def run_cells(rom, soc0, tc, steps):
-    outs = [O.run_cell(rom, s, t, steps) for s, t in zip(soc0, tc)]
+def run_cells(rom, soc0, tc, steps, cfg=None):
+    outs = [O.run_cell(rom, s, t, steps, cfg) for s, t in zip(soc0, tc)]
     res = {k: np.stack([o[k] for o in outs], axis=1) for k in ("u", "v", "soc", "phise", "nexec")}
     res["status"] = np.array([o["status"][-1] for o in outs])
     res["zk_last"] = np.stack([o["zk"][-1] for o in outs])
@@ -40,8 +40,22 @@ def run_cells(rom, soc0, tc, steps):
     return res
 
 
+def make_mb(rom, hsh):
+    """Model-blend ('MB') EKF trajectories (iterEKF.m:90-102 and the MB branches): the fixture
+    the C oracle and the kernel's MB variant will be checked against."""
+    rng = np.random.Generator(np.random.PCG64(0x5EED))
+    soc0, tc = rng.uniform(5, 30, 4), rng.uniform(20, 30, 4)
+    r = run_cells(rom, soc0, tc, 200, {"method": "MB"})
+    np.savez_compressed(os.path.join(OUT, "mb_batch4_200.npz"), rom_hash=hsh, soc0=soc0, tc=tc, **r)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--mb-only" in sys.argv:
+        P = importlib.import_module("mpc-ekf4fastcharge_amd")
+        rom = P.make_synth_rom()
+        make_mb(rom, rom_hash(rom))
+        return
     P = importlib.import_module("mpc-ekf4fastcharge_amd")
     rom = P.make_synth_rom()
     hsh = rom_hash(rom)
@@ -66,7 +80,9 @@ def main():
     r = run_cells(rom1, [12.0, 40.0], [25.0, 22.0], 200)
     np.savez_compressed(os.path.join(OUT, "rom_nt1_200.npz"), rom_hash=rom_hash(rom1), soc0=[12.0, 40.0],
                         tc=[25.0, 22.0], **r)
-    # 5. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
+    # 5. model-blend EKF variant
+    make_mb(rom, hsh)
+    # 6. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
     rng = np.random.default_rng(11)
     n = 24
     a = np.concatenate([rng.uniform(0.2, 0.999, (n, 5)), np.ones((n, 1))], 1)
