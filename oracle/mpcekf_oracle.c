@@ -71,6 +71,7 @@ typedef struct {
   double SigmaV, SigmaW;
   double SigmaX0[NX + 1]; /* diagonal of SigmaX0 (runMPC.m:17) */
   int max_warn;           /* iterEKF.m:55: lockout when warnCount > max_warn */
+  int method;             /* 0 = 'OB' output blend (runMPC.m), 1 = 'MB' model blend (initKF.m:44-49) */
 } orc_cfg;
 
 /* resolved output indices (iterEKF.m:610-735) */
@@ -88,6 +89,9 @@ typedef struct {
   double *xhat; /* [NM][NX] */
   double *S;    /* [NM][NPK] */
   double x0, S0, priorI, SOC0;
+  /* 'MB': one shared model state (x0 above is its integrator, xhat(end)) and one full
+   * (NX+1)x(NX+1) covariance (initKF.m:100-101) */
+  double xmb[NX], Smb[(NX + 1) * (NX + 1)];
   int warn, status;
   /* mpc */
   double uk_1, uk;
@@ -682,7 +686,7 @@ static double get_variables(const orc_ctx *X, orc_cell *s, double ik, const orc_
   if (SOCpAvg > 0.998) { s->warn++; SOCpAvg = 0.998; }
   for (int q = 0; q < nz; ++q) Z[q] = 0.0;
   for (int j = 0; j < 4; ++j) {
-    const double *x = s->xhat + (size_t)xi->m[j] * NX;
+    const double *x = X->c->method ? s->xmb : s->xhat + (size_t)xi->m[j] * NX; /* MB: iterEKF.m:314-315 */
     for (int q = 0; q < nz; ++q) {
       const double *c = Crow(r, xi->m[j], q);
       double acc = 0.0;
@@ -764,6 +768,184 @@ static void get_chat_v(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, 
   *Chat0 = res0p - res0n;
 }
 
+/* ---- 'MB' model blend (iterEKF.m:90-102, 125-128, 160-176, 199-203 and the MB branches of
+ * getVariables / getChatV / getChatZ).  State: s->xmb (NX) + s->x0 (integrator), s->Smb. ---- */
+#define NA (NX + 1)
+
+/* getChatV 'MB' (iterEKF.m:448-459, 475-479, 489-491, 512-517): sums over the four
+ * gamma-weighted corner rows, then the terms, integrator entry last. */
+static void get_chat_v_mb(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, const double *Z, double T,
+                          double ChV[NA]) {
+  const orc_rom *r = X->r;
+  const orc_ind *ix = &X->ix;
+  const orc_electrode *en = &r->neg, *ep = &r->pos;
+  double Rfn = en->Rf, Rfp = ep->Rf;
+  double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
+  double i0n = k0n * msqrt(Z[ix->Thetae1] * (1 - Z[ix->Thetass0]) * Z[ix->Thetass0]);
+  double i0p = k0p * msqrt(Z[ix->ThetaeE] * (1 - Z[ix->Thetass3]) * Z[ix->Thetass3]);
+  double Rctn = r->R * T / (r->F * i0n), Rctp = r->R * T / (r->F * i0p);
+  double dUn0 = fdUocp(en, Z[ix->Thetass0]), dUp3 = fdUocp(ep, Z[ix->Thetass3]);
+  const int rows[7] = {ix->Ifdl3, ix->Ifdl0, ix->If3, ix->If0, ix->PhieE, ix->Thetass3, ix->Thetass0};
+  for (int k = 0; k < NX; ++k) {
+    double sum[7];
+    for (int t = 0; t < 7; ++t) {
+      double a = 0.0;
+      for (int j = 0; j < 4; ++j) a = a + xi->g[j] * Crow(r, xi->m[j], rows[t])[k];
+      sum[t] = a;
+    }
+    double v = Rfp * sum[0] - Rfn * sum[1];
+    v = v + Rctp * sum[2] - Rctn * sum[3];
+    v = v + sum[4];
+    v = v + dUp3 * sum[5] - dUn0 * sum[6];
+    ChV[k] = v;
+  }
+  double dn = fsoc(en, 1) - fsoc(en, 0), dp = fsoc(ep, 1) - fsoc(ep, 0);
+  double res0n = -dUn0 * r->Ts * dn / (3600 * r->Q);
+  double res0p = -dUp3 * r->Ts * dp / (3600 * r->Q);
+  ChV[NX] = res0p - res0n;
+}
+
+static int is_pd_n(int n, const double *a) {
+  double l[NA][NA], d[NA];
+  for (int j = 0; j < n; ++j) {
+    double s = a[j * n + j];
+    for (int k = 0; k < j; ++k) s = fma(-(l[j][k] * l[j][k]), d[k], s);
+    if (!(s > 0)) return 0;
+    d[j] = s;
+    double inv = 1.0 / s;
+    for (int i = j + 1; i < n; ++i) {
+      double t = a[i * n + j];
+      for (int k = 0; k < j; ++k) t = fma(-(l[i][k] * l[j][k]), d[k], t);
+      l[i][j] = t * inv;
+    }
+  }
+  return 1;
+}
+
+/* iterEKF.m:164-173 on the full MB covariance (same polar-factor spelling as orc_meas_cov) */
+static void meas_cov_mb(double *S, const double *L, double St, int bump) {
+  double P[NA * NA], a[NA * NA], V[NA * NA], w[NA], HH[NA * NA];
+  for (int r = 0; r < NA; ++r)
+    for (int c = 0; c < NA; ++c) P[r * NA + c] = fma(-(L[r] * St), L[c], S[r * NA + c]);
+  for (int r = 0; r < NA; ++r)
+    for (int c = 0; c < NA; ++c) a[r * NA + c] = (P[r * NA + c] + P[c * NA + r]) * 0.5;
+  if (is_pd_n(NA, a)) {
+    memcpy(HH, a, sizeof(HH));
+  } else {
+    orc_jacobi(NA, a, V, w);
+    for (int r = 0; r < NA; ++r)
+      for (int c = 0; c < NA; ++c) {
+        double acc = 0.0;
+        for (int k = 0; k < NA; ++k) acc = acc + (V[r * NA + k] * fabs(w[k])) * V[c * NA + k];
+        HH[r * NA + c] = acc;
+      }
+  }
+  for (int r = 0; r < NA; ++r)
+    for (int c = r; c < NA; ++c) {
+      double v = (((P[r * NA + c] + P[c * NA + r]) + HH[r * NA + c]) + HH[c * NA + r]) / 4.0;
+      if (bump) v = v * 2.0;
+      S[r * NA + c] = v;
+      S[c * NA + r] = v;
+    }
+}
+
+static double qform_full(const double *S, const double *row) {
+  double acc = 0.0;
+  for (int c = 0; c < NA; ++c) {
+    double t = 0.0;
+    for (int k = 0; k < NA; ++k) t = fma(S[k * NA + c], row[k], t);
+    acc = fma(t, row[c], acc);
+  }
+  return acc;
+}
+
+static int ekf_step_mb(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tk, double *zk, double *zbk,
+                       orc_xind *xo) {
+  const orc_rom *r = X->r;
+  const orc_cfg *cf = X->c;
+  const orc_ind *ix = &X->ix;
+  int nz = r->nz;
+  double rs = r->Ts / (3600 * r->Q);
+  double W = cf->SigmaW;
+  orc_xind xi;
+  get_xind(X, Tk, s->SOC0 - s->x0 * rs, &xi); /* iterEKF.m:92-93 */
+  double amb[NA];
+  for (int k = 0; k < NX; ++k) {
+    double a = 0.0;
+    for (int j = 0; j < 4; ++j) a = a + r->A[(size_t)xi.m[j] * (NX + 1) + k] * xi.g[j];
+    amb[k] = a;
+  }
+  amb[NX] = 1.0;
+  for (int k = 0; k < NX; ++k) s->xmb[k] = amb[k] * s->xmb[k] + s->priorI;
+  s->x0 = s->x0 + s->priorI;
+  for (int p = 0; p < NA; ++p)
+    for (int q = 0; q < NA; ++q) s->Smb[p * NA + q] = (amb[p] * s->Smb[p * NA + q]) * amb[q] + W;
+  get_xind(X, Tk, s->SOC0 - s->x0 * rs, &xi);
+  double Z[256], Zsoc;
+  double vhat = get_variables(X, s, ik, &xi, Tk, Z, &Zsoc);
+  if (s->status & ST_ERROR) return -1;
+  double ChV[NA], L[NA];
+  get_chat_v_mb(X, s, &xi, Z, Tk, ChV); /* iterEKF.m:125-128 */
+  double St = qform_full(s->Smb, ChV) + cf->SigmaV;
+  for (int p = 0; p < NA; ++p) {
+    double acc = 0.0;
+    for (int k = 0; k < NA; ++k) acc = fma(s->Smb[p * NA + k], ChV[k], acc);
+    L[p] = acc / St;
+  }
+  double res = vk - vhat;
+  for (int k = 0; k < NX; ++k) s->xmb[k] = fma(L[k], res, s->xmb[k]);
+  s->x0 = fma(L[NX], res, s->x0);
+  meas_cov_mb(s->Smb, L, St, res * res > 9 * St);
+  get_xind(X, Tk, s->SOC0 - s->x0 * rs, &xi);
+  vhat = get_variables(X, s, ik, &xi, Tk, Z, &Zsoc);
+  if (s->status & ST_ERROR) return -1;
+  for (int q = 0; q < nz; ++q) zk[q] = Z[q];
+  zk[nz] = vhat;
+  zk[nz + 1] = Zsoc;
+  if (zbk) { /* getChatZ 'MB' (iterEKF.m:537-538, 554-558, 575-576, 596-600) + iterEKF.m:199-203 */
+    const orc_electrode *en = &r->neg, *ep = &r->pos;
+    double ChVz[NA];
+    get_chat_v_mb(X, s, &xi, zk, Tk, ChVz);
+    double res0n = -r->Ts * (fsoc(en, 1) - fsoc(en, 0)) / (3600 * r->Q);
+    double res0p = -r->Ts * (fsoc(ep, 1) - fsoc(ep, 0)) / (3600 * r->Q);
+    double xSOC = s->SOC0 - s->x0 * rs;
+    double dUn = fdUocp(en, fsoc(en, xSOC)), dUp = fdUocp(ep, fsoc(ep, xSOC));
+    double Ch[256][NA];
+    double c0[256];
+    for (int q = 0; q < nz; ++q) {
+      for (int k = 0; k < NX; ++k) {
+        double a = 0.0;
+        for (int j = 0; j < 4; ++j) a = a + xi.g[j] * Crow(r, xi.m[j], q)[k];
+        Ch[q][k] = a;
+      }
+      c0[q] = 0.0;
+    }
+    for (int t = 0; t < ix->nPosPhis; ++t) {
+      int q = ix->posPhis[t];
+      for (int k = 0; k < NX; ++k) Ch[q][k] = Ch[q][k] + ChVz[k];
+      c0[q] = ChVz[NX];
+    }
+    for (int k = 0; k < ix->nNegTh; ++k) c0[ix->negTh[k]] = res0n;
+    for (int k = 0; k < ix->nPosTh; ++k) c0[ix->posTh[k]] = res0p;
+    for (int k = 0; k < ix->nNegPhise; ++k) c0[ix->negPhise[k]] = dUn * res0n;
+    for (int k = 0; k < ix->nPosPhise; ++k) c0[ix->posPhise[k]] = dUp * res0p;
+    for (int k = 0; k < ix->nPhie; ++k) c0[ix->Phie[k]] = -dUn * res0n;
+    for (int t = 0; t < ix->nPhie; ++t) {
+      int q = ix->Phie[t];
+      for (int k = 0; k < NX; ++k) Ch[q][k] = Ch[q][k] - Ch[ix->Phise0][k];
+    }
+    for (int q = 0; q < nz; ++q) {
+      Ch[q][NX] = c0[q];
+      zbk[q] = 3 * msqrt(qform_full(s->Smb, Ch[q]));
+    }
+    zbk[nz] = 3 * msqrt(qform_full(s->Smb, ChVz));
+    zbk[nz + 1] = 3 * msqrt(rs * s->Smb[NA * NA - 1] * rs);
+  }
+  s->priorI = ik;
+  if (xo) *xo = xi;
+  return 0;
+}
+
 /* iterEKF 'OB' one step.  zk: nz+2, zbk: nz+2 (may be NULL). Returns 0 ok. */
 int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc, double *zk, double *zbk,
                  orc_xind *xo) {
@@ -774,6 +956,7 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
   if (s->status & ST_ERROR) return -1;
   if (s->warn > cf->max_warn) { s->status |= ST_LOCKOUT | ST_ERROR; return -1; }
   double Tk = Tc > 100 ? Tc : Tc + 273.15;
+  if (cf->method) return ekf_step_mb(X, s, vk, ik, Tk, zk, zbk, xo);
   double W = cf->SigmaW;
   for (int m = 0; m < X->NM; ++m) {
     const double *a = r->A + (size_t)m * (NX + 1);
@@ -901,7 +1084,7 @@ void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, c
     if (xi->g[j] > xi->g[imax] || (xi->g[imax] != xi->g[imax] && xi->g[j] == xi->g[j])) imax = j;
   int m = xi->m[imax];
   for (int k = 0; k < NX; ++k) { L->xhat[k] = s->xhat[(size_t)m * NX + k]; L->a[k] = r->A[(size_t)m * (NX + 1) + k]; }
-  L->xhat[NX] = 0.0; /* ekfData.xhat(end): never updated in 'OB' */
+  L->xhat[NX] = X->c->method ? s->x0 : 0.0; /* ekfData.xhat(end): never updated in 'OB' */
   L->a[NX] = 1.0;
   double rr = -r->Ts / (3600 * r->Q);
   for (int k = 0; k <= NX; ++k) L->Csoc[k] = 0.0;
@@ -1147,6 +1330,9 @@ static void init_cell(const orc_ctx *X, orc_cell *s, double soc0, double tc) {
   s->Tc = tc;
   s->x0 = 0.0;
   s->S0 = c->SigmaX0[NX];
+  for (int p = 0; p < NX; ++p) s->xmb[p] = 0.0;
+  for (int p = 0; p <= NX; ++p)
+    for (int q = 0; q <= NX; ++q) s->Smb[p * (NX + 1) + q] = p == q ? c->SigmaX0[p] : 0.0;
   s->priorI = 0.0;
   s->SOC0 = soc0 / 100;
   s->warn = 0;

@@ -44,7 +44,7 @@ class _Cfg(C.Structure):
                 ("z_tol", C.c_double), ("use_cur", C.c_int), ("use_v", C.c_int),
                 ("use_eta", C.c_int), ("maxHild", C.c_int), ("hild_tol", C.c_double),
                 ("SigmaV", C.c_double), ("SigmaW", C.c_double), ("SigmaX0", C.c_double * 6),
-                ("max_warn", C.c_int)]
+                ("max_warn", C.c_int), ("method", C.c_int)]
 
 
 def build(quiet=True):
@@ -127,7 +127,8 @@ class PackedRom:
 
 DEFAULTS = dict(Np=5, Nc=2, ref=95.0, u_max=2.0, Crate=2.0, du_min=-50.0, du_max=50.0, v_max=4.1,
                 phise_min=0.08, z_max=0.95, z_tol=0.0, constraints=(1, 1, 1), maxHild=100,
-                hild_tol=1e-6, SigmaV=1e-3, SigmaW=1e2, SigmaX0=(1, 1, 1, 1, 1, 2e6), max_warn=10)
+                hild_tol=1e-6, SigmaV=1e-3, SigmaW=1e2, SigmaX0=(1, 1, 1, 1, 1, 2e6), max_warn=10,
+                method="OB")
 
 
 def make_cfg(**kw):
@@ -141,6 +142,7 @@ def make_cfg(**kw):
     c.use_cur, c.use_v, c.use_eta = (int(x) for x in d["constraints"])
     c.maxHild = d["maxHild"]
     c.max_warn = d["max_warn"]
+    c.method = {"OB": 0, "OUTB": 0, "MB": 1, "MDLB": 1}[str(d["method"]).upper()]   # initKF.m:44-49
     for i in range(6):
         c.SigmaX0[i] = float(d["SigmaX0"][i])
     return c

@@ -108,3 +108,19 @@ def test_mb_golden_fixture(rom):
             np.testing.assert_allclose(o[k], g[k][:, c], rtol=1e-10, atol=0, err_msg=k)
         np.testing.assert_array_equal(o["nexec"], g["nexec"][:, c])
         assert o["status"][-1] == g["status"][c] == 0
+
+
+def test_c_oracle_mb_matches_numpy(rom, oc):
+    """The C restatement's MB branch (oracle/mpcekf_oracle.c: ekf_step_mb) against the numpy
+    one through the MB fixture: the two restatements agree to rounding (1e-12 relative),
+    boundzk included."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "mb_batch4_200.npz"))
+    r = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=2, want_zk=True, method="MB")
+    for k in ("u", "v", "soc", "phise"):
+        np.testing.assert_allclose(r[k], g[k], rtol=1e-12, atol=0, err_msg=k)
+    np.testing.assert_array_equal(r["nexec"], g["nexec"])
+    np.testing.assert_allclose(r["zk"], g["zk_last"], rtol=1e-12, atol=1e-15)
+    np.testing.assert_allclose(r["zbk"], g["zbk_last"], rtol=1e-12, atol=1e-15)
+    ob = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=2)
+    assert not np.array_equal(ob["u"], r["u"])   # the switch really selects another filter
