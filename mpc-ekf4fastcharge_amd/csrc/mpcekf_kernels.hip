@@ -10,8 +10,8 @@
 //                            iterMPC.m and hildreth.m for one cell per lane
 // The ROM (C/D rows, diag(A), OCP tables) is staged once per workgroup in LDS.
 // Arithmetic follows the defined order of oracle/mpcekf_oracle.c (sequential
-// sums from +0.0, no contraction), so results match it bit-for-bit apart from
-// asinh (device libm vs glibc).
+// sums from +0.0, no contraction, asinh spelled out as dasinh), so results match
+// it bit-for-bit.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -43,6 +43,56 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 __device__ __forceinline__ int pk(int r, int c) {
   // packed upper-triangular index, row-major over r <= c
   return r <= c ? r * NX - (r * (r - 1)) / 2 + (c - r) : c * NX - (c * (c - 1)) / 2 + (r - c);
+}
+
+// Defined asinh (the plant/EKF overpotential, OB_step.m:333-334, iterEKF.m:400-401,
+// EKFmatsHandler.m:88-89).  Neither ocml's nor glibc's asinh is correctly rounded, so
+// the kernels and oracle/mpcekf_oracle.c (orc_asinh) both evaluate this spelling: a
+// reduction to log(u) + c with u = 2^k m, m in (sqrt(2)/2, sqrt(2)], and the classic
+// minimax series in s = f / (2 + f), f = m - 1 (Lg1..Lg7, fdlibm's public
+// coefficients).  Only +, -, *, /, sqrt and fma: correctly rounded on both sides.
+namespace dm {
+constexpr double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+constexpr double LN2 = 6.93147180559945286227e-01;
+constexpr double LG1 = 6.666666666666735130e-01, LG2 = 3.999999999940941908e-01, LG3 = 2.857142874366239149e-01,
+                 LG4 = 2.222219843214978396e-01, LG5 = 1.818357216161805012e-01, LG6 = 1.531383769920937332e-01,
+                 LG7 = 1.479819860511658591e-01;
+constexpr double SQRT2 = 1.4142135623730951;
+// log(u) + c for a finite u >= 1; c is the relative correction (u_true - u) / u
+__device__ __forceinline__ double log_core(double u, double c) {
+  unsigned long long b = (unsigned long long)__double_as_longlong(u);
+  int k = (int)(b >> 52) - 1023;
+  double m = __longlong_as_double((long long)((b & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL));
+  if (m > SQRT2) { m = 0.5 * m; k = k + 1; }
+  double f = m - 1.0;
+  double s = f / (2.0 + f);
+  double z = s * s;
+  double w = z * z;
+  double t1 = w * (LG2 + w * (LG4 + w * LG6));
+  double t2 = z * (LG1 + w * (LG3 + w * (LG5 + w * LG7)));
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  double dk = (double)k;
+  return dk * LN2_HI - ((hfsq - (s * (hfsq + R) + (dk * LN2_LO + c))) - f);
+}
+}  // namespace dm
+__device__ __forceinline__ double dasinh(double x) {
+  double a = fabs(x);
+  if (!(a < __builtin_inf())) return x + x;  // NaN, +-inf
+  if (a < 0x1p-28) return x;
+  double t;
+  if (a > 0x1p28) {
+    t = dm::log_core(a, 0.0) + dm::LN2;
+  } else if (a > 2.0) {
+    t = dm::log_core(2.0 * a + 1.0 / (sqrt(fma(a, a, 1.0)) + a), 0.0);
+  } else {  // log1p(a + a^2 / (1 + sqrt(1 + a^2)))
+    double a2 = a * a;
+    double xx = a + a2 / (1.0 + sqrt(1.0 + a2));
+    double u = 1.0 + xx;
+    double c = (xx - (u - 1.0)) / u;
+    t = dm::log_core(u, c);
+  }
+  return x < 0 ? -t : t;
 }
 
 __device__ __forceinline__ double tabi(const double *t, int n, double x) {
@@ -427,8 +477,8 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   }
   double i0n = cc.k0n * sqrt(Z[R_TE1] * (1 - Z[R_TH0]) * Z[R_TH0]);
   double i0p = cc.k0p * sqrt(Z[R_TEE] * (1 - Z[R_TH3]) * Z[R_TH3]);
-  double negEta0 = 2 * r.R * cc.T / r.F * asinh(If0 / (2 * i0n));
-  double posEta3 = 2 * r.R * cc.T / r.F * asinh(If3 / (2 * i0p));
+  double negEta0 = 2 * r.R * cc.T / r.F * dasinh(If0 / (2 * i0n));
+  double posEta3 = 2 * r.R * cc.T / r.F * dasinh(If3 / (2 * i0p));
   double Uocpn0 = uocp(cc.tb, cc.ntab, 0, Z[R_TH0], cc.dT), Uocpp3 = uocp(cc.tb, cc.ntab, 1, Z[R_TH3], cc.dT);
   double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (r.Rfp * Z[R_IFDL3] - r.Rfn * Z[R_IFDL0]);
 #pragma unroll
@@ -522,8 +572,8 @@ __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, c
   L.Dv = r.Rfp * Dm[R_IFDL3] - r.Rfn * Dm[R_IFDL0] + Dm[R_PHIE];
   double dT = TK - r.Tref;
   double Upos = uocp(cc.tb, cc.ntab, 1, zr[R_TH3], dT), Uneg = uocp(cc.tb, cc.ntab, 0, zr[R_TH0], dT);
-  double negEta0 = 2 * r.R * TK / r.F * asinh(zr[R_IF0] / (2 * i0n));
-  double posEta3 = 2 * r.R * TK / r.F * asinh(zr[R_IF3] / (2 * i0p));
+  double negEta0 = 2 * r.R * TK / r.F * dasinh(zr[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * TK / r.F * dasinh(zr[R_IF3] / (2 * i0p));
   double b_phi = 0.01 * 0;
   L.bv = (Upos - Uneg) + (posEta3 - negEta0) + b_phi;
   L.bphi = uocp(cc.tb, cc.ntab, 0, SOCnAvg, r.Tref - r.Tref);
@@ -1130,8 +1180,8 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   double teE = fmax(yk[R_TEE] + 1, 1e-6);
   double i0n = s.k0n[c] * sqrt(te1 * (1 - th0) * th0);
   double i0p = s.k0p[c] * sqrt(teE * (1 - th3) * th3);
-  double negEta0 = 2 * r.R * T / r.F * asinh(yk[R_IF0] / (2 * i0n));
-  double posEta3 = 2 * r.R * T / r.F * asinh(yk[R_IF3] / (2 * i0p));
+  double negEta0 = 2 * r.R * T / r.F * dasinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * T / r.F * dasinh(yk[R_IF3] / (2 * i0p));
   double Uocpn0 = uocp(tb, nt, 0, th0, dT), Uocpp3 = uocp(tb, nt, 1, th3, dT);
   double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (r.Rfp * yk[R_IFDL3] - r.Rfn * yk[R_IFDL0]);
   V = V - r.Rc * Iapp;

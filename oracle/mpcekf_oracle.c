@@ -31,6 +31,58 @@
 #include <omp.h>
 #endif
 
+/* Defined asinh, the same spelling as dasinh in mpcekf_kernels.hip (the overpotential
+ * of OB_step.m:333-334, iterEKF.m:400-401, EKFmatsHandler.m:88-89).  glibc's asinh is not
+ * correctly rounded, and neither is the GPU's, so both sides evaluate log(u) + c with
+ * u = 2^k m, m in (sqrt(2)/2, sqrt(2)], and the minimax series in s = f / (2 + f),
+ * f = m - 1 (fdlibm's published Lg1..Lg7).  Only +, -, *, /, sqrt and fma. */
+static const double DM_LN2_HI = 6.93147180369123816490e-01, DM_LN2_LO = 1.90821492927058770002e-10;
+static const double DM_LN2 = 6.93147180559945286227e-01;
+static const double DM_LG1 = 6.666666666666735130e-01, DM_LG2 = 3.999999999940941908e-01,
+                    DM_LG3 = 2.857142874366239149e-01, DM_LG4 = 2.222219843214978396e-01,
+                    DM_LG5 = 1.818357216161805012e-01, DM_LG6 = 1.531383769920937332e-01,
+                    DM_LG7 = 1.479819860511658591e-01;
+
+static double dm_log_core(double u, double c) { /* log(u) + c, u >= 1 finite */
+  uint64_t b;
+  memcpy(&b, &u, 8);
+  int k = (int)(b >> 52) - 1023;
+  uint64_t mb = (b & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL;
+  double m;
+  memcpy(&m, &mb, 8);
+  if (m > 1.4142135623730951) { m = 0.5 * m; k = k + 1; }
+  double f = m - 1.0;
+  double s = f / (2.0 + f);
+  double z = s * s;
+  double w = z * z;
+  double t1 = w * (DM_LG2 + w * (DM_LG4 + w * DM_LG6));
+  double t2 = z * (DM_LG1 + w * (DM_LG3 + w * (DM_LG5 + w * DM_LG7)));
+  double R = t2 + t1;
+  double hfsq = 0.5 * f * f;
+  double dk = (double)k;
+  return dk * DM_LN2_HI - ((hfsq - (s * (hfsq + R) + (dk * DM_LN2_LO + c))) - f);
+}
+
+double orc_asinh(double x) {
+  double a = fabs(x);
+  if (!(a < INFINITY)) return x + x;
+  if (a < 0x1p-28) return x;
+  double t;
+  if (a > 0x1p28) {
+    t = dm_log_core(a, 0.0) + DM_LN2;
+  } else if (a > 2.0) {
+    t = dm_log_core(2.0 * a + 1.0 / (sqrt(fma(a, a, 1.0)) + a), 0.0);
+  } else { /* log1p(a + a^2 / (1 + sqrt(1 + a^2))) */
+    double a2 = a * a;
+    double xx = a + a2 / (1.0 + sqrt(1.0 + a2));
+    double u = 1.0 + xx;
+    double c = (xx - (u - 1.0)) / u;
+    t = dm_log_core(u, c);
+  }
+  return x < 0 ? -t : t;
+}
+#define dasinh orc_asinh
+
 #define NX 5
 #define NPK 15
 #define NPMAX 20
@@ -659,8 +711,8 @@ double orc_plant_step(const orc_ctx *X, orc_cell *s, double Iapp) {
   double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
   double i0n = k0n * msqrt(te1 * (1 - th0) * th0);
   double i0p = k0p * msqrt(teE * (1 - th3) * th3);
-  double negEta0 = 2 * R * T / F * asinh(yk[R_IF0] / (2 * i0n));
-  double posEta3 = 2 * R * T / F * asinh(yk[R_IF3] / (2 * i0p));
+  double negEta0 = 2 * R * T / F * dasinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * R * T / F * dasinh(yk[R_IF3] / (2 * i0p));
   double Uocpn0 = fUocp(r, en, th0, T), Uocpp3 = fUocp(r, ep, th3, T);
   double Rfn = en->Rf, Rfp = ep->Rf;
   (void)negSOC; (void)posSOC;
@@ -724,8 +776,8 @@ static double get_variables(const orc_ctx *X, orc_cell *s, double ik, const orc_
   double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
   double i0n = k0n * msqrt(Z[ix->Thetae1] * (1 - Z[ix->Thetass0]) * Z[ix->Thetass0]);
   double i0p = k0p * msqrt(Z[ix->ThetaeE] * (1 - Z[ix->Thetass3]) * Z[ix->Thetass3]);
-  double negEta0 = 2 * r->R * T / r->F * asinh(If0 / (2 * i0n));
-  double posEta3 = 2 * r->R * T / r->F * asinh(If3 / (2 * i0p));
+  double negEta0 = 2 * r->R * T / r->F * dasinh(If0 / (2 * i0n));
+  double posEta3 = 2 * r->R * T / r->F * dasinh(If3 / (2 * i0p));
   double Uocpn0 = fUocp(r, en, Z[ix->Thetass0], T), Uocpp3 = fUocp(r, ep, Z[ix->Thetass3], T);
   double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (ep->Rf * Z[ix->Ifdl3] - en->Rf * Z[ix->Ifdl0]);
   for (int k = 0; k < ix->nPosPhis; ++k) Z[ix->posPhis[k]] = Z[ix->posPhis[k]] + V;
@@ -1102,8 +1154,8 @@ void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, c
   L->Cv[NX] = 0.0;
   L->Dv = Rfp * Dval(r, m, ix->Ifdl3) - Rfn * Dval(r, m, ix->Ifdl0) + Dval(r, m, ix->PhieE);
   double Upos = fUocp(r, ep, zk[ix->Thetass3], TK), Uneg = fUocp(r, en, zk[ix->Thetass0], TK);
-  double negEta0 = 2 * r->R * TK / r->F * asinh(zk[ix->If0] / (2 * i0n));
-  double posEta3 = 2 * r->R * TK / r->F * asinh(zk[ix->If3] / (2 * i0p));
+  double negEta0 = 2 * r->R * TK / r->F * dasinh(zk[ix->If0] / (2 * i0n));
+  double posEta3 = 2 * r->R * TK / r->F * dasinh(zk[ix->If3] / (2 * i0p));
   double b_phi = 0.01 * 0;
   L->bv = (Upos - Uneg) + (posEta3 - negEta0) + b_phi;
   L->bphi = fUocp(r, en, SOCnAvg, r->Tref); /* one-argument call */

@@ -1,10 +1,11 @@
 """GPU parity: the HIP path (through the C-ABI) against the C oracle.
 
 Tolerances.  The kernels evaluate the same defined operation order as
-oracle/mpcekf_oracle.c, so most quantities agree bit-for-bit; the only
-intended difference is asinh (device libm vs glibc, <= a few ulp).  Open-loop
-and short closed-loop checks therefore use rtol 1e-9; the north_star bar
-(1e-6 relative, BASELINE.json) is asserted on the 400-step closed loop.
+oracle/mpcekf_oracle.c (explicit fma, ascending sums from +0.0, asinh spelled
+out as dasinh/orc_asinh on both sides), so every comparison with the C oracle
+is BITWISE (NaN patterns included).  Against the numpy restatement's golden
+fixtures (LAPACK, libm asinh) the north_star bar 1e-6 relative applies, or
+1e-9 where the fixture stays well conditioned.
 """
 import numpy as np
 import pytest
@@ -40,12 +41,27 @@ def test_closed_loop_matches_oracle(rom, oc, M):
     soc0[0], tc[0] = 10.0, 25.0          # the golden runMPC.m cell
     ref = oc.run(rom, soc0, tc, steps, nthreads=8)
     out = M.runMPC(rom, soc0, tc, steps)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        _bitwise(out[k], ref[k], k)
+
+
+def _bitwise(a, b, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    same = (a == b) | (np.isnan(a) & np.isnan(b)) if a.dtype.kind == "f" else (a == b)
+    if not same.all():
+        i = np.argwhere(~same)[0]
+        raise AssertionError(f"{what}: {int((~same).sum())} entries differ, first at {tuple(i)}: "
+                             f"{a[tuple(i)]!r} vs {b[tuple(i)]!r} (max rel {_rel(a, b).max():.3e})")
+
+
+def _agree_steps(ref, g, rtol):
+    """Number of leading steps on which two trajectory sets agree to rtol (u, v, soc, phise)."""
+    bad = np.zeros(g["u"].shape[0], dtype=bool)
     for k in ("u", "v", "soc", "phise"):
-        r = _rel(out[k], ref[k])
-        assert r.max() <= RTOL_NORTH_STAR, (k, r.max(), np.unravel_index(r.argmax(), r.shape))
-    assert np.array_equal(out["nexec"], ref["nexec"])
-    # most of the horizon should in fact be (near) bit-identical
-    assert np.median(_rel(out["u"], ref["u"])) <= RTOL_TIGHT
+        r = _rel(ref[k], g[k])
+        bad |= (r > rtol).reshape(r.shape[0], -1).any(axis=1)
+    return int(np.argmax(bad)) if bad.any() else int(bad.shape[0])
 
 
 def test_lockout_and_error_cells(rom, oc, M):
@@ -58,9 +74,7 @@ def test_lockout_and_error_cells(rom, oc, M):
     assert np.array_equal(out["status"], ref["status"])
     assert (out["status"][[1, 3]] & 1).all()
     for k in ("u", "v", "soc", "phise"):
-        assert np.array_equal(np.isnan(out[k]), np.isnan(ref[k])), k
-        r = _rel(out[k], ref[k])
-        assert r.max() <= RTOL_TIGHT, (k, r.max())
+        _bitwise(out[k], ref[k], k)
 
 
 def test_stage_entry_points_match_fused(rom, M):
@@ -162,11 +176,8 @@ def test_zk_and_boundzk_match_oracle(rom, oc, M):
         ctx.init_cells(soc0, tc)
         ctx.step(steps)
         zk, zb = ctx.get_zk()
-    for nm, a, b in (("zk", zk, ref["zk"]), ("boundzk", zb, ref["zbk"])):
-        print(nm, "bit-exact" if np.array_equal(a, b, equal_nan=True) else "differs",
-              "max rel", _rel(a, b).max(), "entries differing", int(np.sum(a != b)))
-    assert _rel(zk, ref["zk"]).max() <= RTOL_TIGHT
-    assert _rel(zb, ref["zbk"]).max() <= RTOL_TIGHT
+    _bitwise(zk, ref["zk"], "zk")
+    _bitwise(zb, ref["zbk"], "boundzk")
 
 
 def test_checkpoint_restore_is_exact(rom, M):
@@ -183,11 +194,24 @@ def test_checkpoint_restore_is_exact(rom, M):
         np.testing.assert_array_equal(a[k], b[k])
 
 
-def test_runmpc_cell_prefix_matches_golden(rom, M):
+def test_runmpc_cell_full_charge(rom, oc, M):
+    """configs[0]: the runMPC.m cell (SOC0 = 10 %, 25 degC), all 3001 steps.
+
+    Bitwise against the C oracle over the whole charge.  Against the numpy golden
+    (LAPACK / libm arithmetic) within north_star's 1e-6 up to the step where the two
+    restatements themselves part: from ~2,900 on, hildreth.m runs into maxIter on
+    infeasible QPs every step and ulp-level differences grow to O(1)
+    (tests/test_oracle.py::test_tail_is_ill_conditioned shows a 1-ulp change of SOC0
+    does the same), so no implementation can be held to 1e-6 there."""
     g = _golden("runmpc_soc10_tc25")
     out = M.runMPC(rom, g["soc0"], g["tc"], 3001)
+    ref = oc.run(rom, g["soc0"], g["tc"], 3001, nthreads=1)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        _bitwise(out[k], ref[k], k)
+    agree = _agree_steps(ref, g, RTOL_NORTH_STAR)
+    assert agree >= 2900, agree
     for k in ("u", "v", "soc", "phise"):
-        assert _rel(out[k][:2400], g[k][:2400]).max() <= 1e-9, k
+        assert _rel(out[k][:agree], g[k][:agree]).max() <= RTOL_NORTH_STAR, k
 
 
 def test_deferred_time_update_is_schedule_invariant(rom, M):
@@ -276,9 +300,8 @@ def test_structured_hildreth_edge_paths_match_oracle(oc, M):
 @pytest.mark.parametrize("Np,Nc", [(5, 2), (20, 10)])
 def test_step_diagnostics_match_oracle(rom, oc, M, Np, Nc):
     """Every runMPC.m store per step (mpcekf_step_ex): x_store, zkEst, zkBound and
-    mpcData.cost (J_uncon, J_final, norm_DU, viol) against the oracle; the lock-out cell
-    gives NaN / 0 from its failing step on.  Tolerance as the short closed loops (1e-9:
-    asinh differs by ulps upstream); the integer viol count must match exactly."""
+    mpcData.cost (J_uncon, J_final, norm_DU, viol) against the oracle, bitwise; the
+    lock-out cell gives NaN / 0 from its failing step on."""
     n, steps = 24, 40
     soc0, tc = batch_inputs(n, seed=13)
     soc0[3] = 130.0  # lock-out
@@ -291,9 +314,7 @@ def test_step_diagnostics_match_oracle(rom, oc, M, Np, Nc):
         zk_last, zb_last = ctx.get_zk()
     pairs = dict(x="x", zk="zk_traj", zbk="zbk_traj", J_unc="J_unc", J_fin="J_fin", norm_du="norm_du")
     for k, rk in pairs.items():
-        assert np.array_equal(np.isnan(out[k]), np.isnan(ref[rk])), k
-        r = _rel(out[k], ref[rk])
-        assert r.max() <= RTOL_TIGHT, (k, r.max())
+        _bitwise(out[k], ref[rk], k)
     np.testing.assert_array_equal(out["nviol"], ref["nviol"])
     np.testing.assert_array_equal(out["nexec"], ref["nexec"])
     assert np.isnan(out["zk"][-1, 3]).all() and (out["nviol"][-1, 3] == 0)

@@ -2,10 +2,9 @@
 
 The wide MPC stage (mpcekf_wide.hip: k_mpc_wide, k_hild_wide 16-lane groups,
 k_hild_wide_slow, k_mpc_wide_finish) evaluates oracle/mpcekf_oracle.c's defined
-order, including the lane-tree row sums of hild_row_t, so the QP is bit-exact;
-asinh (device libm vs glibc) is the only intended difference upstream of it.
-Tolerances as in test_gpu_parity.py: 1e-9 on short runs, north_star's 1e-6 on
-the longer closed loop.
+order, including the lane-tree row sums of hild_row_t, and the plant/EKF
+upstream of it share the oracle's defined arithmetic (asinh included), so every
+comparison with the C oracle is bitwise.
 """
 import numpy as np
 import pytest
@@ -47,23 +46,35 @@ def test_wide_closed_loop_matches_oracle(rom, oc, M):
     ref = oc.run(rom, soc0, tc, steps, nthreads=8, Np=NP, Nc=NC)
     out = M.runMPC(rom, soc0, tc, steps, cfg=_cfg(M))
     np.testing.assert_array_equal(out["status"], ref["status"])
-    for k in ("u", "v", "soc", "phise"):
-        r = _rel(out[k], ref[k])
-        assert r.max() <= RTOL_NORTH_STAR, (k, r.max(), np.unravel_index(r.argmax(), r.shape))
-    assert np.array_equal(out["nexec"], ref["nexec"])
-    assert np.median(_rel(out["u"], ref["u"])) <= RTOL_TIGHT
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        assert np.array_equal(out[k], ref[k], equal_nan=k != "nexec"), k
+
+
+NEAR_SOC0 = np.array([88.0, 90.0, 93.0, 94.0, 94.5, 95.0, 96.0, 10.0, 50.0, 70.0, 80.0, 94.9, 95.1, 92.0, 25.0, 60.0])
+NEAR_TC = np.array([25.0, 22.0, 25.0, 20.0, 30.0, 25.0, 25.0, 25.0, 28.0, 21.0, 35.0, 15.0, 25.0, 33.0, 20.0, 26.0])
+
+
+def test_wide_closed_loop_near_limit(rom, oc, M):
+    """Cells started at 88-96 % SOC: hildreth.m runs into maxIter on most steps and the
+    zero G_soc row meets gamma <= 0 (the exact inf/NaN path, k_hild_wide_slow).  Closed
+    loop, 400 steps, bitwise against the oracle (round 1 could only check this open loop:
+    the plant's libm asinh made the chaotic maxIter regime diverge)."""
+    steps = 400
+    ref = oc.run(rom, NEAR_SOC0, NEAR_TC, steps, nthreads=8, Np=NP, Nc=NC)
+    out = M.runMPC(rom, NEAR_SOC0, NEAR_TC, steps, cfg=_cfg(M))
+    np.testing.assert_array_equal(out["status"], ref["status"])
+    assert (out["nexec"] == 100).sum() > steps  # the maxIter regime is really exercised
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        assert np.array_equal(out[k], ref[k], equal_nan=k != "nexec"), k
 
 
 def test_wide_mpc_stage_open_loop_near_limit(rom, oc, M):
-    """Cells started at 88-96 % SOC run hildreth.m into maxIter on every step, so closed
-    loops amplify the plant's asinh ulp differences chaotically (tools/diag_wide.py:
-    first divergence after ~30-270 steps).  The MPC stage itself is checked open loop:
+    """The MPC stage entry point on the near-limit cells, open loop:
     every step the GPU's own linearisation record, mpcData.uk_1 and warm start go
     through iterMPC on the GPU and in the oracle, which must agree bit for bit (uk,
     nexec, lambda).  Near the 95 % limit the zero G_soc row meets gamma <= 0, the
     exact inf/NaN path (k_hild_wide_slow)."""
-    soc0 = np.array([88.0, 90.0, 93.0, 94.0, 94.5, 95.0, 96.0, 10.0, 50.0, 70.0, 80.0, 94.9, 95.1, 92.0, 25.0, 60.0])
-    tc = np.array([25.0, 22.0, 25.0, 20.0, 30.0, 25.0, 25.0, 25.0, 28.0, 21.0, 35.0, 15.0, 25.0, 33.0, 20.0, 26.0])
+    soc0, tc = NEAR_SOC0, NEAR_TC
     n, steps = len(soc0), 120
     with M.Context(rom, n, _cfg(M)) as ctx:
         ctx.init_cells(soc0, tc)

@@ -243,3 +243,41 @@ def test_oracle_mpc_lin_matches_numpy_iter_mpc(rom, oc):
             assert ne_c[0] == info["nexec"], k
             lam_np = lam_in if mpc["lam"] is None else np.asarray(mpc["lam"], dtype=float)
             assert rel(lam_c[0], lam_np).max() <= 1e-9, k
+
+
+def test_defined_asinh_accuracy(oc):
+    """orc_asinh (= the kernels' dasinh spelling) is within 1 ulp of libm's asinh over
+    every branch (|x| < 2^-28, the log1p form, the log form, |x| > 2^28) and keeps
+    NaN / +-inf / signed zero."""
+    import ctypes
+    import math
+    f = oc.lib().orc_asinh
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_double]
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(-3, 3, 20000),
+                         10 ** rng.uniform(-12, 12, 20000) * rng.choice([-1, 1], 20000),
+                         [0.0, 2.0, -2.0, 2.0 ** 28, 2.0 ** -28, 1e300, -1e300, 5e-324]])
+    worst = 0.0
+    for x in xs:
+        a, b = f(float(x)), math.asinh(float(x))
+        worst = max(worst, abs(a - b) / math.ulp(b) if b else abs(a))
+    assert worst <= 1.0, worst
+    assert math.isnan(f(float("nan"))) and f(float("inf")) == float("inf") and f(-float("inf")) == -float("inf")
+    assert math.copysign(1.0, f(-0.0)) == -1.0
+
+
+def test_tail_is_ill_conditioned(rom, oc):
+    """Why the numpy golden is compared only up to step ~2,900 (test_gpu_parity.py::
+    test_runmpc_cell_full_charge): near the 95 % target hildreth.m runs into maxIter
+    on infeasible QPs and the closed loop amplifies ulps.  Moving SOC0 by 1e-15
+    relative (a few ulps) in the C oracle leaves the first 2,400 steps within 1e-9 and
+    then departs by more than 1e-6 before the end of the charge, as the two
+    restatements do."""
+    g = load("runmpc_soc10_tc25")
+    a = oc.run(rom, g["soc0"], g["tc"], 3001, nthreads=1)
+    b = oc.run(rom, g["soc0"] * (1 + 1e-15), g["tc"], 3001, nthreads=1)
+    r = rel(b["u"], a["u"])[:, 0]
+    assert r[:2400].max() <= 1e-9
+    assert r.max() > 1e-6
+    assert (a["nexec"][2400:] == 100).sum() > 100
