@@ -9,7 +9,11 @@ TC ~ U[20,30] degC (seed 0x5EED).  Multi-GPU: one process per GPU, cells sharded
 contiguously with no collective on the data path (weak scaling); the only
 collectives are the timing barrier and the max-over-ranks of the elapsed time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--cells-per-gpu C]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cells-per-gpu C | --total-cells T]
+
+--gpus N without torchrun starts N rank processes itself (one per GPU, before any
+GPU call); under torchrun the ranks come from RANK/WORLD_SIZE.  configs[3] is
+``--gpus 8 --total-cells 1048576`` (131 072 cells per GPU, strong scaling).
 """
 from __future__ import annotations
 
@@ -77,15 +81,62 @@ def batch_inputs(n, seed=0x5EED):
     return rng.uniform(5, 30, n), rng.uniform(20, 30, n)
 
 
+def shard_range(total, world, rank):
+    """Contiguous cell range [start, stop) of one rank (runMPC.m:83-112 has no cross-cell
+    term, so any split gives the same bits per cell)."""
+    base, rem = divmod(total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def cpu_threads_default():
+    """The host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS
+    (the GPU box sets it to its 16-CPU share; os.cpu_count() there is the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(rom, soc0, tc, cells, steps, threads, Np=5, Nc=2):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c
     t0 = time.perf_counter()
     oracle_c.run(rom, soc0[:cells], tc[:cells], steps, nthreads=threads, Np=Np, Nc=Nc)
     dt = time.perf_counter() - t0
+    # configs[0]: the runMPC.m cell (SOC0 10 %, 25 degC), the whole 3001-step charge on one core
+    t1 = time.perf_counter()
+    oracle_c.run(rom, np.array([10.0]), np.array([25.0]), 3001, nthreads=1, Np=Np, Nc=Nc)
+    d1 = time.perf_counter() - t1
     return dict(value=cells * steps / dt, unit="cell-steps/s", cores=threads, kind="port",
+                host_cpus=os.cpu_count(),
                 sample=f"C oracle (oracle/mpcekf_oracle.c, -O3 fp64, OpenMP) on the first {cells} cells "
-                       f"of the workload x {steps} steps from init, {threads} host threads, {dt:.1f} s")
+                       f"of the workload x {steps} steps from init, {threads} host threads of {os.cpu_count()} "
+                       f"logical CPUs, {dt:.1f} s",
+                configs0={"cells": 1, "steps": 3001, "cores": 1, "wall_s": d1, "steps_per_s": 3001 / d1,
+                          "what": "runMPC.m cell (SOC0 10 %, 25 degC), full charge, 1 thread"})
+
+
+def launch_ranks(args):
+    """--gpus N without torchrun: N worker processes, one per GPU, started before this
+    process touches the GPU; exits with the first failing rank's code."""
+    import socket
+    import subprocess
+    if not (args.dry_run or args.share_device):
+        import torch
+        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        if have < args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c]
+    sys.exit(bad[0] if bad else 0)
 
 
 def main():
@@ -93,101 +144,110 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--cells-per-gpu", type=int, default=65536)
+    ap.add_argument("--cells-per-gpu", type=int, default=65536, help="weak scaling (default)")
+    ap.add_argument("--total-cells", type=int, default=0,
+                    help="strong scaling: split this many cells over the ranks (configs[3]: 1048576 on 8)")
     ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
     ap.add_argument("--np", type=int, default=5, help="prediction horizon (configs[4]: 20)")
     ap.add_argument("--nc", type=int, default=2, help="control horizon (configs[4]: 10)")
     ap.add_argument("--cpu-cells", type=int, default=32768)
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="default: the cores this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="per-kernel HIP-event timing on every N-th step of the timed region (N | 32)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--share-device", action="store_true",
+                    help="all ranks on device 0 with gloo timing collectives (1-GPU multi-rank test)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: rank/shard/timing orchestration only (CPU tests)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
+    total = args.total_cells or args.cells_per_gpu * world
+    lo, hi = shard_range(total, world, rank)
+    ncell = hi - lo
+    device = 0 if args.share_device else local
     import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    P = importlib.import_module("mpc-ekf4fastcharge_amd")
-    M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
-    rom = P.make_synth_rom()
-    cpg = args.cells_per_gpu
-    total = cpg * world
-    soc0_all, tc_all = batch_inputs(total)
-    sl = slice(rank * cpg, (rank + 1) * cpg)
-    cfg = M.make_config(bounds=bool(args.bounds), Np=args.np, Nc=args.nc)
-    ncon = 4 * args.nc + 3 * args.np
-    ctx = M.Context(rom, cpg, cfg, device=local)
-    ctx.init_cells(soc0_all[sl], tc_all[sl])
-    dev = torch.device("cuda", local)
+        if args.dry_run or args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    print(f"bench.py rank {rank}/{world}: cells [{lo}, {hi}) ({ncell}) on "
+          f"{'no device (dry run)' if args.dry_run else f'cuda:{device}'}", file=sys.stderr, flush=True)
     K, W = args.steps, args.warmup
-    outs = [torch.empty((max(K, W), cpg), dtype=torch.float64, device=dev) for _ in range(4)]
-    nex = torch.empty((max(K, W), cpg), dtype=torch.int32, device=dev)
-    ptrs = [t.data_ptr() for t in outs] + [nex.data_ptr()]
-    if W:
-        ctx.step_device(W, *ptrs)
-    ctx.set_timing(args.timing_every)
-    ctx.get_timing()
+    coll_dev = torch.device("cpu") if (args.dry_run or args.share_device) else torch.device("cuda", device)
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize(torch.device("cuda", device))
+
+    if args.dry_run:
+        rom = None
+        soc0_all, tc_all = batch_inputs(total)
+        if dist:
+            dist.barrier()
+        t0 = time.perf_counter()
+        _ = soc0_all[lo:hi].sum() + tc_all[lo:hi].sum()
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        tim, nerr, mean_nexec, u_last = {}, 0, 0.0, np.zeros(0)
+    else:
+        P = importlib.import_module("mpc-ekf4fastcharge_amd")
+        M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
+        rom = P.make_synth_rom()
+        soc0_all, tc_all = batch_inputs(total)
+        cfg = M.make_config(bounds=bool(args.bounds), Np=args.np, Nc=args.nc)
+        ctx = M.Context(rom, ncell, cfg, device=device)
+        ctx.init_cells(soc0_all[lo:hi], tc_all[lo:hi])
+        dev = torch.device("cuda", device)
+        outs = [torch.empty((max(K, W), ncell), dtype=torch.float64, device=dev) for _ in range(4)]
+        nex = torch.empty((max(K, W), ncell), dtype=torch.int32, device=dev)
+        ptrs = [t.data_ptr() for t in outs] + [nex.data_ptr()]
+        if W:
+            ctx.step_device(W, *ptrs)
+        ctx.set_timing(args.timing_every)
+        ctx.get_timing()
+        sync()
+        if dist:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        ctx.step_device(K, *ptrs)
+        sync()
+        if dist:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        tim = ctx.get_timing()
+        status = ctx.get_state()["status"]
+        nerr = int((status & 1).sum())
+        u_last = outs[0][K - 1].double().cpu().numpy() if K else np.zeros(0)
+        mean_nexec = float(nex[:K].float().mean().item()) if K else 0.0
+        build_id = ctx.L.mpcekf_build_id().decode()
+        ctx.close()
     if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ctx.step_device(K, *ptrs)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    tim = ctx.get_timing()
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    status = ctx.get_state()["status"]
-    nerr = int((status & 1).sum())
-    u_last = outs[0][K - 1].double().cpu().numpy() if K else np.zeros(0)
-    mean_nexec = float(nex[:K].float().mean().item()) if K else 0.0
-    ctx.close()
+        t = torch.tensor([dt, float(nerr), mean_nexec * ncell], dtype=torch.float64, device=coll_dev)
+        dt_max = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(dt_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dt = float(dt_max.item())
+        nerr = int(t[1].item())
+        mean_nexec = float(t[2].item()) / total
 
     if rank == 0:
         cell_steps = total * K
         value = cell_steps / dt if dt > 0 else 0.0
-        bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
-        # HIP-event averages over the sampled launches (--timing-every); every flush step is
-        # sampled, so a kernel's share of a step is its average x its launches per step
-        n_flush = K // 32 + (1 if K % 32 else 0)
-        per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches_timed=tim[k][1],
-                              launches=(n_flush if k == "flush" else K))
-                      for k in tim if tim[k][1] > 0}
-        for v in per_kernel.values():
-            v["ms_total"] = v["ms_per_launch"] * v["launches"]
-        # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
-        dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
-        ms = per_kernel[dom]["ms_per_launch"]
-        achieved = bpc[dom] * cpg / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-        pmc = {}
-        if os.path.exists(args.pmc):
-            try:
-                pmc = json.load(open(args.pmc))
-            except Exception:
-                pmc = {}
-        traffic = pmc.get("per_launch_bytes", {}).get(dom)
-        flops = pmc.get("fp64_flops_per_launch", {}).get(dom)
-        fp64 = None
-        if flops and ms > 0:
-            tf = flops / (ms * 1e-3) / 1e12
-            fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                    "flops_per_launch": flops, "source": os.path.relpath(args.pmc, ROOT)}
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, cpg), args.cpu_steps or (W + K),
-                               args.cpu_threads, Np=args.np, Nc=args.nc)
         line = {
             "metric": METRIC,
             "value": value,
@@ -197,40 +257,95 @@ def main():
             "warmup": W,
             "ms_per_step": dt / K * 1e3 if K else 0.0,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_cells else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (synthetic NMC30-like ROM; SOC0~U[5,30]%, TC~U[20,30]C, seed 0x5EED)",
             "config": {
-                "workload": f"{cpg} cells per GPU ({total} total), Np={args.np} Nc={args.nc}, closed loop runMPC.m:84-111 "
-                            f"incl. plant, boundzk={'on' if args.bounds else 'off'}",
-                "cells_per_gpu": cpg, "total_cells": total, "Np": args.np, "Nc": args.nc, "models_per_cell": rom.NM,
-                "rom_outputs": rom.nz, "parallelism": f"cell-shard x{world} (no data-path collective)",
+                "workload": f"{total} cells ({shard_range(total, world, 0)[1]} on rank 0), Np={args.np} Nc={args.nc}, "
+                            f"closed loop runMPC.m:84-111 incl. plant, boundzk={'on' if args.bounds else 'off'}",
+                "total_cells": total, "cells_per_gpu": [shard_range(total, world, r)[1] - shard_range(total, world, r)[0]
+                                                        for r in range(world)],
+                "Np": args.np, "Nc": args.nc, "models_per_cell": rom.NM if rom else None,
+                "rom_outputs": rom.nz if rom else None,
+                "parallelism": f"cell-shard x{world} (no data-path collective)",
+                "step_window": [W, W + K], "mean_nexec": round(mean_nexec, 3),
             },
-            "roofline": {
-                "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "algorithmic_bytes_per_cell": bpc[dom],
-                "fp64": fp64,
-                "step_equivalent": {
-                    "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, ncon),
-                    "achieved": value * survey_bytes_per_cell_step(rom.NM, ncon) / 1e9, "unit": "GB/s",
-                    "note": "SURVEY.md 8(d): whole-step state r+w per cell-step x cell-steps/s",
-                },
-            },
-            "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
-                                launches_timed=v["launches_timed"],
-                                ms_per_step=round(v["ms_total"] / K, 5) if K else None,
-                                gbs_algorithmic=round(bpc[k] * cpg / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
-                                if v["ms_per_launch"] > 0 else None)
-                        for k, v in per_kernel.items()},
-            "cpu_baseline": cpu,
-            "checks": {"cells_in_error": nerr, "mean_nexec": round(mean_nexec, 3),
-                       "u_last_mean": float(np.nanmean(u_last)) if u_last.size else None},
         }
-        print(json.dumps(line), flush=True)
+        if args.dry_run:
+            line["dry_run"] = True
+            line["value"] = None
+            print(json.dumps(line), flush=True)
+        else:
+            line.update(report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id,
+                               soc0_all, tc_all, world))
+            print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, soc0_all, tc_all, world):
+    """Rank 0's roofline / per-kernel / CPU-baseline objects (rank 0's shard timings)."""
+    ncon = 4 * args.nc + 3 * args.np
+    bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
+    # HIP-event averages over the sampled launches (--timing-every); every flush step is
+    # sampled, so a kernel's share of a step is its average x its launches per step
+    n_flush = K // 32 + (1 if K % 32 else 0)
+    per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches_timed=tim[k][1],
+                          launches=(n_flush if k == "flush" else K))
+                  for k in tim if tim[k][1] > 0}
+    for v in per_kernel.values():
+        v["ms_total"] = v["ms_per_launch"] * v["launches"]
+    # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
+    ms = per_kernel[dom]["ms_per_launch"]
+    achieved = bpc[dom] * ncell / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    pmc = {}
+    if os.path.exists(args.pmc):
+        try:
+            with open(args.pmc) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            pmc = {}
+    pmc_ok = pmc.get("build_id") == build_id and pmc.get("cells") == ncell and \
+        pmc.get("Np", 5) == args.np and pmc.get("bounds", 1) == args.bounds
+    traffic = pmc.get("per_launch_bytes", {}).get(dom) if pmc_ok else None
+    flops = pmc.get("fp64_flops_per_launch", {}).get(dom) if pmc_ok else None
+    fp64 = None
+    if flops and ms > 0:
+        tf = flops / (ms * 1e-3) / 1e12
+        fp64 = {"achieved": tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                "flops_per_launch": flops, "source": os.path.relpath(args.pmc, ROOT)}
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(rom, soc0_all, tc_all, min(args.cpu_cells, ncell), args.cpu_steps or (args.warmup + K),
+                           args.cpu_threads or cpu_threads_default(), Np=args.np, Nc=args.nc)
+    return {
+        "roofline": {
+            "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_source": (os.path.relpath(args.pmc, ROOT) if traffic is not None else
+                               f"null: {os.path.relpath(args.pmc, ROOT)} was not measured on this build "
+                               f"({build_id}) and workload"),
+            "algorithmic_bytes_per_cell": bpc[dom], "cells_per_launch": ncell,
+            "fp64": fp64,
+            "step_equivalent": {
+                "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, ncon),
+                "achieved": value * survey_bytes_per_cell_step(rom.NM, ncon) / 1e9, "unit": "GB/s",
+                "note": "notional: SURVEY.md 8(d) eager-algorithm bytes x cell-steps/s; the deferred time "
+                        "update does not move these bytes every step, so this is not achieved bandwidth",
+            },
+        },
+        "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
+                            launches_timed=v["launches_timed"],
+                            ms_per_step=round(v["ms_total"] / K, 5) if K else None,
+                            gbs_algorithmic=round(bpc[k] * ncell / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
+                            if v["ms_per_launch"] > 0 else None)
+                    for k, v in per_kernel.items()},
+        "cpu_baseline": cpu,
+        "checks": {"cells_in_error": nerr, "mean_nexec": round(mean_nexec, 3), "build_id": build_id,
+                   "u_last_mean_rank0": float(np.nanmean(u_last)) if u_last.size else None},
+    }
 
 
 if __name__ == "__main__":

@@ -127,6 +127,9 @@ typedef struct {
 typedef struct mpcekf_ctx mpcekf_ctx;
 
 int mpcekf_abi_version(void);
+/* sha256 prefix of the sources this library was built from (profiles record the one
+ * they were measured on; bench.py refuses stale PMC figures). */
+const char *mpcekf_build_id(void);
 const char *mpcekf_last_error(void);
 void mpcekf_config_defaults(mpcekf_config *cfg); /* the runMPC.m values */
 

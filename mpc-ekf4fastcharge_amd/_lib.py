@@ -70,6 +70,7 @@ EXPORTS = [
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
+    "mpcekf_build_id",
 ]
 
 _lib = None
@@ -86,6 +87,7 @@ def load():
     vp = C.c_void_p
     L.mpcekf_abi_version.restype = C.c_int
     L.mpcekf_last_error.restype = C.c_char_p
+    L.mpcekf_build_id.restype = C.c_char_p
     L.mpcekf_config_defaults.argtypes = [C.POINTER(Config)]
     L.mpcekf_config_defaults.restype = None
     L.mpcekf_ctx_create.argtypes = [C.POINTER(Rom), C.POINTER(Config), C.c_int, C.c_int64, C.POINTER(vp)]
@@ -113,7 +115,7 @@ def load():
     L.mpcekf_hildreth_structured.argtypes = [C.c_int, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int32,
                                              C.c_double, _dp, _ip]
     for nm in EXPORTS:
-        if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults"):
+        if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_build_id"):
             getattr(L, nm).restype = C.c_int
     if L.mpcekf_abi_version() != 1:
         raise MpcekfError("ABI version mismatch")

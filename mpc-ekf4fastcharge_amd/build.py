@@ -6,6 +6,7 @@ semantics are part of the reference behaviour, SURVEY.md §7 hard part 3).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import subprocess
 import sys
@@ -30,8 +31,19 @@ def _mtime(p):
 
 
 def _stale(obj, src):
-    newest = max([_mtime(src)] + [_mtime(os.path.join(SRC, d)) for d in DEPS])
+    deps = DEPS + (SOURCES if os.path.basename(src) == "mpcekf_host.cpp" else [])  # it embeds the source hash
+    newest = max([_mtime(src)] + [_mtime(os.path.join(SRC, d)) for d in deps])
     return _mtime(obj) < newest
+
+
+def source_hash():
+    """sha256 (16 hex) over the kernel/host sources and headers: the library reports it
+    (mpcekf_build_id) and profiles/pmc_traffic.json records the one it was measured on."""
+    h = hashlib.sha256()
+    for f in sorted(SOURCES + DEPS):
+        with open(os.path.join(SRC, f), "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 def build(force=False, verbose=False, variant=""):
@@ -41,6 +53,7 @@ def build(force=False, verbose=False, variant=""):
     objs = []
     sfx = f"_{variant}" if variant else ""
     extra = ["-DMPCEKF_STAMPS"] if variant == "stamps" else []
+    extra.append(f'-DMPCEKF_SRC_HASH="{source_hash()}"')
     lib = os.path.join(OUT, f"libmpcekf{sfx}.so")
     for s in SOURCES:
         src = os.path.join(SRC, s)

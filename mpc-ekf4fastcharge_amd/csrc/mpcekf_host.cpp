@@ -111,6 +111,11 @@ extern "C" {
 
 int mpcekf_abi_version(void) { return MPCEKF_ABI_VERSION; }
 
+#ifndef MPCEKF_SRC_HASH
+#define MPCEKF_SRC_HASH "unknown"
+#endif
+const char *mpcekf_build_id(void) { return MPCEKF_SRC_HASH; }
+
 const char *mpcekf_last_error(void) { return g_err.c_str(); }
 
 void mpcekf_config_defaults(mpcekf_config *c) {

@@ -48,3 +48,12 @@ def test_last_error_is_empty_string_initially(P):
     from importlib import import_module
     L = import_module("mpc-ekf4fastcharge_amd._lib").load()
     assert isinstance(L.mpcekf_last_error(), bytes)
+
+
+def test_build_id_is_the_source_hash(P):
+    """The library embeds the hash of the sources it was built from (build.py source_hash);
+    bench.py attaches PMC traffic only when profiles/pmc_traffic.json was measured on it."""
+    from importlib import import_module
+    L = import_module("mpc-ekf4fastcharge_amd._lib").load()
+    b = import_module("mpc-ekf4fastcharge_amd.build")
+    assert L.mpcekf_build_id().decode() == b.source_hash()

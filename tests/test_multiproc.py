@@ -23,16 +23,19 @@ def _worker(rank, world, port, cpg, steps, q):
     import oracle_c
     P = importlib.import_module("mpc-ekf4fastcharge_amd")
     rom = P.make_synth_rom()
-    soc0, tc = bench.batch_inputs(cpg * world)
-    sl = slice(rank * cpg, (rank + 1) * cpg)
-    out = oracle_c.run(rom, soc0[sl], tc[sl], steps, nthreads=1)
+    soc0, tc = bench.batch_inputs(cpg * world - 5)       # ragged: shards of 22 and 21 cells
+    lo, hi = bench.shard_range(cpg * world - 5, world, rank)
+    out = oracle_c.run(rom, soc0[lo:hi], tc[lo:hi], steps, nthreads=1)
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)       # bench.py's max-over-ranks timing
-    u = torch.from_numpy(np.ascontiguousarray(out["u"]))
+    u = torch.zeros((steps, cpg), dtype=torch.float64)
+    u[:, :hi - lo] = torch.from_numpy(np.ascontiguousarray(out["u"]))
     gathered = [torch.empty_like(u) for _ in range(world)]
     dist.all_gather(gathered, u)
     if rank == 0:
-        q.put((float(t.item()), torch.cat(gathered, dim=1).numpy()))
+        parts = [g[:, :b - a] for g, (a, b) in zip(gathered, [bench.shard_range(cpg * world - 5, world, r)
+                                                                for r in range(world)])]
+        q.put((float(t.item()), torch.cat(parts, dim=1).numpy()))
     dist.destroy_process_group()
 
 
@@ -50,7 +53,7 @@ def test_two_rank_shards_equal_single_process(oc, rom):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert tmax == 2.0
-    soc0, tc = bench.batch_inputs(cpg * world)
+    soc0, tc = bench.batch_inputs(cpg * world - 5)
     single = oc.run(rom, soc0, tc, steps, nthreads=2)
     np.testing.assert_array_equal(u_sharded, single["u"])
 
@@ -62,3 +65,57 @@ def test_bench_algorithmic_bytes():
     # 416*NM state bytes, + model timestamps and the two input rings
     assert b["flush"] == 416 * 63 + 2 * 2 * 4 * 63 + 2 * 8 * 32
     assert bench.survey_bytes_per_cell_step(63, 23) == 26736
+
+
+def test_shard_ranges_cover_the_batch():
+    sys.path.insert(0, ROOT)
+    import bench
+    for total in (0, 1, 7, 1024, 1048576, 1048579):
+        for world in (1, 2, 3, 8):
+            r = [bench.shard_range(total, world, k) for k in range(world)]
+            assert r[0][0] == 0 and r[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+            sizes = [b - a for a, b in r]
+            assert max(sizes) - min(sizes) <= 1
+    assert bench.shard_range(1048576, 8, 3) == (3 * 131072, 4 * 131072)   # configs[3]
+
+
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       env=e, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return lines[0], r.stderr
+
+
+@pytest.mark.parametrize("gpus,extra,total,per", [
+    (2, [], 131072, [65536, 65536]),
+    (3, ["--cells-per-gpu", "1000"], 3000, [1000, 1000, 1000]),
+    (8, ["--total-cells", "1048576"], 1048576, [131072] * 8),     # configs[3]
+    (3, ["--total-cells", "1000"], 1000, [334, 333, 333]),
+])
+def test_bench_spawns_ranks_over_gloo(gpus, extra, total, per):
+    """bench.py --gpus N without torchrun starts N rank processes (here with --dry-run:
+    gloo collectives, no GPU); each prints its contiguous cell range, rank 0 prints the
+    one JSON line with n_gpus = N and the whole-job cell count."""
+    line, err = _bench("--gpus", str(gpus), "--dry-run", "--steps", "3", *extra)
+    assert line["n_gpus"] == gpus and line["dry_run"] is True
+    assert line["config"]["total_cells"] == total and line["config"]["cells_per_gpu"] == per
+    assert line["scaling"] == ("strong" if "--total-cells" in extra else "weak")
+    for r in range(gpus):
+        assert f"rank {r}/{gpus}: cells [" in err
+
+
+def test_bench_refuses_world_size_mismatch():
+    import subprocess
+    e = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, env=e, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

@@ -39,10 +39,22 @@ def read_counter(d, name):
 
 
 def main():
-    base = sys.argv[1]
+    import argparse
+    import importlib
+    ap = argparse.ArgumentParser()
+    ap.add_argument("base")
+    ap.add_argument("--cells", type=int, default=65536)
+    ap.add_argument("--np", type=int, default=5)
+    ap.add_argument("--bounds", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    a = ap.parse_args()
+    base = a.base
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    L = importlib.import_module("mpc-ekf4fastcharge_amd._lib").load()
     fetch = read_counter(os.path.join(base, "fetch"), "FETCH_SIZE")
     write = read_counter(os.path.join(base, "write"), "WRITE_SIZE")
-    out = {"unit": "bytes per launch", "fetch_kib_raw": fetch, "write_kib_raw": write,
+    out = {"unit": "bytes per launch", "build_id": L.mpcekf_build_id().decode(), "cells": a.cells, "Np": a.np,
+           "bounds": a.bounds, "steps": a.steps, "fetch_kib_raw": fetch, "write_kib_raw": write,
            "correction": "reads x2 (gfx950 FETCH_SIZE halves 16-B/lane streaming reads)",
            "per_launch_bytes": {}}
     for k in set(fetch) | set(write):
