@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPCEKF_ABI_VERSION 1
+#define MPCEKF_ABI_VERSION 2
 
 /* return codes */
 #define MPCEKF_OK 0
@@ -65,16 +65,24 @@ enum {
   MPCEKF_TF_COUNT
 };
 
-/* One electrode of cellData.function.* in tabulated form (see DESIGN.md "ROM").
- *   soc(z)       = theta0 + z*(theta100-theta0)
- *   Uocp(th,T)   = interp(U,th) + (T-Tref)*interp(dUdT,th)   (1-arg call: T = Tref)
- *   dUocp(th)    = interp(dU,th)
- *   k0(th,T)     = k0ref*exp(Ea_k0/R*(1/Tref-1/T))
- *   Rf, wDL, Cdl, nDL constants; interp = piecewise linear on a uniform grid over [0,1]. */
+/* One electrode's cellData.function.{neg,pos} handles in tabulated form.
+ * The 2-D tables are [ntemp][ntheta] (row j = the handle at T = rom.tab_T_K[j] over a
+ * uniform theta grid on [0, 1]) and are evaluated by the defined bilinear interpolation
+ * (theta clamped to [0, 1], T clamped to the grid ends; ntemp == 1: theta only):
+ *   soc(z,T)     = soc0(T) + z*(soc100(T) - soc0(T))   iterEKF.m:282-283,439-440,497-498;
+ *                                                      EKFmatsHandler.m:57-58; OB_step.m:64-65
+ *   Uocp(th,T)   = Uocp       OB_step.m:313-314,337-338; iterEKF.m:362-363,404-405; EKFmatsHandler.m:84-85
+ *   Uocp(th)     = Uocp1      the one-argument call, EKFmatsHandler.m:96
+ *   dUocp(th,T)  = dUocp      OB_step.m:231-232; iterEKF.m:495-496,579-580
+ *   k0(th,T)     = k0         OB_step.m:329-330; iterEKF.m:392-393,463-464; EKFmatsHandler.m:60-61
+ *   Rf(th,T)     = Rf         OB_step.m:339-340; iterEKF.m:406-407,441-442; EKFmatsHandler.m:68-69
+ *   Cdl(th,T)^(2-nDL) * wDL(th,T)^(nDL-1) = Cdleff, read at th = SOC0n/p (OB_step.m:212-219)
+ * theta0/theta100 are the zero-argument calls the plant makes (OB_step.m:207-210). */
 typedef struct {
-  double theta0, theta100, Rf, k0ref, Ea_k0, wDL, Cdl, nDL;
-  int32_t ntab;
-  const double *U, *dUdT, *dU; /* [ntab] each */
+  double theta0, theta100;
+  const double *soc0, *soc100;                 /* [ntemp] soc(0,T), soc(1,T)       */
+  const double *Uocp, *dUocp, *k0, *Rf, *Cdleff; /* [ntemp][ntheta] each            */
+  const double *Uocp1;                         /* [ntheta]                         */
 } mpcekf_electrode;
 
 /* The ROM struct of runMPC.m:5 as plain arrays.  Set-points ascending. */
@@ -91,6 +99,9 @@ typedef struct {
   const int32_t *tf_code;  /* [nz] MPCEKF_TF_*   tfData.names                      */
   const double *tf_xloc;   /* [nz]               tfData.xLoc                       */
   double F, R, Q, Rc, Tref;
+  int32_t tab_ntheta;      /* theta grid points of the electrode tables (>= 2)     */
+  int32_t tab_ntemp;       /* temperature grid points (>= 1)                       */
+  const double *tab_T_K;   /* [tab_ntemp] ascending, Kelvin                        */
   mpcekf_electrode neg, pos;
 } mpcekf_rom;
 
@@ -139,15 +150,19 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
 int mpcekf_ctx_destroy(mpcekf_ctx *ctx);
 int mpcekf_ctx_info(const mpcekf_ctx *ctx, int64_t *ncells, int32_t *nmodels, int32_t *nz, int32_t *ncon);
 
-/* initKF + initMPC + OB_step first call for every cell: SOC0 in percent, Tc in degC. */
+/* initKF + initMPC + OB_step first call for every cell: SOC0 in percent, Tc in degC
+ * (the cell temperature until a call passes another one). */
 int mpcekf_init_cells(mpcekf_ctx *ctx, const double *soc0_pct, const double *tc_degC);
 
-/* nsteps fused closed-loop steps.  Each output may be NULL; non-NULL outputs are
- * [nsteps][ncells] host arrays (or device arrays when outputs_on_device != 0):
+/* nsteps fused closed-loop steps.  tc_degC is the temperature runMPC.m:85-92 passes to
+ * OB_step, iterEKF and EKFmatsHandler at each step, [nsteps][ncells] in degC, or NULL to
+ * keep every cell's current temperature.  Each output may be NULL; non-NULL outputs are
+ * [nsteps][ncells] host arrays (or device arrays when outputs_on_device != 0, which
+ * then also applies to tc_degC):
  *   traj_u = u_store (MPC command), traj_v = voltage_store, traj_soc = SOC_store
  *   (zk(end)), traj_phise = phise_store, traj_nexec = mpcData.cost.nexec. */
-int mpcekf_step(mpcekf_ctx *ctx, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
-                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device);
+int mpcekf_step(mpcekf_ctx *ctx, int32_t nsteps, const double *tc_degC, double *traj_u, double *traj_v,
+                double *traj_soc, double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device);
 
 /* Per-step outputs of mpcekf_step_ex (runMPC.m:55-69 stores, filled at runMPC.m:94-111
  * and iterMPC.m:89-95).  Every pointer may be NULL.  Step-major arrays, host pointers
@@ -164,22 +179,25 @@ typedef struct {
   double *J_unc, *J_fin, *norm_du; /* mpcData.cost.J_uncon / J_final / norm_DU          */
   int32_t *nviol;                  /* mpcData.cost.viol                                 */
 } mpcekf_traj;
-int mpcekf_step_ex(mpcekf_ctx *ctx, int32_t nsteps, const mpcekf_traj *traj, int32_t outputs_on_device);
+int mpcekf_step_ex(mpcekf_ctx *ctx, int32_t nsteps, const double *tc_degC, const mpcekf_traj *traj,
+                   int32_t outputs_on_device);
 
 /* Optional per-step EKF output of the LAST mpcekf_step call: zk and boundzk
  * ([ncells][nz+2], boundzk only with MPCEKF_CF_BOUNDS). */
 int mpcekf_get_zk(mpcekf_ctx *ctx, double *zk, double *boundzk);
 
-/* ---- stage entry points (one MATLAB function each; all batched over cells) ---- */
-/* OB_step: applies iapp[c] to the plant state, returns vcell[c]. */
-int mpcekf_plant_step(mpcekf_ctx *ctx, const double *iapp, double *vcell);
+/* ---- stage entry points (one MATLAB function each; all batched over cells) ----
+ * The temperature argument (Tc of OB_step.m:1, Tk of iterEKF.m:30 / EKFmatsHandler.m:1,
+ * degC, [ncells]) sets each cell's temperature for this and later calls; NULL keeps it. */
+/* OB_step: applies iapp[c] to the plant state at tc_degC[c], returns vcell[c]. */
+int mpcekf_plant_step(mpcekf_ctx *ctx, const double *iapp, const double *tc_degC, double *vcell);
 /* iterEKF: zk/boundzk [ncells][nz+2] (boundzk may be NULL), xind_model [ncells][4]
  * (model index t*nZ+z of Xind.theT/theZ), xind_gamma [ncells][4]. */
-int mpcekf_ekf_step(mpcekf_ctx *ctx, const double *vk, const double *ik, double *zk, double *boundzk,
-                    int32_t *xind_model, double *xind_gamma);
+int mpcekf_ekf_step(mpcekf_ctx *ctx, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                    double *boundzk, int32_t *xind_model, double *xind_gamma);
 /* EKFmatsHandler: lin [ncells][MPCEKF_LIN_SIZE]. */
 int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_model, const double *xind_gamma,
-                     double *lin);
+                     const double *tk_degC, double *lin);
 /* iterMPC (uses and updates the context's uk_1 and lambda warm start):
  * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec. */
 int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);

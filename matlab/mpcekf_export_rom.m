@@ -1,38 +1,47 @@
-function mpcekf_export_rom(matFile, jsonFile, ntab)
+function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
 % MPCEKF_EXPORT_ROM  Tabulate a reference ROM (.mat) into the JSON file the MI355X
-% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py).
+% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py, format v2).
 %
-%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json')        % 201-point tables
-%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json', 401)
+%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json')          % 101 x 6 tables
+%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json', 201, [15 25 35])
 %
 % Runs on a machine with MATLAB and the reference's ROM file (runMPC.m:4-5; the file
-% is listed in .MISSING_LARGE_BLOBS:1 and is not in this repository).  The
-% cellData.function handles are called exactly as the hot path calls them:
-%   soc(z,T)       OB_step.m:231-232, iterEKF.m:282-283
-%   Uocp(theta,T)  iterEKF.m:362-363, EKFmatsHandler.m:96 (1-arg call -> Tref)
-%   dUocp(theta,T) iterEKF.m:392-407, EKFmatsHandler.m:53-92
-%   k0(theta,T), Rf(theta,T), wDL(theta,T), Cdl(theta,T), nDL(), theta0(), theta100()
-%                  OB_step.m:205-219, 313-314, 329-340
-%   const.Q(), const.Rc()                      initMPC.m:66-67, OB_step.m:206
-% and tabulated into the library's electrode model (include/mpcekf.h, mpcekf_electrode):
-%   U(theta)    = Uocp(theta,Tref)             on ntab uniform points over [0,1]
-%   dUdT(theta) = Uocp(theta,Tref+1) - Uocp(theta,Tref)   (per kelvin)
-%   dU(theta)   = dUocp(theta,Tref)
-%   k0(theta,T) = k0ref*exp(Ea_k0/R*(1/Tref-1/T)), Ea_k0 fitted from Tref and Tref+10
-%   Rf, wDL, Cdl at theta = 0.5, T = Tref (the reference uses them as cell constants,
-%   OB_step.m:313-314 evaluates wDL/Cdl at SOC0 only)
-% The approximation error of the tables is reported by mpcekf_check_tables below.
+% is listed in .MISSING_LARGE_BLOBS:1 and is not in this repository).  Every
+% cellData.function handle the hot path calls is evaluated on a (T, theta) grid --
+% TdegC (default: 6 points from 10 degC below the coldest to 10 degC above the warmest
+% ROM set-point) x ntheta uniform points over [0, 1] -- and written as the library's
+% [ntemp][ntheta] tables (include/mpcekf.h, mpcekf_electrode):
+%   Uocp(theta,T)   OB_step.m:313-314,337-338; iterEKF.m:362-363,404-405; EKFmatsHandler.m:84-85
+%   Uocp(theta)     the one-argument call of EKFmatsHandler.m:96 (its own 1-D table)
+%   dUocp(theta,T)  OB_step.m:231-232; iterEKF.m:495-496,579-580
+%   k0(theta,T)     OB_step.m:329-330; iterEKF.m:392-393,463-464; EKFmatsHandler.m:60-61
+%   Rf(theta,T)     OB_step.m:339-340; iterEKF.m:406-407,441-442; EKFmatsHandler.m:68-69
+%   Cdleff(theta,T) = Cdl(theta,T)^(2-nDL) * wDL(theta,T)^(nDL-1)   OB_step.m:212-219
+%   soc(0,T), soc(1,T)   soc(z,T) is taken as linear in z (checked)  iterEKF.m:282-283
+%   theta0(), theta100(), const.Q(), const.Rc()     OB_step.m:205-210, initMPC.m:66-67
+% The library evaluates the tables with a defined bilinear interpolation (theta, then
+% T; both clamped to the grid).  mpcekf_check_tables reports how far that is from the
+% handles between the grid points: the part of a real-MATLAB parity gap that comes from
+% tabulation rather than the kernels.  LDS budget: the kernels stage 4 (plant: 5) of
+% the tables per electrode next to the ROM models, so ntheta x ntemp is bounded
+% (mpcekf_ctx_create fails with MPCEKF_E_UNSUPPORTED when they do not fit 160 KiB).
 %
 % Every array is written as {"shape": size(X), "order": "F", "data": X(:)'} so the
 % loader needs no knowledge of MATLAB's N-D jsonencode nesting.
-  if nargin < 3, ntab = 201; end
+  if nargin < 3 || isempty(ntheta), ntheta = 101; end
   S = load(matFile);
   if isfield(S, 'ROM'), ROM = S.ROM; else, f = fieldnames(S); ROM = S.(f{1}); end
   cd = ROM.cellData;  fn = cd.function;  Tref = 298.15;
-  th = linspace(0, 1, ntab);
+  if nargin < 4 || isempty(TdegC)
+    TdegC = linspace(min(ROM.xraData.T) - 10, max(ROM.xraData.T) + 10, 6);
+  end
+  assert(numel(TdegC) >= 1 && numel(TdegC) <= 8 && all(diff(TdegC) > 0), ...
+         'mpcekf_export_rom: 1..8 ascending table temperatures');
+  TK = TdegC(:)' + 273.15;
+  th = linspace(0, 1, ntheta);
 
   out = struct();
-  out.format = 'mpcekf-rom-v1';
+  out.format = 'mpcekf-rom-v2';
   out.source = matFile;
   out.T_degC = arr(ROM.xraData.T(:)');
   out.SOC_pct = arr(ROM.xraData.SOC(:)');
@@ -43,10 +52,11 @@ function mpcekf_export_rom(matFile, jsonFile, ntab)
   out.xloc = arr(xloc(:)');
   out.F = cd.const.F;  out.R = cd.const.R;
   out.Q = fn.const.Q();  out.Rc = fn.const.Rc();  out.Tref = Tref;
-  out.neg = electrode(fn.neg, th, Tref, cd.const.R);
-  out.pos = electrode(fn.pos, th, Tref, cd.const.R);
-  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, out.neg, Tref, cd.const.R), ...
-                         'pos', mpcekf_check_tables(fn.pos, out.pos, Tref, cd.const.R));
+  out.tab_T_K = arr(TK);
+  out.neg = electrode(fn.neg, th, TK);
+  out.pos = electrode(fn.pos, th, TK);
+  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, out.neg, th, TK), ...
+                         'pos', mpcekf_check_tables(fn.pos, out.pos, th, TK));
 
   fid = fopen(jsonFile, 'w');
   assert(fid > 0, 'mpcekf_export_rom: cannot open %s', jsonFile);
@@ -54,17 +64,28 @@ function mpcekf_export_rom(matFile, jsonFile, ntab)
   fclose(fid);
 end
 
-function e = electrode(f, th, Tref, R)
+function e = electrode(f, th, TK)
+  nt = numel(TK);  nth = numel(th);
   e = struct();
   e.theta0 = f.theta0();  e.theta100 = f.theta100();
-  e.Rf = f.Rf(0.5, Tref);
-  e.k0ref = f.k0(0.5, Tref);
-  e.Ea_k0 = R * log(f.k0(0.5, Tref + 10) / e.k0ref) / (1/Tref - 1/(Tref + 10));
-  e.wDL = f.wDL(0.5, Tref);  e.Cdl = f.Cdl(0.5, Tref);  e.nDL = f.nDL();
-  U = arrayfun(@(t) f.Uocp(t, Tref), th);
-  e.U = arr(U);
-  e.dUdT = arr(arrayfun(@(t) f.Uocp(t, Tref + 1), th) - U);
-  e.dU = arr(arrayfun(@(t) f.dUocp(t, Tref), th));
+  e.soc0 = arr(arrayfun(@(T) f.soc(0, T), TK));
+  e.soc100 = arr(arrayfun(@(T) f.soc(1, T), TK));
+  [U, dU, K0, RF, CDL] = deal(zeros(nt, nth));
+  nDL = f.nDL();
+  for j = 1:nt
+    T = TK(j);
+    U(j, :) = arrayfun(@(t) f.Uocp(t, T), th);
+    dU(j, :) = arrayfun(@(t) f.dUocp(t, T), th);
+    K0(j, :) = arrayfun(@(t) f.k0(t, T), th);
+    RF(j, :) = arrayfun(@(t) f.Rf(t, T), th);
+    CDL(j, :) = arrayfun(@(t) f.Cdl(t, T)^(2 - nDL) * f.wDL(t, T)^(nDL - 1), th);
+  end
+  e.Uocp = arr(U);  e.dUocp = arr(dU);  e.k0 = arr(K0);  e.Rf = arr(RF);  e.Cdleff = arr(CDL);
+  try
+    e.Uocp1 = arr(arrayfun(@(t) f.Uocp(t), th));         % EKFmatsHandler.m:96, one argument
+  catch
+    e.Uocp1 = arr(arrayfun(@(t) f.Uocp(t, 298.15), th)); % a handle that needs T: Tref
+  end
 end
 
 function a = arr(X)

@@ -26,17 +26,16 @@ _ip = C.POINTER(C.c_int32)
 
 
 class Electrode(C.Structure):
-    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("Rf", C.c_double),
-                ("k0ref", C.c_double), ("Ea_k0", C.c_double), ("wDL", C.c_double), ("Cdl", C.c_double),
-                ("nDL", C.c_double), ("ntab", C.c_int32), ("U", _dp), ("dUdT", _dp), ("dU", _dp)]
+    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
+                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp)]
 
 
 class Rom(C.Structure):
     _fields_ = [("nT", C.c_int32), ("nZ", C.c_int32), ("n", C.c_int32), ("nz", C.c_int32),
                 ("T_degC", _dp), ("SOC_pct", _dp), ("Ts", C.c_double), ("A", _dp), ("C", _dp),
                 ("D", _dp), ("tf_code", _ip), ("tf_xloc", _dp), ("F", C.c_double), ("R", C.c_double),
-                ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double), ("neg", Electrode),
-                ("pos", Electrode)]
+                ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double), ("tab_ntheta", C.c_int32),
+                ("tab_ntemp", C.c_int32), ("tab_T_K", _dp), ("neg", Electrode), ("pos", Electrode)]
 
 
 class Config(C.Structure):
@@ -94,12 +93,12 @@ def load():
     L.mpcekf_ctx_destroy.argtypes = [vp]
     L.mpcekf_ctx_info.argtypes = [vp, C.POINTER(C.c_int64), _ip, _ip, _ip]
     L.mpcekf_init_cells.argtypes = [vp, _dp, _dp]
-    L.mpcekf_step.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32]
-    L.mpcekf_step_ex.argtypes = [vp, C.c_int32, C.POINTER(Traj), C.c_int32]
+    L.mpcekf_step.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32]
+    L.mpcekf_step_ex.argtypes = [vp, C.c_int32, vp, C.POINTER(Traj), C.c_int32]
     L.mpcekf_get_zk.argtypes = [vp, _dp, _dp]
-    L.mpcekf_plant_step.argtypes = [vp, _dp, _dp]
-    L.mpcekf_ekf_step.argtypes = [vp, _dp, _dp, _dp, _dp, _ip, _dp]
-    L.mpcekf_linearize.argtypes = [vp, _dp, _ip, _dp, _dp]
+    L.mpcekf_plant_step.argtypes = [vp, _dp, _dp, _dp]
+    L.mpcekf_ekf_step.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _ip, _dp]
+    L.mpcekf_linearize.argtypes = [vp, _dp, _ip, _dp, _dp, _dp]
     L.mpcekf_mpc_step.argtypes = [vp, _dp, _dp, _dp, _ip]
     L.mpcekf_predmat.argtypes = [C.c_int, C.c_int64, C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp]
     L.mpcekf_constraints.argtypes = [C.c_int, C.POINTER(Config), C.c_double, C.c_int64, _dp, _dp, _dp,
@@ -117,7 +116,7 @@ def load():
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_build_id"):
             getattr(L, nm).restype = C.c_int
-    if L.mpcekf_abi_version() != 1:
+    if L.mpcekf_abi_version() != 2:
         raise MpcekfError("ABI version mismatch")
     _lib = L
     return L

@@ -92,9 +92,8 @@ struct mpcekf_ctx {
   std::vector<hipEvent_t> ev;
   double t_ms[MPCEKF_NKERNELS] = {};
   int64_t t_n[MPCEKF_NKERNELS] = {};
-  // electrode constants kept for per-cell initialisation (k0(T), Cdleff)
-  double Tref = 0, Rgas = 0, th0[2] = {0, 0}, th100[2] = {0, 0}, k0ref[2] = {0, 0}, Ea[2] = {0, 0};
-  double Cdl[2] = {0, 0}, wDL[2] = {0, 0}, nDL[2] = {0, 0};
+  // soc(z,T) ends and the table temperatures, for SOC0n/p at init (OB_step.m:63-65)
+  std::vector<double> tabT, soc_end[2][2];
 
   int tmp(size_t bytes) {
     if (bytes <= tmp_bytes) return MPCEKF_OK;
@@ -153,9 +152,14 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   if (R->nT < 1 || R->nT > MAXT || R->nZ < 1 || R->nZ > MAXZ)
     return fail(MPCEKF_E_UNSUPPORTED, "rom: grid %dx%d exceeds %dx%d", R->nT, R->nZ, MAXT, MAXZ);
   if (R->nz < NROLE || R->nz > MAXROWS) return fail(MPCEKF_E_UNSUPPORTED, "rom: nz = %d outside [11, 64]", R->nz);
-  if (R->neg.ntab < 2 || R->neg.ntab != R->pos.ntab || !R->neg.U || !R->pos.U || !R->neg.dU || !R->pos.dU ||
-      !R->neg.dUdT || !R->pos.dUdT)
-    return fail(MPCEKF_E_ROM, "rom: OCP tables missing or of different lengths");
+  if (R->tab_ntheta < 2 || R->tab_ntemp < 1 || R->tab_ntemp > MAXTT || !R->tab_T_K)
+    return fail(MPCEKF_E_UNSUPPORTED, "rom: electrode tables need ntheta >= 2 and 1 <= ntemp <= %d", MAXTT);
+  for (int j = 0; j < R->tab_ntemp; ++j)
+    if (!std::isfinite(R->tab_T_K[j]) || (j && !(R->tab_T_K[j] > R->tab_T_K[j - 1])))
+      return fail(MPCEKF_E_ROM, "rom: electrode table temperatures must be finite and ascending");
+  for (const mpcekf_electrode *e : {&R->neg, &R->pos})
+    if (!e->soc0 || !e->soc100 || !e->Uocp || !e->dUocp || !e->k0 || !e->Rf || !e->Cdleff || !e->Uocp1)
+      return fail(MPCEKF_E_ROM, "rom: electrode table missing");
   for (int i = 1; i < R->nT; ++i)
     if (!(R->T_degC[i] > R->T_degC[i - 1])) return fail(MPCEKF_E_ROM, "rom: T set-points not ascending");
   for (int i = 1; i < R->nZ; ++i)
@@ -263,19 +267,30 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   }
   std::memcpy(r.flags, flags, sizeof flags);
   std::memcpy(r.c0k, c0k, sizeof c0k);
-  r.NM = NM; r.nT = nT; r.nZ = nZ; r.nz = nz; r.nzp = nzp; r.ntab = R->neg.ntab;
+  r.NM = NM; r.nT = nT; r.nZ = nZ; r.nz = nz; r.nzp = nzp;
+  r.nth = R->tab_ntheta; r.nte = R->tab_ntemp;
   r.Ts = R->Ts; r.Q = R->Q; r.F = R->F; r.R = R->R; r.Rc = R->Rc; r.Tref = R->Tref;
   r.th0n = R->neg.theta0; r.th100n = R->neg.theta100; r.th0p = R->pos.theta0; r.th100p = R->pos.theta100;
-  r.Rfn = R->neg.Rf; r.Rfp = R->pos.Rf;
 
-  // --- blobs ---
-  const int nt = r.ntab;
+  // --- electrode tables (mpcekf_kernels.hip ETab): header, then [fn][side][nte][nth] ---
+  const int nth = r.nth, nte = r.nte;
+  const mpcekf_electrode *els[2] = {&R->neg, &R->pos};
   std::vector<double> tabs;
-  for (const mpcekf_electrode *e : {&R->neg, &R->pos}) {
-    tabs.insert(tabs.end(), e->U, e->U + nt);
-    tabs.insert(tabs.end(), e->dUdT, e->dUdT + nt);
-    tabs.insert(tabs.end(), e->dU, e->dU + nt);
-  }
+  for (const mpcekf_electrode *e : els) tabs.insert(tabs.end(), e->Uocp1, e->Uocp1 + nth);
+  for (int j = 0; j < MAXTT; ++j) tabs.push_back(j < nte ? R->tab_T_K[j] : 0.0);
+  X->tabT.assign(R->tab_T_K, R->tab_T_K + nte);
+  for (int e = 0; e < 2; ++e)
+    for (int one = 0; one < 2; ++one) {
+      const double *src = one ? els[e]->soc100 : els[e]->soc0;
+      X->soc_end[e][one].assign(src, src + nte);
+      for (int j = 0; j < MAXTT; ++j) tabs.push_back(j < nte ? src[j] : 0.0);
+    }
+  for (int fn = 0; fn < 5; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
+    for (const mpcekf_electrode *e : els) {
+      const double *t = fn == 0 ? e->Uocp : fn == 1 ? e->dUocp : fn == 2 ? e->k0 : fn == 3 ? e->Rf : e->Cdleff;
+      tabs.insert(tabs.end(), t, t + (size_t)nte * nth);
+    }
+  const size_t cell_tablen = tabs.size() - (size_t)2 * nte * nth;  // k_cell / k_bounds: no Cdleff
   std::vector<double> pts(MAXT + MAXZ, 0.0);
   for (int t = 0; t < nT; ++t) pts[t] = R->T_degC[t] + 273.15;  // ROMmdls(t,z).T (initKF.m:58)
   for (int z = 0; z < nZ; ++z) pts[MAXT + z] = R->SOC_pct[z] / 100;  // ROMmdls(t,z).SOC
@@ -300,7 +315,8 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       b[nzp * NX + nzp + NX + i] = R->A[(size_t)m * n1 + pr[i]] * R->A[(size_t)m * n1 + pc[i]];
   }
   r.cell_tab = (int)cb.size();
-  cb.insert(cb.end(), tabs.begin(), tabs.end());
+  r.cell_tablen = (int)cell_tablen;
+  cb.insert(cb.end(), tabs.begin(), tabs.begin() + cell_tablen);
   cb.insert(cb.end(), pts.begin(), pts.end());
   r.cell_len = (int)cb.size();
   // plant blob: per model [C 9 x 5][res0 9][D 9] over role rows 0..8
@@ -315,6 +331,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     for (int e = 0; e < 6; ++e) b[NPLANT * NX + 2 * NPLANT + e] = R->A[(size_t)m * n1 + e];  // bigA column
   }
   r.plant_tab = (int)pb.size();
+  r.plant_tablen = (int)tabs.size();
   pb.insert(pb.end(), tabs.begin(), tabs.end());
   pb.insert(pb.end(), pts.begin(), pts.end());
   r.plant_len = (int)pb.size();
@@ -328,8 +345,9 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     for (int i = 0; i < NPK; ++i) cC[m * REC + NX + i] = a[pr[i]] * a[pc[i]];
     for (int e = 0; e < 6; ++e) cP[m * 6 + e] = a[e];
   }
-  if (cell_lds_bytes(r) > 160 * 1024)
-    return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of ROM tables exceed the 160 KiB LDS", cell_lds_bytes(r));
+  const int lds_need = std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r)), plant_lds_bytes(r));
+  if (lds_need > 160 * 1024)
+    return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of ROM tables exceed the 160 KiB LDS", lds_need);
   int rc;
   if ((rc = dalloc(&X->d_cell_blob, cb.size()))) return rc;
   if ((rc = dalloc(&X->d_plant_blob, pb.size()))) return rc;
@@ -400,13 +418,6 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   }
   // MPCEKF_SPLIT_CELL=1: the fused step's k_cell as two kernels (results identical).
   if (const char *e = std::getenv("MPCEKF_SPLIT_CELL")) X->split_cell = std::atoi(e) != 0;
-  X->Tref = rom->Tref;
-  X->Rgas = rom->R;
-  const mpcekf_electrode *el[2] = {&rom->neg, &rom->pos};
-  for (int i = 0; i < 2; ++i) {
-    X->th0[i] = el[i]->theta0; X->th100[i] = el[i]->theta100; X->k0ref[i] = el[i]->k0ref; X->Ea[i] = el[i]->Ea_k0;
-    X->Cdl[i] = el[i]->Cdl; X->wDL[i] = el[i]->wDL; X->nDL[i] = el[i]->nDL;
-  }
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
   const size_t n = (size_t)ncells, NM = (size_t)X->NM;
@@ -436,8 +447,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
   double *cs = X->d_const;
-  s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n; s.k0n = cs + 4 * n; s.k0p = cs + 5 * n;
-  s.Cdlen = cs + 6 * n; s.Cdlep = cs + 7 * n;
+  s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n;
   if (X->wide) {
     KWide &w = X->w;
     w.Np = cfg->Np; w.Nc = cfg->Nc; w.ncon = X->ncon;
@@ -482,27 +492,53 @@ int mpcekf_ctx_info(const mpcekf_ctx *X, int64_t *ncells, int32_t *nmodels, int3
   return MPCEKF_OK;
 }
 
-// initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.  The
-// T-only cellData functions are evaluated here once per cell with the host libm
-// (bit-identical to evaluating them at every call, since Tc is constant).
+// soc(z,T) on the host, the sequence of ETab::bracket / ETab::soc (and orc tidx / fsoc)
+static double host_soc(const mpcekf_ctx *X, int side, double z, double T) {
+  const std::vector<double> &tk = X->tabT;
+  const int nte = (int)tk.size();
+  const std::vector<double> &a = X->soc_end[side][0], &b = X->soc_end[side][1];
+  if (nte == 1) return a[0] + z * (b[0] - a[0]);
+  const double Tc = std::fmin(std::fmax(T, tk[0]), tk[nte - 1]);
+  int j = 0;
+  while (j < nte - 2 && Tc >= tk[j + 1]) ++j;
+  const double g = (Tc - tk[j]) / (tk[j + 1] - tk[j]);
+  const double s0 = a[j] + g * (a[j + 1] - a[j]), s1 = b[j] + g * (b[j + 1] - b[j]);
+  return s0 + z * (s1 - s0);
+}
+
+static int check_tc(const double *tc, size_t count) {
+  for (size_t i = 0; i < count; ++i)
+    if (!(tc[i] <= 100) || !std::isfinite(tc[i]))
+      return fail(MPCEKF_E_ARG, "temperature %zu = %g: must be finite and in degC (iterEKF.m:62)", i, tc[i]);
+  return MPCEKF_OK;
+}
+
+// A stage call's temperature argument (OB_step's Tc, iterEKF's / EKFmatsHandler's Tk)
+// becomes the cell's temperature for this and later calls.
+static int set_tc(mpcekf_ctx *X, const double *tc) {
+  if (!tc) return MPCEKF_OK;
+  int rc = check_tc(tc, (size_t)X->n);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(X->s.Tc, tc, (size_t)X->n * 8, hipMemcpyHostToDevice, X->stream));
+  return MPCEKF_OK;
+}
+
+// initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.
 int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_degC) {
   if (!X || ((!soc0_pct || !tc_degC) && X->n)) return fail(MPCEKF_E_ARG, "init_cells: null argument");
   HIPCHK(hipSetDevice(X->device));
   const size_t n = (size_t)X->n;
+  int rc0 = 0;
+  if ((X->n && (rc0 = check_tc(tc_degC, n)))) return rc0;
   std::vector<double> cst(n * 8), sc(n * 10, 0.0);
   for (size_t c = 0; c < n; ++c) {
     double tc = tc_degC[c], soc0 = soc0_pct[c];
-    if (!(tc <= 100)) return fail(MPCEKF_E_ARG, "cell %zu: Tc = %g; Tc must be in degC (iterEKF.m:62)", c, tc);
-    double T = tc + 273.15;  // OB_step.m:63,75
+    double T = tc + 273.15;  // OB_step.m:63
     double z = soc0 / 100;
     cst[0 * n + c] = tc;
-    cst[1 * n + c] = z;                                          // ekfData.SOC0 (initKF.m:133)
-    cst[2 * n + c] = X->th0[0] + z * (X->th100[0] - X->th0[0]);  // SOC0n (OB_step.m:64)
-    cst[3 * n + c] = X->th0[1] + z * (X->th100[1] - X->th0[1]);  // SOC0p
-    for (int e = 0; e < 2; ++e) {
-      cst[(4 + e) * n + c] = X->k0ref[e] * std::exp(X->Ea[e] / X->Rgas * (1.0 / X->Tref - 1.0 / T));
-      cst[(6 + e) * n + c] = std::pow(X->Cdl[e], 2 - X->nDL[e]) * std::pow(X->wDL[e], X->nDL[e] - 1);  // OB_step.m:218
-    }
+    cst[1 * n + c] = z;                              // ekfData.SOC0 (initKF.m:133)
+    cst[2 * n + c] = host_soc(X, 0, z, T);           // SOC0n = soc(SOC0/100, Tk1) (OB_step.m:64)
+    cst[3 * n + c] = host_soc(X, 1, z, T);           // SOC0p
     sc[0 * n + c] = cst[2 * n + c];  // SOCnAvg
     sc[1 * n + c] = cst[3 * n + c];  // SOCpAvg
     sc[3 * n + c] = X->cfg.SigmaX0[5];  // ekfData.SigmaX0 (initKF.m:99)
@@ -533,10 +569,12 @@ static int lerr(int rc, const char *what) {
 
 // runMPC.m:84-111, nsteps times: OB_step -> (all-model advance + EKF time
 // update) -> iterEKF measurement update -> EKFmatsHandler -> iterMPC.
-int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const mpcekf_traj *tr, int32_t outputs_on_device) {
+int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const mpcekf_traj *tr,
+                   int32_t outputs_on_device) {
   int rc = need_init(X);
   if (rc) return rc;
   if (nsteps < 0) return fail(MPCEKF_E_ARG, "nsteps < 0");
+  if (tc_degC && !outputs_on_device && (rc = check_tc(tc_degC, (size_t)X->n * (size_t)nsteps))) return rc;
   mpcekf_traj none{};
   if (!tr) tr = &none;
   const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
@@ -552,15 +590,20 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const mpcekf_traj *tr, int32_t
            {tr->zk, 8, nzz, nullptr},    {tr->zbk, 8, nzz, nullptr},  {tr->J_unc, 8, 1, nullptr},
            {tr->J_fin, 8, 1, nullptr},   {tr->norm_du, 8, 1, nullptr}, {tr->nviol, 4, 1, nullptr}};
   constexpr int NF = sizeof(f) / sizeof(f[0]);
+  const double *dtc = tc_degC;  // [nsteps][n] device copy of the per-step temperatures
   if (outputs_on_device) {
     for (F &e : f) e.dev = (char *)e.host;
   } else {
-    size_t need = 0;
+    size_t need = tc_degC ? ((per * 8 + 255) & ~(size_t)255) : 0;
     for (F &e : f) need += e.host ? ((per * e.width * e.esz + 255) & ~(size_t)255) : 0;
     if ((rc = X->tmp(need + 256))) return rc;
     char *p = (char *)X->d_tmp;
     for (F &e : f)
       if (e.host) { e.dev = p; p += (per * e.width * e.esz + 255) & ~(size_t)255; }
+    if (tc_degC) {
+      HIPCHK(hipMemcpyAsync(p, tc_degC, per * 8, hipMemcpyHostToDevice, X->stream));
+      dtc = (const double *)p;
+    }
   }
   auto row = [&](int i, int k) -> char * {  // step k's [ncells][width] block of field i
     return f[i].dev ? f[i].dev + (size_t)k * n * f[i].width * f[i].esz : nullptr;
@@ -583,7 +626,9 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const mpcekf_traj *tr, int32_t
     const bool sample = X->timing && ((k + 1) % X->timing_every == 0 || k == nsteps - 1);
     hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
-    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, X->stream), "plant"))) return rc;
+    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
+                   "plant")))
+      return rc;
     if (E) HIPCHK(hipEventRecord(E[1], X->stream));
     KIO io{};
     io.mode = MODE_FUSED;
@@ -675,15 +720,15 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const mpcekf_traj *tr, int32_t
   return MPCEKF_OK;
 }
 
-int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, double *traj_u, double *traj_v, double *traj_soc,
-                double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device) {
+int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, double *traj_u, double *traj_v,
+                double *traj_soc, double *traj_phise, int32_t *traj_nexec, int32_t outputs_on_device) {
   mpcekf_traj tr{};
   tr.u = traj_u;
   tr.v = traj_v;
   tr.soc = traj_soc;
   tr.phise = traj_phise;
   tr.nexec = traj_nexec;
-  return mpcekf_step_ex(X, nsteps, &tr, outputs_on_device);
+  return mpcekf_step_ex(X, nsteps, tc_degC, &tr, outputs_on_device);
 }
 
 int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {
@@ -729,27 +774,29 @@ struct Slab {
 };
 extern "C" {
 
-int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, double *vcell) {
+int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!iapp || !vcell) return fail(MPCEKF_E_ARG, "plant_step: null argument");
+  if ((rc = set_tc(X, tc_degC))) return rc;
   size_t n = (size_t)X->n;
   if ((rc = X->tmp(2 * n * 8 + 512))) return rc;
   Slab sl{(char *)X->d_tmp};
   double *di = sl.take<double>(n), *dv = sl.take<double>(n);
   HIPCHK(hipMemcpyAsync(di, iapp, n * 8, hipMemcpyHostToDevice, X->stream));
-  if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, X->stream), "plant"))) return rc;
+  if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, nullptr, X->stream), "plant"))) return rc;
   if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
   HIPCHK(hipMemcpyAsync(vcell, dv, n * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   return MPCEKF_OK;
 }
 
-int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, double *zk, double *boundzk,
-                    int32_t *xind_model, double *xind_gamma) {
+int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                    double *boundzk, int32_t *xind_model, double *xind_gamma) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!vk || !ik || !zk || !xind_model || !xind_gamma) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
+  if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
   if ((rc = X->tmp((2 * n + 2 * n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048))) return rc;
   Slab sl{(char *)X->d_tmp};
@@ -781,10 +828,11 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, double *z
 }
 
 int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
-                     double *lin) {
+                     const double *tk_degC, double *lin) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!zk || !xind_model || !xind_gamma || !lin) return fail(MPCEKF_E_ARG, "linearize: null argument");
+  if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
   if ((rc = X->tmp((n * nzz + 4 * n + n * MPCEKF_LIN_SIZE) * 8 + 4 * n * 4 + 2048))) return rc;
   Slab sl{(char *)X->d_tmp};

@@ -104,13 +104,56 @@ __device__ __forceinline__ double tabi(const double *t, int n, double x) {
   double f = tt - (double)i;
   return t[i] + f * (t[i + 1] - t[i]);
 }
-// tables: [U_n, dUdT_n, dU_n, U_p, dUdT_p, dU_p], each ntab long
-__device__ __forceinline__ double uocp(const double *tb, int n, int side, double th, double dT) {
-  const double *b = tb + side * 3 * n;
-  return tabi(b, n, th) + dT * tabi(b + n, n, th);
-}
-__device__ __forceinline__ double duocp(const double *tb, int n, int side, double th) {
-  return tabi(tb + side * 3 * n + 2 * n, n, th);
+// Electrode tables in LDS (include/mpcekf.h mpcekf_electrode; host: build_rom): a
+// header [Uocp1 [side][nth] | TK [MAXTT] | soc(0,T), soc(1,T) [side][2][MAXTT]], then
+// the 2-D tables [EF_*][side][nte][nth].  EF_CDL is last and only the plant blob
+// carries it (k_cell / k_bounds never read Cdleff).  A cell's temperature bracket
+// (j, g) is found once per step (bracket); a lookup is then the theta interpolation of
+// rows j and j + 1 and a + g (b - a), the sequence of oracle/mpcekf_oracle.c tab2/tidx.
+enum { EF_U = 0, EF_DU, EF_K0, EF_RF, EF_CDL, NEF };
+__host__ __device__ constexpr int etab_header(int nth) { return 2 * nth + 5 * MAXTT; }
+struct ETab {
+  const double *b;  // LDS base of the tables
+  int nth, nte;
+  int j;            // temperature bracket of this cell-step
+  double g;
+  __device__ __forceinline__ double f(int side, int fn, double th) const {
+    const double *t = b + etab_header(nth) + ((fn * 2 + side) * nte + j) * nth;
+    const double a = tabi(t, nth, th);
+    if (nte == 1) return a;
+    const double c = tabi(t + nth, nth, th);
+    return a + g * (c - a);
+  }
+  __device__ __forceinline__ double u1(int side, double th) const { return tabi(b + side * nth, nth, th); }
+  __device__ __forceinline__ double tk(int i) const { return b[2 * nth + i]; }
+  __device__ __forceinline__ double send(int side, int one) const {  // soc(one, T) at the bracket
+    const double *t = b + 2 * nth + MAXTT + (side * 2 + one) * MAXTT;
+    if (nte == 1) return t[0];
+    return t[j] + g * (t[j + 1] - t[j]);
+  }
+  __device__ __forceinline__ void bracket(double T) {
+    j = 0;
+    g = 0.0;
+    if (nte == 1) return;
+    const double Tc = fmin(fmax(T, tk(0)), tk(nte - 1));
+    int k = 0;
+    while (k < nte - 2 && Tc >= tk(k + 1)) ++k;
+    j = k;
+    g = (Tc - tk(k)) / (tk(k + 1) - tk(k));
+  }
+  // soc(z,T) = soc0 + z (soc100 - soc0) (iterEKF.m:282-283)
+  __device__ __forceinline__ double soc(int side, double z) const {
+    const double s0 = send(side, 0), s1 = send(side, 1);
+    return s0 + z * (s1 - s0);
+  }
+};
+__device__ __forceinline__ ETab etab(const KRom &r, const double *base, double T) {
+  ETab e;
+  e.b = base;
+  e.nth = r.nth;
+  e.nte = r.nte;
+  e.bracket(T);
+  return e;
 }
 
 __device__ __forceinline__ void two_nearest(const double *pts, int n, double x, int &i1, int &i2) {
@@ -352,11 +395,11 @@ __device__ __forceinline__ void meas_update(double *rec, const double L[NX], dou
 // ---------------------------------------------------------------------------
 struct CellCtx {
   const double *L;   // LDS: model blob base
-  const double *tb;  // LDS: tables
   const double *Tp, *Zp;  // LDS set-points
   double *erec;      // this cell's EKF records in HBM
-  int ntab, stride;
-  double T, dT, k0n, k0p;
+  int stride;
+  double T;          // iterEKF's Tk in K (iterEKF.m:62-66)
+  ETab et;           // electrode tables, bracketed at T
 };
 
 // getVariables (iterEKF.m:259-417).  Z is the permuted output vector.
@@ -365,8 +408,8 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
                                            double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc,
                                            const double (*xr)[NX] = nullptr) {
   double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
-  double SOCnAvg = r.th0n + xSOC * (r.th100n - r.th0n);
-  double SOCpAvg = r.th0p + xSOC * (r.th100p - r.th0p);
+  double SOCnAvg = cc.et.soc(0, xSOC);
+  double SOCpAvg = cc.et.soc(1, xSOC);
   if (SOCnAvg < 0) { warn++; SOCnAvg = 1e-6; }
   if (SOCnAvg > 1) { warn++; SOCnAvg = 1 - 1e-6; }
   if (SOCpAvg < 0) { warn++; SOCpAvg = 1e-6; }
@@ -452,7 +495,7 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
     for (int q = 0; q < NZ; ++q)
       if ((r.flags[q] & G_PTH) && Z[q] > 0.998) Z[q] = 0.998;
   }
-  double Un = uocp(cc.tb, cc.ntab, 0, SOCnAvg, cc.dT), Up = uocp(cc.tb, cc.ntab, 1, SOCpAvg, cc.dT);
+  double Un = cc.et.f(0, EF_U, SOCnAvg), Up = cc.et.f(1, EF_U, SOCpAvg);
 #pragma unroll
   for (int q = 0; q < NZ; ++q) {
     if (r.flags[q] & G_NPHISE) Z[q] = Z[q] + Un;
@@ -475,12 +518,14 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
     st |= ST_ERROR | ST_THETAE_NEG;
     return __builtin_nan("");
   }
-  double i0n = cc.k0n * sqrt(Z[R_TE1] * (1 - Z[R_TH0]) * Z[R_TH0]);
-  double i0p = cc.k0p * sqrt(Z[R_TEE] * (1 - Z[R_TH3]) * Z[R_TH3]);
+  double k0n = cc.et.f(0, EF_K0, SOCnAvg), k0p = cc.et.f(1, EF_K0, SOCpAvg);  // iterEKF.m:392-393
+  double i0n = k0n * sqrt(Z[R_TE1] * (1 - Z[R_TH0]) * Z[R_TH0]);
+  double i0p = k0p * sqrt(Z[R_TEE] * (1 - Z[R_TH3]) * Z[R_TH3]);
   double negEta0 = 2 * r.R * cc.T / r.F * dasinh(If0 / (2 * i0n));
   double posEta3 = 2 * r.R * cc.T / r.F * dasinh(If3 / (2 * i0p));
-  double Uocpn0 = uocp(cc.tb, cc.ntab, 0, Z[R_TH0], cc.dT), Uocpp3 = uocp(cc.tb, cc.ntab, 1, Z[R_TH3], cc.dT);
-  double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (r.Rfp * Z[R_IFDL3] - r.Rfn * Z[R_IFDL0]);
+  double Uocpn0 = cc.et.f(0, EF_U, Z[R_TH0]), Uocpp3 = cc.et.f(1, EF_U, Z[R_TH3]);
+  double Rfn = cc.et.f(0, EF_RF, SOCnAvg), Rfp = cc.et.f(1, EF_RF, SOCpAvg);  // iterEKF.m:406-407
+  double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (Rfp * Z[R_IFDL3] - Rfn * Z[R_IFDL0]);
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
     if (r.flags[q] & G_PPHIS) Z[q] = Z[q] + V;
@@ -490,24 +535,31 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
 
 // getChatV (iterEKF.m:421-519) pieces.  Cell scalars of the voltage Jacobian.
 struct ChatK {
-  double Rctn, Rctp, dUn0, dUp3;
+  double Rfn, Rfp, Rctn, Rctp, dUn0, dUp3, dn, dp;
 };
-__device__ __forceinline__ ChatK chat_k(const KRom &r, const CellCtx &cc, double zTE1, double zTH0, double zTEE,
-                                        double zTH3) {
+// xSOC = SOC0 - x0 Ts/(3600 Q) with the x0 of the call: Rf and k0 at the unclamped
+// soc(xSOC, Tk) (iterEKF.m:437-442,463-464)
+__device__ __forceinline__ ChatK chat_k(const KRom &r, const CellCtx &cc, double xSOC, double zTE1, double zTH0,
+                                        double zTEE, double zTH3) {
   ChatK k;
-  double i0n = cc.k0n * sqrt(zTE1 * (1 - zTH0) * zTH0);
-  double i0p = cc.k0p * sqrt(zTEE * (1 - zTH3) * zTH3);
+  const double SOCnAvg = cc.et.soc(0, xSOC), SOCpAvg = cc.et.soc(1, xSOC);
+  k.Rfn = cc.et.f(0, EF_RF, SOCnAvg);
+  k.Rfp = cc.et.f(1, EF_RF, SOCpAvg);
+  double i0n = cc.et.f(0, EF_K0, SOCnAvg) * sqrt(zTE1 * (1 - zTH0) * zTH0);
+  double i0p = cc.et.f(1, EF_K0, SOCpAvg) * sqrt(zTEE * (1 - zTH3) * zTH3);
   k.Rctn = r.R * cc.T / (r.F * i0n);
   k.Rctp = r.R * cc.T / (r.F * i0p);
-  k.dUn0 = duocp(cc.tb, cc.ntab, 0, zTH0);
-  k.dUp3 = duocp(cc.tb, cc.ntab, 1, zTH3);
+  k.dUn0 = cc.et.f(0, EF_DU, zTH0);
+  k.dUp3 = cc.et.f(1, EF_DU, zTH3);
+  k.dn = cc.et.soc(0, 1) - cc.et.soc(0, 0);  // soc(1,Tk) - soc(0,Tk) (iterEKF.m:497-500)
+  k.dp = cc.et.soc(1, 1) - cc.et.soc(1, 0);
   return k;
 }
 // The row of one corner (model blob Cm, interpolation weight g).
 __device__ __forceinline__ void chat_row(const KRom &r, const ChatK &K, const double *Cm, double g, double Chat[NX]) {
 #pragma unroll
   for (int k = 0; k < NX; ++k) {
-    double v = r.Rfp * (g * Cm[R_IFDL3 * NX + k]) - r.Rfn * (g * Cm[R_IFDL0 * NX + k]);
+    double v = K.Rfp * (g * Cm[R_IFDL3 * NX + k]) - K.Rfn * (g * Cm[R_IFDL0 * NX + k]);
     v = v + K.Rctp * (g * Cm[R_IF3 * NX + k]) - K.Rctn * (g * Cm[R_IF0 * NX + k]);
     v = v + g * Cm[R_PHIE * NX + k];
     v = v + (K.dUp3 * (g * Cm[R_TH3 * NX + k]) - K.dUn0 * (g * Cm[R_TH0 * NX + k]));
@@ -515,17 +567,15 @@ __device__ __forceinline__ void chat_row(const KRom &r, const ChatK &K, const do
   }
 }
 __device__ __forceinline__ double chat0(const KRom &r, const ChatK &K) {
-  double dn = (r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n));
-  double dp = (r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p));
-  double res0n = -K.dUn0 * r.Ts * dn / (3600 * r.Q);
-  double res0p = -K.dUp3 * r.Ts * dp / (3600 * r.Q);
+  double res0n = -K.dUn0 * r.Ts * K.dn / (3600 * r.Q);
+  double res0p = -K.dUp3 * r.Ts * K.dp / (3600 * r.Q);
   return res0p - res0n;
 }
 // Voltage Jacobian rows of the 4 corners.
 template <int NZ>
-__device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, const XI &xi, double zTE1, double zTH0,
-                                          double zTEE, double zTH3, double Chat[4][NX], double &Chat0) {
-  const ChatK K = chat_k(r, cc, zTE1, zTH0, zTEE, zTH3);
+__device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, const XI &xi, double xSOC, double zTE1,
+                                          double zTH0, double zTEE, double zTH3, double Chat[4][NX], double &Chat0) {
+  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
 #pragma unroll
   for (int j = 0; j < 4; ++j) chat_row(r, K, cc.L + xi.m[j] * cc.stride, xi.g[j], Chat[j]);
   Chat0 = chat0(r, K);
@@ -562,21 +612,23 @@ __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, c
   for (int k = 0; k < 6; ++k) L.Csoc[k] = 0.0;
   L.Csoc[NX] = rr;
   L.Dsoc = 0.0;
-  double SOCnAvg = r.th0n + Zsoc * (r.th100n - r.th0n);
-  double i0n = cc.k0n * sqrt(zr[R_TE1] * (1 - zr[R_TH0]) * zr[R_TH0]);
-  double i0p = cc.k0p * sqrt(zr[R_TEE] * (1 - zr[R_TH3]) * zr[R_TH3]);
+  ETab et = cc.et;
+  et.bracket(TK);  // EKFmatsHandler.m:53: TK = Tk + 273.15
+  double SOCnAvg = et.soc(0, Zsoc), SOCpAvg = et.soc(1, Zsoc);  // EKFmatsHandler.m:57-58
+  double i0n = et.f(0, EF_K0, SOCnAvg) * sqrt(zr[R_TE1] * (1 - zr[R_TH0]) * zr[R_TH0]);
+  double i0p = et.f(1, EF_K0, SOCpAvg) * sqrt(zr[R_TEE] * (1 - zr[R_TH3]) * zr[R_TH3]);
+  const double Rfn = et.f(0, EF_RF, SOCnAvg), Rfp = et.f(1, EF_RF, SOCpAvg);  // EKFmatsHandler.m:68-69
 #pragma unroll
   for (int k = 0; k < NX; ++k)
-    L.Cv[k] = r.Rfp * Cm[R_IFDL3 * NX + k] - r.Rfn * Cm[R_IFDL0 * NX + k] + Cm[R_PHIE * NX + k];
+    L.Cv[k] = Rfp * Cm[R_IFDL3 * NX + k] - Rfn * Cm[R_IFDL0 * NX + k] + Cm[R_PHIE * NX + k];
   L.Cv[NX] = 0.0;
-  L.Dv = r.Rfp * Dm[R_IFDL3] - r.Rfn * Dm[R_IFDL0] + Dm[R_PHIE];
-  double dT = TK - r.Tref;
-  double Upos = uocp(cc.tb, cc.ntab, 1, zr[R_TH3], dT), Uneg = uocp(cc.tb, cc.ntab, 0, zr[R_TH0], dT);
+  L.Dv = Rfp * Dm[R_IFDL3] - Rfn * Dm[R_IFDL0] + Dm[R_PHIE];
+  double Upos = et.f(1, EF_U, zr[R_TH3]), Uneg = et.f(0, EF_U, zr[R_TH0]);
   double negEta0 = 2 * r.R * TK / r.F * dasinh(zr[R_IF0] / (2 * i0n));
   double posEta3 = 2 * r.R * TK / r.F * dasinh(zr[R_IF3] / (2 * i0p));
   double b_phi = 0.01 * 0;
   L.bv = (Upos - Uneg) + (posEta3 - negEta0) + b_phi;
-  L.bphi = uocp(cc.tb, cc.ntab, 0, SOCnAvg, r.Tref - r.Tref);
+  L.bphi = et.u1(0, SOCnAvg);  // one-argument Uocp (EKFmatsHandler.m:96)
 #pragma unroll
   for (int k = 0; k < NX; ++k) L.Cphi[k] = Cm[R_NPHISE2 * NX + k];
   L.Cphi[NX] = 0.0;
@@ -1079,15 +1131,16 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
 // k_plant: OB_step simStep outputs for every cell (lane per cell)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout,
-                                               const int lazy_t) {
+                                               const int lazy_t, const double *tc_in) {
   extern __shared__ double lds[];
   stage_lds(lds, r.plant_blob, r.plant_len);
   __syncthreads();
-  const double *Tp = lds + r.plant_tab + 6 * r.ntab;
+  const double *Tp = lds + r.plant_tab + r.plant_tablen;
   const double *Zp = Tp + MAXT;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
   if (c >= s.n) return;
+  if (tc_in) s.Tc[c] = tc_in[c];  // this step's TC (runMPC.m:85-92), read by every later kernel
   if (lazy_t) {  // this step's inputs, for the deferred updates of every model (k_cell, k_flush)
     const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
     s.hist_u[slot] = iapp[c];
@@ -1097,17 +1150,17 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
     vout[c] = __builtin_nan("");
     return;
   }
-  const double *tb = lds + r.plant_tab;
-  int nt = r.ntab;
   double Iapp = iapp[c];
-  double T = s.Tc[c] + 273.15;
-  double dT = T - r.Tref;
+  double T = (tc_in ? tc_in[c] : s.Tc[c]) + 273.15;  // OB_step.m:75
+  const ETab et = etab(r, lds + r.plant_tab, T);
   double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
+  const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
   double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
-  double dUn = duocp(tb, nt, 0, SOCnAvg), dUp = duocp(tb, nt, 1, SOCpAvg);
+  const double Cdleffn = et.f(0, EF_CDL, s.SOC0n[c]), Cdleffp = et.f(1, EF_CDL, s.SOC0p[c]);  // OB_step.m:212-219
+  double dUn = et.f(0, EF_DU, SOCnAvg), dUp = et.f(1, EF_DU, SOCpAvg);
   double dQn = fabs(r.th100n - r.th0n), dQp = fabs(r.th100p - r.th0p);
-  double res0n = -dQn / (3600 * r.Q - s.Cdlen[c] * dQn * dUn);
-  double res0p = dQp / (3600 * r.Q - s.Cdlep[c] * dQp * dUp);
+  double res0n = -dQn / (3600 * r.Q - Cdleffn * dQn * dUn);
+  double res0p = dQp / (3600 * r.Q - Cdleffp * dQp * dUp);
   SOCnAvg = SOCnAvg + res0n * Iapp * r.Ts;
   SOCpAvg = SOCpAvg + res0p * Iapp * r.Ts;
   if (SOCnAvg < 0) SOCnAvg = 0;
@@ -1178,12 +1231,13 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   double th3 = fmin(fmax(yk[R_TH3] + s.SOC0p[c], 1e-6), 1 - 1e-6);
   double te1 = fmax(yk[R_TE1] + 1, 1e-6);
   double teE = fmax(yk[R_TEE] + 1, 1e-6);
-  double i0n = s.k0n[c] * sqrt(te1 * (1 - th0) * th0);
-  double i0p = s.k0p[c] * sqrt(teE * (1 - th3) * th3);
+  double i0n = et.f(0, EF_K0, negSOC) * sqrt(te1 * (1 - th0) * th0);  // OB_step.m:329-332
+  double i0p = et.f(1, EF_K0, posSOC) * sqrt(teE * (1 - th3) * th3);
   double negEta0 = 2 * r.R * T / r.F * dasinh(yk[R_IF0] / (2 * i0n));
   double posEta3 = 2 * r.R * T / r.F * dasinh(yk[R_IF3] / (2 * i0p));
-  double Uocpn0 = uocp(tb, nt, 0, th0, dT), Uocpp3 = uocp(tb, nt, 1, th3, dT);
-  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (r.Rfp * yk[R_IFDL3] - r.Rfn * yk[R_IFDL0]);
+  double Uocpn0 = et.f(0, EF_U, th0), Uocpp3 = et.f(1, EF_U, th3);
+  const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
+  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
   V = V - r.Rc * Iapp;
   s.SOCn[c] = SOCnAvg;
   s.SOCp[c] = SOCpAvg;
@@ -1403,7 +1457,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   extern __shared__ double lds[];
   stage_lds(lds, r.cell_blob, r.cell_len);
   __syncthreads();
-  const double *Tp = lds + r.cell_tab + 6 * r.ntab;
+  const double *Tp = lds + r.cell_tab + r.cell_tablen;
   const double *Zp = Tp + MAXT;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
@@ -1411,17 +1465,13 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   const double NaN = __builtin_nan("");
   CellCtx cc;
   cc.L = lds;
-  cc.tb = lds + r.cell_tab;
   cc.Tp = Tp;
   cc.Zp = Zp;
   cc.erec = s.ekf + (size_t)c * r.NM * REC;
-  cc.ntab = r.ntab;
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.dT = cc.T - r.Tref;
-  cc.k0n = s.k0n[c];
-  cc.k0p = s.k0p[c];
+  cc.et = etab(r, lds + r.cell_tab, cc.T);
   int st = s.status[c];
   const bool fused = io.mode & MODE_FUSED;
   if (io.mode & (MODE_MPC | MODE_FUSED)) s.hflag[c] = 0;  // set again only if hildreth.m must run
@@ -1518,7 +1568,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
     __builtin_amdgcn_sched_barrier(0);
     double ChatV[4][NX], C0;
-    get_chatv<NZ>(r, cc, xi, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
+    get_chatv<NZ>(r, cc, xi, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
     double S1[NPK];
     load_S(cc.erec + (size_t)xi.m[0] * REC, S1);
     if (t) replay_S(S1, cc.L + xi.m[0] * cc.stride + NZ * NX + NZ, tsj[0], t, cf.SigmaW);
@@ -1784,14 +1834,10 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   const bool valid = cq < n && bd[BD_M * n + c] >= 0.0;
   CellCtx cc;
   cc.L = lds;
-  cc.tb = lds + r.cell_tab;
-  cc.ntab = r.ntab;
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;
-  cc.dT = cc.T - r.Tref;
-  cc.k0n = s.k0n[c];
-  cc.k0p = s.k0p[c];
+  cc.et = etab(r, lds + r.cell_tab, cc.T);
   const double g = bd[(BD_G + j) * n + c];
   const int m = valid ? (int)bd[(BD_M + j) * n + c] : 0;
   const double *Cm = cc.L + m * cc.stride;
@@ -1805,15 +1851,15 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   for (int k = 0; k < NX; ++k)
 #pragma unroll
     for (int l = k + 1; l < NX; ++l) S1b[pk(k, l)] = 2 * S1b[pk(k, l)];
-  const ChatK K = chat_k(r, cc, zTE1, zTH0, zTEE, zTH3);
+  const double xSOC = s.SOC0[c] - x0 * (r.Ts / (3600 * r.Q));
+  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
   double ChV[NX];
   chat_row(r, K, Cm, g, ChV);
   const double ChV0 = chat0(r, K);
-  const double res0n = -r.Ts * ((r.th0n + 1 * (r.th100n - r.th0n)) - (r.th0n + 0 * (r.th100n - r.th0n))) / (3600 * r.Q);
-  const double res0p = -r.Ts * ((r.th0p + 1 * (r.th100p - r.th0p)) - (r.th0p + 0 * (r.th100p - r.th0p))) / (3600 * r.Q);
-  const double xSOC = s.SOC0[c] - x0 * (r.Ts / (3600 * r.Q));
-  const double dUn = duocp(cc.tb, cc.ntab, 0, r.th0n + xSOC * (r.th100n - r.th0n));
-  const double dUp = duocp(cc.tb, cc.ntab, 1, r.th0p + xSOC * (r.th100p - r.th0p));
+  const double res0n = -r.Ts * K.dn / (3600 * r.Q);  // iterEKF.m:562-565
+  const double res0p = -r.Ts * K.dp / (3600 * r.Q);
+  const double dUn = cc.et.f(0, EF_DU, cc.et.soc(0, xSOC));  // iterEKF.m:576-580
+  const double dUp = cc.et.f(1, EF_DU, cc.et.soc(1, xSOC));
   const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
   double cph0[NX];
 #pragma unroll
@@ -2226,14 +2272,16 @@ int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double
 static int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
 int cell_lds_bytes(const KRom &r) { return (int)((r.cell_len + 1) * sizeof(double)); }
+int bounds_lds_bytes(const KRom &r) { return (bounds_c0_base(r) + BOUNDS_BLOCK / 4 * 8) * (int)sizeof(double); }
 int plant_lds_bytes(const KRom &r) { return (int)((r.plant_len + 1) * sizeof(double)); }
 
 bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
 
-int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, void *stream) {
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
+                 void *stream) {
   if (s.n == 0) return 0;
   hipLaunchKernelGGL(k_plant, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r, s,
-                     iapp, vout, lazy_t);
+                     iapp, vout, lazy_t, tc_in);
   return (int)hipGetLastError();
 }
 
@@ -2294,7 +2342,7 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
 template <int NZ>
 static void launch_bounds_t(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
   static bool attr = false;
-  int lds = (bounds_c0_base(r) + BOUNDS_BLOCK / 4 * 8) * (int)sizeof(double);
+  int lds = bounds_lds_bytes(r);
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_bounds<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;

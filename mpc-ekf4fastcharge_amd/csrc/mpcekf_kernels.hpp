@@ -17,6 +17,7 @@ constexpr int MAXROWS = 64;
 constexpr int NPLANT = 9;  // role rows the plant needs (OB_step.m:289-344)
 constexpr int PREC = NPLANT * NX + NPLANT + NPLANT + 6;  // plant blob record per model: C[9][5], res0[9], D[9], a[6]
 constexpr int LAZY_H = 32;  // deferred time update: input ring length = flush period (steps)
+constexpr int MAXTT = 8;    // max electrode-table temperatures (mpcekf_rom.tab_ntemp)
 
 // role slots = the first rows of the permuted output vector (rom.py ROLE_NAMES)
 enum { R_IFDL0 = 0, R_IFDL3, R_IF0, R_IF3, R_TH0, R_TH3, R_TE1, R_TEE, R_PHIE, R_PHISE0, R_NPHISE2, NROLE };
@@ -27,17 +28,19 @@ enum { C0_ZERO = 0, C0_CHATV0, C0_RES0N, C0_RES0P, C0_DUN, C0_DUP, C0_MDUN };
 enum { ST_ERROR = 1, ST_LOCKOUT = 2, ST_THETAE_NEG = 4 };
 
 struct KRom {
-  int NM, nT, nZ, nz, nzp, ntab;  // nzp = padded row count the kernel was built for
+  int NM, nT, nZ, nz, nzp;  // nzp = padded row count the kernel was built for
+  int nth, nte;                   // electrode tables: theta points, temperatures
   double Ts, Q, F, R, Rc, Tref;
-  double th0n, th100n, th0p, th100p, Rfn, Rfp;
+  double th0n, th100n, th0p, th100p;  // theta0(), theta100() of the plant (OB_step.m:207-210)
   unsigned char flags[MAXROWS];   // per permuted row
   unsigned char c0k[MAXROWS];     // getChatZ Chat0 kind per permuted row
   short perm[MAXROWS];            // permuted row -> ROM row
-  // blobs end with: tables [6][ntab], Tpts [MAXT] (K), Zpts [MAXZ] (fraction)
+  // blobs end with: electrode tables (mpcekf_kernels.hip ETab; *_tablen doubles), Tpts
+  // [MAXT] (K), Zpts [MAXZ] (fraction)
   const double *cell_blob;        // per model [C nzp*5][D nzp][a 5] ... then tables
-  int cell_stride, cell_tab, cell_len;
+  int cell_stride, cell_tab, cell_tablen, cell_len;
   const double *plant_blob;       // per model [C 9*5][res0 9][D 9] ... then tables
-  int plant_tab, plant_len;
+  int plant_tab, plant_tablen, plant_len;
   const double *bulk_tab;         // cA[NM*20], cB[NM*20], cP[NM*6]
 };
 
@@ -54,7 +57,8 @@ struct KState {
   double *lam;    // [ncon][n]
   int *warn, *status;
   // per-cell constants (set at init)
-  const double *Tc, *SOC0, *SOC0n, *SOC0p, *k0n, *k0p, *Cdlen, *Cdlep;
+  double *Tc;  // the cell's temperature (degC): set at init, by per-call arguments and per fused step
+  const double *SOC0, *SOC0n, *SOC0p;
   // diagnostics of the last MPC step
   double *J_unc, *J_fin;
   int *nviol;
@@ -116,7 +120,9 @@ struct KWide {
 
 // host-side launchers (defined in mpcekf_kernels.hip)
 // lazy_t > 0: deferred mode (corners replayed/advanced in place, inputs logged to the rings)
-int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, void *stream);
+// tc_in (device, [n] degC, may be null): the step's temperature, stored into s.Tc first
+int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
+                 void *stream);
 // brings every model of every cell from its ts to step t, then sets ts = new_ts
 int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream);
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
@@ -154,6 +160,7 @@ int launch_predmat_wide(int64_t n, int Np, int Nc, const double *a, const double
 int launch_constraints_wide(const KCfg &c, int Np, int Nc, int64_t n, const double *lin, const double *uk_1,
                             const double *soc_k1, double *M, double *gam, void *stream);
 int cell_lds_bytes(const KRom &r);
+int bounds_lds_bytes(const KRom &r);
 int plant_lds_bytes(const KRom &r);
 
 }  // namespace mk

@@ -84,12 +84,14 @@ class _PackedRom:
         r.tf_code = iptr(arr([TF_CODE[n] for n in rom.names], np.int32))
         r.tf_xloc = dptr(arr(rom.xloc))
         r.F, r.R, r.Q, r.Rc, r.Tref = rom.F, rom.R, rom.Q, rom.Rc, rom.Tref
+        r.tab_ntheta, r.tab_ntemp = rom.ntheta, rom.ntemp
+        r.tab_T_K = dptr(arr(np.atleast_1d(rom.tab_T_K)))
         for side in ("neg", "pos"):
             e = getattr(rom, side)
             s = getattr(r, side)
-            s.theta0, s.theta100, s.Rf, s.k0ref, s.Ea_k0 = e.theta0, e.theta100, e.Rf, e.k0ref, e.Ea_k0
-            s.wDL, s.Cdl, s.nDL, s.ntab = e.wDL, e.Cdl, e.nDL, len(e.U)
-            s.U, s.dUdT, s.dU = dptr(arr(e.U)), dptr(arr(e.dUdT)), dptr(arr(e.dU))
+            s.theta0, s.theta100 = e.theta0, e.theta100
+            for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
+                setattr(s, k, dptr(arr(getattr(e, k))))
         self.s = r
 
 
@@ -144,12 +146,17 @@ class Context:
                        zbk=(np.float64, None), J_unc=(np.float64, ()), J_fin=(np.float64, ()),
                        norm_du=(np.float64, ()), nviol=(np.int32, ()))
 
-    def step(self, nsteps, outputs=("u", "v", "soc", "phise", "nexec")):
+    def step(self, nsteps, outputs=("u", "v", "soc", "phise", "nexec"), tc=None):
         """nsteps fused closed-loop steps (runMPC.m:83-112).  ``outputs`` names the per-step
         stores to return as [nsteps, ncells(, k)] arrays: u, v, soc, phise, nexec, and the
         diagnostics x (x_store), zk / zbk (zkEst / zkBound), J_unc, J_fin, norm_du, nviol
-        (mpcData.cost)."""
+        (mpcData.cost).  ``tc`` [nsteps, ncells] (or broadcastable): the TC of each step
+        in degC (runMPC.m:85-92); None keeps every cell's current temperature."""
         n = self.n
+        tcs = None
+        if tc is not None:
+            tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc, dtype=np.float64).reshape(
+                (nsteps, -1) if np.ndim(tc) else (1, 1)), (nsteps, n)))
         out = {}
         tr = _lib.Traj()
         for k in outputs:
@@ -159,13 +166,14 @@ class Context:
             tail = (self.nz + 2,) if tail is None else tail
             out[k] = np.empty((nsteps, n) + tail, dtype=dt)
             setattr(tr, k, out[k].ctypes.data_as(C.c_void_p).value)
-        check(self.L.mpcekf_step_ex(self.h, int(nsteps), C.byref(tr), 0))
+        check(self.L.mpcekf_step_ex(self.h, int(nsteps), tcs.ctypes.data_as(C.c_void_p) if tcs is not None else None,
+                                    C.byref(tr), 0))
         return out
 
     def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
         """Fused steps writing [nsteps][ncells] outputs to device pointers (ints)."""
         p = [C.c_void_p(x) if x else None for x in (u, v, soc, phise, nexec)]
-        check(self.L.mpcekf_step(self.h, int(nsteps), *p, 1))
+        check(self.L.mpcekf_step(self.h, int(nsteps), None, *p, 1))
 
     def set_timing(self, enable=True):
         """enable: True/1 = every step; N > 1 = sample every N-th step (less perturbation)."""
@@ -203,36 +211,43 @@ class Context:
         return zk, zb
 
     # -- MATLAB-named stage functions --------------------------------------
-    def OB_step(self, Iapp):
-        """[Vcell, ~, cellState] = OB_step(Iapp, Tc, cellState, ROM)  (OB_step.m:1)."""
+    def _tvec(self, T):
+        return None if T is None else self._vec(T)
+
+    def OB_step(self, Iapp, Tc=None):
+        """[Vcell, ~, cellState] = OB_step(Iapp, Tc, cellState, ROM)  (OB_step.m:1).
+        Tc (degC, scalar or [n]) becomes the cell temperature; None keeps the current one."""
         i = self._vec(Iapp)
+        t = self._tvec(Tc)
         v = np.empty(self.n)
-        check(self.L.mpcekf_plant_step(self.h, dptr(i), dptr(v)))
+        check(self.L.mpcekf_plant_step(self.h, dptr(i), dptr(t), dptr(v)))
         return v
 
-    def iterEKF(self, vk, ik, bounds=True):
+    def iterEKF(self, vk, ik, Tk=None, bounds=True):
         """[zk, boundzk, ekfData, Xind] = iterEKF(vk, ik, Tk, ekfData)  (iterEKF.m:30).
 
         Xind is returned as dict(model=[n,4] model index t*nZ+z, theT, theZ, gamma)."""
         v = self._vec(vk)
         i = self._vec(ik)
+        t = self._tvec(Tk)
         zk = np.empty((self.n, self.nz + 2))
         zb = np.empty((self.n, self.nz + 2)) if bounds else None
         xm = np.empty((self.n, 4), dtype=np.int32)
         xg = np.empty((self.n, 4))
-        check(self.L.mpcekf_ekf_step(self.h, dptr(v), dptr(i), dptr(zk), dptr(zb), iptr(xm), dptr(xg)))
+        check(self.L.mpcekf_ekf_step(self.h, dptr(v), dptr(i), dptr(t), dptr(zk), dptr(zb), iptr(xm), dptr(xg)))
         xind = dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
         return zk, zb, xind
 
-    def EKFmatsHandler(self, zk, Xind):
+    def EKFmatsHandler(self, zk, Xind, Tk=None):
         """[MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)  (EKFmatsHandler.m:1).
 
         Returns the packed linearisation records [n, 35] (fields: LIN_FIELDS)."""
         zk = np.ascontiguousarray(zk, dtype=np.float64)
         xm = np.ascontiguousarray(Xind["model"], dtype=np.int32)
         xg = np.ascontiguousarray(Xind["gamma"], dtype=np.float64)
+        t = self._tvec(Tk)
         lin = np.empty((self.n, LIN_SIZE))
-        check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(lin)))
+        check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin)))
         return lin
 
     def iterMPC(self, lin, SOCk_1):
@@ -343,12 +358,13 @@ def structured_M(Hv, He, Hs):
     return M
 
 
-def runMPC(rom, SOC0, TC, nsteps, cfg=None, device=0, ncells=None):
-    """runMPC.m:72-112 for a batch of cells; returns trajectories [nsteps, ncells]."""
+def runMPC(rom, SOC0, TC, nsteps, cfg=None, device=0, ncells=None, tc_traj=None):
+    """runMPC.m:72-112 for a batch of cells; returns trajectories [nsteps, ncells].
+    tc_traj [nsteps, ncells] (degC): a temperature profile (TC is the initial one)."""
     SOC0 = np.atleast_1d(np.asarray(SOC0, dtype=np.float64))
     n = ncells or SOC0.shape[0]
     with Context(rom, n, cfg, device) as ctx:
         ctx.init_cells(SOC0, TC)
-        out = ctx.step(nsteps)
+        out = ctx.step(nsteps, tc=tc_traj)
         out["status"] = ctx.get_state()["status"]
         return out

@@ -9,8 +9,9 @@ iterEKF.m:282-283,362-363,392-407, EKFmatsHandler.m:53-92).  This module
   (``ROMmdls(T,Z).{A,B,C,D,T,SOC}``, ``tfData.{names,xLoc}``,
   ``xraData.{T,SOC,Tsamp}``, ``cellData``);
 * defines the *tabulated* ``cellData.function`` semantics this framework uses
-  (piecewise-linear OCP tables, Arrhenius ``k0``, constant ``Rf``/``wDL``/``Cdl``),
-  identical in the numpy oracle, the C oracle and the HIP kernels;
+  (every handle of (theta, T) as a [ntemp, ntheta] table with a defined bilinear
+  lookup, ``soc(z, T)`` from its z = 0 / 1 ends), identical in the numpy oracle, the
+  C oracle and the HIP kernels;
 * generates a deterministic synthetic NMC30-like ROM (3 x 21 set-points, n = 5,
   nz = 26 outputs) that satisfies every index check of iterEKF.m:692-734 and
   OB_step.m:140-158;
@@ -60,26 +61,30 @@ C0_ZERO, C0_CHATV0, C0_RES0N, C0_RES0P, C0_DUN_RES0N, C0_DUP_RES0P, C0_MDUN_RES0
 EPS = np.finfo(float).eps
 
 
+EL_TABLES = ("Uocp", "dUocp", "k0", "Rf", "Cdleff")   # [ntemp, ntheta] each (include/mpcekf.h)
+
+
 @dataclass
 class Electrode:
-    theta0: float
-    theta100: float
-    Rf: float
-    k0ref: float
-    Ea_k0: float
-    wDL: float
-    Cdl: float
-    nDL: float
-    U: np.ndarray          # OCP table on a uniform grid over theta in [0, 1]
-    dUdT: np.ndarray       # entropic coefficient table (V/K)
-    dU: np.ndarray         # dUocp/dtheta table
+    """One electrode's ``cellData.function.{neg,pos}`` handles, tabulated on the ROM's
+    (T, theta) grid (:attr:`ROM.tab_T_K` x uniform theta over [0, 1])."""
+    theta0: float              # theta0(): the plant's zero-argument call (OB_step.m:207-210)
+    theta100: float            # theta100()
+    soc0: np.ndarray           # [ntemp] soc(0, T)
+    soc100: np.ndarray         # [ntemp] soc(1, T)
+    Uocp: np.ndarray           # [ntemp, ntheta] Uocp(theta, T)
+    Uocp1: np.ndarray          # [ntheta] Uocp(theta), the one-argument call (EKFmatsHandler.m:96)
+    dUocp: np.ndarray          # [ntemp, ntheta] dUocp(theta, T)
+    k0: np.ndarray             # [ntemp, ntheta] k0(theta, T)
+    Rf: np.ndarray             # [ntemp, ntheta] Rf(theta, T)
+    Cdleff: np.ndarray         # [ntemp, ntheta] Cdl^(2-nDL) wDL^(nDL-1) (OB_step.m:212-219)
 
 
 def interp_tab(tab: np.ndarray, x: float) -> float:
     """Piecewise-linear table lookup on a uniform grid over [0, 1].
 
     NaN in -> NaN out; the abscissa is clamped to [0, 1].  The C oracle
-    (oracle/mpcekf_oracle.c: tab_interp) and the kernels (csrc: tab_interp)
+    (oracle/mpcekf_oracle.c: tab_interp) and the kernels (csrc: tabi)
     evaluate exactly this expression sequence.
     """
     if x != x:
@@ -94,41 +99,67 @@ def interp_tab(tab: np.ndarray, x: float) -> float:
     return float(tab[i] + f * (tab[i + 1] - tab[i]))
 
 
+def temp_index(T_K: np.ndarray, T: float):
+    """(j, g) of T on the table temperature grid: T clamped to the grid ends, j the
+    last grid index with T_K[j] <= T (at most ntemp - 2), g = (T - T_K[j]) / (T_K[j+1] - T_K[j]).
+    A single-point grid gives (0, 0.0).  Same sequence in the kernels and the C oracle."""
+    nt = len(T_K)
+    if nt == 1:
+        return 0, 0.0
+    Tc = min(max(T, float(T_K[0])), float(T_K[-1]))
+    j = 0
+    while j < nt - 2 and Tc >= T_K[j + 1]:
+        j += 1
+    return j, float((Tc - T_K[j]) / (T_K[j + 1] - T_K[j]))
+
+
+def eval_tab2(tab2: np.ndarray, theta: float, jg) -> float:
+    """Defined bilinear lookup of a [ntemp, ntheta] table: the theta interpolation of rows
+    j and j+1, then a + g (b - a)."""
+    j, g = jg
+    a = interp_tab(tab2[j], theta)
+    if tab2.shape[0] == 1:
+        return a
+    b = interp_tab(tab2[j + 1], theta)
+    return float(a + g * (b - a))
+
+
+def eval_tab1(tab1: np.ndarray, jg) -> float:
+    """A [ntemp] table at (j, g): tab[j] + g (tab[j+1] - tab[j])."""
+    j, g = jg
+    if tab1.shape[0] == 1:
+        return float(tab1[0])
+    return float(tab1[j] + g * (tab1[j + 1] - tab1[j]))
+
+
 class CellFunctions:
-    """Tabulated stand-in for one electrode's ``cellData.function.{neg,pos}``."""
+    """The tabulated ``cellData.function.{neg,pos}`` handles of one electrode."""
 
-    def __init__(self, e: Electrode, Tref: float, R: float):
+    def __init__(self, e: Electrode, T_K: np.ndarray):
         self.e = e
-        self.Tref = Tref
-        self.R = R
+        self.T_K = np.asarray(T_K, dtype=float)
 
-    def soc(self, z, T=None):                 # cellData.function.neg.soc(z,T)
-        e = self.e
-        return e.theta0 + z * (e.theta100 - e.theta0)
+    def soc(self, z, T):                      # cellData.function.neg.soc(z,T)
+        jg = temp_index(self.T_K, T)
+        s0, s1 = eval_tab1(self.e.soc0, jg), eval_tab1(self.e.soc100, jg)
+        return s0 + z * (s1 - s0)
 
-    def Uocp(self, theta, T=None):            # 1-arg call == Tref (EKFmatsHandler.m:96)
+    def Uocp(self, theta, T=None):            # 1-arg call: its own table (EKFmatsHandler.m:96)
         if T is None:
-            T = self.Tref
-        return interp_tab(self.e.U, theta) + (T - self.Tref) * interp_tab(self.e.dUdT, theta)
+            return interp_tab(self.e.Uocp1, theta)
+        return eval_tab2(self.e.Uocp, theta, temp_index(self.T_K, T))
 
-    def dUocp(self, theta, T=None):
-        return interp_tab(self.e.dU, theta)
+    def dUocp(self, theta, T):
+        return eval_tab2(self.e.dUocp, theta, temp_index(self.T_K, T))
 
     def k0(self, theta, T):
-        e = self.e
-        return e.k0ref * math.exp(e.Ea_k0 / self.R * (1.0 / self.Tref - 1.0 / T))
+        return eval_tab2(self.e.k0, theta, temp_index(self.T_K, T))
 
-    def Rf(self, theta, T=None):
-        return self.e.Rf
+    def Rf(self, theta, T):
+        return eval_tab2(self.e.Rf, theta, temp_index(self.T_K, T))
 
-    def wDL(self, theta=None, T=None):
-        return self.e.wDL
-
-    def Cdl(self, theta=None, T=None):
-        return self.e.Cdl
-
-    def nDL(self):
-        return self.e.nDL
+    def Cdleff(self, theta, T):
+        return eval_tab2(self.e.Cdleff, theta, temp_index(self.T_K, T))
 
     def theta0(self):
         return self.e.theta0
@@ -153,6 +184,7 @@ class ROM:
     Q: float                   # cellData.function.const.Q(), Ah
     Rc: float
     Tref: float
+    tab_T_K: np.ndarray        # [ntemp] temperature grid of the electrode tables (K, ascending)
     neg: Electrode
     pos: Electrode
     meta: dict = field(default_factory=dict)
@@ -179,7 +211,15 @@ class ROM:
         return self.nT * self.nZ
 
     def fn(self, which):
-        return CellFunctions(self.neg if which == "neg" else self.pos, self.Tref, self.R)
+        return CellFunctions(self.neg if which == "neg" else self.pos, self.tab_T_K)
+
+    @property
+    def ntheta(self):
+        return int(self.neg.Uocp.shape[1])
+
+    @property
+    def ntemp(self):
+        return int(np.asarray(self.tab_T_K).size)
 
     # ROMmdls(t,z).T / .SOC exactly as initKF.m:57-59 reads them
     def mdl_T_K(self):
@@ -251,9 +291,19 @@ class ROM:
                     Thetae=Thetae, roles=roles, loc=loc)
 
     def validate(self):
-        """initKF.m:66-91 structure checks plus grid ordering."""
+        """initKF.m:66-91 structure checks plus grid ordering and table shapes."""
         if np.any(np.diff(self.T_degC) <= 0) or np.any(np.diff(self.SOC_pct) <= 0):
             raise ValueError("ROM set-points must be strictly ascending")
+        tk = np.asarray(self.tab_T_K, dtype=float)
+        if tk.ndim != 1 or tk.size < 1 or np.any(np.diff(tk) <= 0):
+            raise ValueError("electrode table temperatures must be strictly ascending")
+        for e in (self.neg, self.pos):
+            for k in EL_TABLES:
+                t = getattr(e, k)
+                if t.ndim != 2 or t.shape != (tk.size, self.ntheta) or t.shape[1] < 2:
+                    raise ValueError(f"electrode table {k}: shape {t.shape}, expected ({tk.size}, ntheta >= 2)")
+            if e.Uocp1.shape != (self.ntheta,) or e.soc0.shape != (tk.size,) or e.soc100.shape != (tk.size,):
+                raise ValueError("electrode tables Uocp1 / soc0 / soc100 have the wrong length")
         if not np.all(self.A[..., -1] == 1):
             raise ValueError("A does not have integrator state (initKF.m:74)")
         self.resolve_indices()
@@ -306,7 +356,7 @@ class ROM:
     def to_npz_dict(self):
         d = dict(T_degC=self.T_degC, SOC_pct=self.SOC_pct, Ts=self.Ts, A=self.A, C=self.C, D=self.D,
                  names=np.array(self.names), xloc=self.xloc, F=self.F, R=self.R, Q=self.Q, Rc=self.Rc,
-                 Tref=self.Tref)
+                 Tref=self.Tref, tab_T_K=self.tab_T_K)
         for side, e in (("neg", self.neg), ("pos", self.pos)):
             for k, v in e.__dict__.items():
                 d[f"{side}_{k}"] = v
@@ -320,9 +370,8 @@ class ROM:
         z = np.load(path, allow_pickle=False)
 
         def el(side):
-            keys = ["theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL"]
-            kw = {k: float(z[f"{side}_{k}"]) for k in keys}
-            for k in ("U", "dUdT", "dU"):
+            kw = {k: float(z[f"{side}_{k}"]) for k in _EL_SCALARS}
+            for k in _EL_ARRAYS:
                 kw[k] = np.array(z[f"{side}_{k}"], dtype=float)
             return Electrode(**kw)
 
@@ -331,11 +380,11 @@ class ROM:
                    D=np.array(z["D"], float), names=[str(s) for s in z["names"]],
                    xloc=np.array(z["xloc"], float), F=float(z["F"]), R=float(z["R"]),
                    Q=float(z["Q"]), Rc=float(z["Rc"]), Tref=float(z["Tref"]),
-                   neg=el("neg"), pos=el("pos"))
+                   tab_T_K=np.array(z["tab_T_K"], float), neg=el("neg"), pos=el("pos"))
 
 
     # ---- JSON exchange format (matlab/mpcekf_export_rom.m) ------------------
-    JSON_FORMAT = "mpcekf-rom-v1"
+    JSON_FORMAT = "mpcekf-rom-v2"
 
     def to_json_dict(self):
         """The dict ``matlab/mpcekf_export_rom.m`` writes: every array as
@@ -347,14 +396,14 @@ class ROM:
 
         def el(e):
             d = {k: float(getattr(e, k)) for k in _EL_SCALARS}
-            d.update({k: arr(getattr(e, k)) for k in ("U", "dUdT", "dU")})
+            d.update({k: arr(getattr(e, k)) for k in _EL_ARRAYS})
             return d
 
         return {"format": self.JSON_FORMAT, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
                 "Ts": float(self.Ts), "A": arr(self.A), "C": arr(self.C), "D": arr(self.D),
                 "names": list(self.names), "xloc": arr(self.xloc), "F": float(self.F), "R": float(self.R),
                 "Q": float(self.Q), "Rc": float(self.Rc), "Tref": float(self.Tref),
-                "neg": el(self.neg), "pos": el(self.pos)}
+                "tab_T_K": arr(self.tab_T_K), "neg": el(self.neg), "pos": el(self.pos)}
 
     def save_json(self, path):
         import json
@@ -386,9 +435,16 @@ class ROM:
                 raise ValueError(f"ROM json: expected {ndim}-D array, got shape {shape}")
             return x
 
+        ntemp = arr(d["tab_T_K"], 1).size
+
         def el(e):
             kw = {k: float(e[k]) for k in _EL_SCALARS}
-            kw.update({k: arr(e[k], 1) for k in ("U", "dUdT", "dU")})
+            for k in _EL_ARRAYS:
+                if k in EL_TABLES:     # [ntemp, ntheta]; MATLAB drops the leading 1 of ntemp = 1
+                    x = arr(e[k], 1) if ntemp == 1 else arr(e[k], 2)
+                    kw[k] = x.reshape(ntemp, -1)
+                else:
+                    kw[k] = arr(e[k], 1)
             return Electrode(**kw)
 
         names = d["names"]
@@ -396,7 +452,8 @@ class ROM:
         rom = ROM(T_degC=arr(d["T_degC"], 1), SOC_pct=arr(d["SOC_pct"], 1), Ts=float(d["Ts"]),
                   A=arr(d["A"], 3), C=arr(d["C"], 4), D=arr(d["D"], 3), names=names,
                   xloc=arr(d["xloc"], 1), F=float(d["F"]), R=float(d["R"]), Q=float(d["Q"]),
-                  Rc=float(d["Rc"]), Tref=float(d["Tref"]), neg=el(d["neg"]), pos=el(d["pos"]),
+                  Rc=float(d["Rc"]), Tref=float(d["Tref"]), tab_T_K=arr(d["tab_T_K"], 1),
+                  neg=el(d["neg"]), pos=el(d["pos"]),
                   meta={k: d[k] for k in ("source", "tab_error") if k in d})
         nT, nZ = rom.T_degC.size, rom.SOC_pct.size
         if rom.A.shape[:2] != (nT, nZ) or rom.C.shape[:2] != (nT, nZ) or rom.D.shape[:2] != (nT, nZ):
@@ -418,7 +475,8 @@ class ROM:
         return ROM.load_json(path) if str(path).endswith(".json") else ROM.load_npz(path)
 
 
-_EL_SCALARS = ("theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL")
+_EL_SCALARS = ("theta0", "theta100")
+_EL_ARRAYS = ("soc0", "soc100", "Uocp", "Uocp1", "dUocp", "k0", "Rf", "Cdleff")
 
 
 def _json_num(v):
@@ -480,13 +538,33 @@ def _deriv(fun, th, h=1e-6):
     return (fun(th + h) - fun(th - h)) / (2 * h)
 
 
+def _synth_electrode(T_K, th, Tref, R, *, theta0, theta100, u, dudt, k0ref, Ea_k0, Rf, Ea_rf, wDL, Cdl, nDL):
+    """Tabulate one synthetic electrode: entropic OCP U(th) + (T - Tref) dU/dT(th) and its
+    theta derivative, Arrhenius k0 with a mild theta dependence, Arrhenius film
+    resistance growing with lithiation, and the double-layer Cdleff of OB_step.m:212-219
+    with a small temperature coefficient."""
+    dT = (T_K - Tref)[:, None]
+    arr_k = np.exp(Ea_k0 / R * (1.0 / Tref - 1.0 / T_K))[:, None]
+    arr_r = np.exp(Ea_rf / R * (1.0 / T_K - 1.0 / Tref))[:, None]
+    cdl = Cdl * (1.0 + 2e-3 * dT)
+    ones = np.ones((T_K.size, 1))
+    return Electrode(theta0=theta0, theta100=theta100, soc0=np.full(T_K.size, theta0),
+                     soc100=np.full(T_K.size, theta100),
+                     Uocp=u(th)[None, :] + dT * dudt(th)[None, :], Uocp1=u(th),
+                     dUocp=_deriv(u, th)[None, :] + dT * _deriv(dudt, th)[None, :],
+                     k0=k0ref * arr_k * (0.9 + 0.4 * th * (1 - th))[None, :],
+                     Rf=Rf * arr_r * (0.8 + 0.4 * th)[None, :],
+                     Cdleff=(cdl ** (2 - nDL)) * (wDL ** (nDL - 1)) * ones * np.ones_like(th)[None, :])
+
+
 def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), Ts=1.0,
-                   ntab=201) -> ROM:
+                   ntab=201, tab_T_degC=(5.0, 25.0, 45.0)) -> ROM:
     """Deterministic synthetic NMC30-like xRA ROM.
 
     Every number is fixed here; nothing random.  Local models differ smoothly with
     temperature (Arrhenius) and SOC so the bilinear blends of OB_step.m:281-285 and
-    iterEKF.m:312-313 exercise real interpolation.
+    iterEKF.m:312-313 exercise real interpolation.  The electrode handles are tabulated
+    on ``tab_T_degC`` x ``ntab`` theta points (include/mpcekf.h mpcekf_electrode).
     """
     T_degC = np.asarray(T_degC, dtype=float)
     SOC_pct = np.asarray(SOC_pct, dtype=float)
@@ -498,12 +576,13 @@ def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), T
     nT, nZ, nz = len(T_degC), len(SOC_pct), len(_OUTPUTS)
 
     th = np.linspace(0.0, 1.0, ntab)
-    neg = Electrode(theta0=0.01, theta100=0.80, Rf=2.0e-3, k0ref=2.0, Ea_k0=3.0e4,
-                    wDL=5.0, Cdl=150.0, nDL=0.95,
-                    U=_u_neg(th), dUdT=-1.0e-4 * np.exp(-5 * th), dU=_deriv(_u_neg, th))
-    pos = Electrode(theta0=0.93, theta100=0.40, Rf=3.0e-3, k0ref=4.0, Ea_k0=4.0e4,
-                    wDL=5.0, Cdl=120.0, nDL=0.93,
-                    U=_u_pos(th), dUdT=-0.5e-4 * (1 - th), dU=_deriv(_u_pos, th))
+    T_K = np.asarray(tab_T_degC, dtype=float) + 273.15
+    neg = _synth_electrode(T_K, th, Tref, R, theta0=0.01, theta100=0.80, u=_u_neg,
+                           dudt=lambda x: -1.0e-4 * np.exp(-5 * x), k0ref=2.0, Ea_k0=3.0e4, Rf=2.0e-3,
+                           Ea_rf=1.0e4, wDL=5.0, Cdl=150.0, nDL=0.95)
+    pos = _synth_electrode(T_K, th, Tref, R, theta0=0.93, theta100=0.40, u=_u_pos,
+                           dudt=lambda x: -0.5e-4 * (1 - x), k0ref=4.0, Ea_k0=4.0e4, Rf=3.0e-3,
+                           Ea_rf=1.0e4, wDL=5.0, Cdl=120.0, nDL=0.93)
     res0n = -Ts * (neg.theta100 - neg.theta0) / (3600 * Q)
     res0p = -Ts * (pos.theta100 - pos.theta0) / (3600 * Q)
 
@@ -533,7 +612,7 @@ def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), T
                 C[t, z, r, n] = res0n if r0 == "n" else (res0p if r0 == "p" else 0.0)
     rom = ROM(T_degC=T_degC, SOC_pct=SOC_pct, Ts=float(Ts), A=A, C=C, D=D,
               names=[o[0] for o in _OUTPUTS], xloc=np.array([o[1] for o in _OUTPUTS]),
-              F=F, R=R, Q=Q, Rc=8.0e-4, Tref=Tref, neg=neg, pos=pos,
-              meta={"kind": "synthetic-NMC30-like", "version": 1})
+              F=F, R=R, Q=Q, Rc=8.0e-4, Tref=Tref, tab_T_K=T_K, neg=neg, pos=pos,
+              meta={"kind": "synthetic-NMC30-like", "version": 2})
     rom.validate()
     return rom

@@ -95,10 +95,12 @@ enum { TF_negIfdl, TF_posIfdl, TF_negIf, TF_posIf, TF_negIdl, TF_posIdl, TF_negP
 
 enum { ST_ERROR = 1, ST_LOCKOUT = 2, ST_THETAE_NEG = 4 };
 
+/* cellData.function.{neg,pos} tabulated on (rom.TK x uniform theta over [0,1]) */
 typedef struct {
-  double theta0, theta100, Rf, k0ref, Ea, wDL, Cdl, nDL;
-  int ntab;
-  const double *U, *dUdT, *dU;
+  double theta0, theta100;                       /* zero-argument calls (OB_step.m:207-210) */
+  const double *soc0, *soc100;                   /* [ntemp] */
+  const double *Uocp, *dUocp, *k0, *Rf, *Cdleff; /* [ntemp][ntheta] */
+  const double *Uocp1;                           /* [ntheta] one-argument Uocp (EKFmatsHandler.m:96) */
 } orc_electrode;
 
 typedef struct {
@@ -111,6 +113,8 @@ typedef struct {
   const int32_t *tf; /* [nz] TF_* codes   */
   const double *xloc;
   double F, R, Q, Rc, Tref;
+  int ntheta, ntemp;
+  const double *TK; /* [ntemp] table temperatures (K, ascending) */
   orc_electrode neg, pos;
 } orc_rom;
 
@@ -183,14 +187,45 @@ static double tab_interp(const double *tab, int n, double x) {
   double f = t - (double)i;
   return tab[i] + f * (tab[i + 1] - tab[i]);
 }
-static double fsoc(const orc_electrode *e, double z) { return e->theta0 + z * (e->theta100 - e->theta0); }
-static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab_interp(e->U, e->ntab, th) + (T - r->Tref) * tab_interp(e->dUdT, e->ntab, th);
+/* the table temperature bracket of T: clamp to the grid ends, j = last index with
+ * TK[j] <= T (at most ntemp - 2), g = (T - TK[j]) / (TK[j+1] - TK[j]) */
+static void tidx(const orc_rom *r, double T, int *j, double *g) {
+  *j = 0;
+  *g = 0.0;
+  if (r->ntemp == 1) return;
+  double Tc = fmin(fmax(T, r->TK[0]), r->TK[r->ntemp - 1]);
+  int k = 0;
+  while (k < r->ntemp - 2 && Tc >= r->TK[k + 1]) ++k;
+  *j = k;
+  *g = (Tc - r->TK[k]) / (r->TK[k + 1] - r->TK[k]);
 }
-static double fdUocp(const orc_electrode *e, double th) { return tab_interp(e->dU, e->ntab, th); }
-static double fk0(const orc_rom *r, const orc_electrode *e, double T) {
-  return e->k0ref * exp(e->Ea / r->R * (1.0 / r->Tref - 1.0 / T));
+static double tab2(const orc_rom *r, const double *t, double th, double T) {
+  int j;
+  double g;
+  tidx(r, T, &j, &g);
+  double a = tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
+  if (r->ntemp == 1) return a;
+  double b = tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
+  return a + g * (b - a);
 }
+static double tab1T(const orc_rom *r, const double *t, double T) {
+  int j;
+  double g;
+  tidx(r, T, &j, &g);
+  if (r->ntemp == 1) return t[0];
+  return t[j] + g * (t[j + 1] - t[j]);
+}
+/* soc(z,T) (iterEKF.m:282-283; EKFmatsHandler.m:57-58; OB_step.m:64-65) */
+static double fsoc(const orc_rom *r, const orc_electrode *e, double z, double T) {
+  double s0 = tab1T(r, e->soc0, T), s1 = tab1T(r, e->soc100, T);
+  return s0 + z * (s1 - s0);
+}
+static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Uocp, th, T); }
+static double fUocp1(const orc_rom *r, const orc_electrode *e, double th) { return tab_interp(e->Uocp1, r->ntheta, th); }
+static double fdUocp(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->dUocp, th, T); }
+static double fk0(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->k0, th, T); }
+static double fRf(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Rf, th, T); }
+static double fCdl(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Cdleff, th, T); }
 static double msqrt(double x) { return x >= 0 ? sqrt(x) : NAN; }
 
 /* ----------------------------------------------------------------------- */
@@ -654,12 +689,11 @@ double orc_plant_step(const orc_ctx *X, orc_cell *s, double Iapp) {
   const orc_electrode *en = &r->neg, *ep = &r->pos;
   double T = s->Tc + 273.15;
   double F = r->F, R = r->R, Q = r->Q, Rc = r->Rc;
-  double Cdleffn = pow(en->Cdl, 2 - en->nDL) * pow(en->wDL, en->nDL - 1);
-  double Cdleffp = pow(ep->Cdl, 2 - ep->nDL) * pow(ep->wDL, ep->nDL - 1);
+  double Cdleffn = fCdl(r, en, s->SOC0n, T), Cdleffp = fCdl(r, ep, s->SOC0p, T); /* OB_step.m:212-219 */
   double SOCnAvg = s->SOCnAvg, SOCpAvg = s->SOCpAvg;
   double negSOC = SOCnAvg, posSOC = SOCpAvg;
   double cellSOC = (SOCnAvg - en->theta0) / (en->theta100 - en->theta0);
-  double dUn = fdUocp(en, SOCnAvg), dUp = fdUocp(ep, SOCpAvg);
+  double dUn = fdUocp(r, en, SOCnAvg, T), dUp = fdUocp(r, ep, SOCpAvg, T);
   double dQn = fabs(en->theta100 - en->theta0), dQp = fabs(ep->theta100 - ep->theta0);
   double res0n = -dQn / (3600 * Q - Cdleffn * dQn * dUn);
   double res0p = dQp / (3600 * Q - Cdleffp * dQp * dUp);
@@ -708,14 +742,13 @@ double orc_plant_step(const orc_ctx *X, orc_cell *s, double Iapp) {
   double th3 = fmin(fmax(yk[R_TH3] + s->SOC0p, 1e-6), 1 - 1e-6);
   double te1 = fmax(yk[R_TE1] + 1, 1e-6);
   double teE = fmax(yk[R_TEE] + 1, 1e-6);
-  double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
+  double k0n = fk0(r, en, negSOC, T), k0p = fk0(r, ep, posSOC, T); /* OB_step.m:329-330 */
   double i0n = k0n * msqrt(te1 * (1 - th0) * th0);
   double i0p = k0p * msqrt(teE * (1 - th3) * th3);
   double negEta0 = 2 * R * T / F * dasinh(yk[R_IF0] / (2 * i0n));
   double posEta3 = 2 * R * T / F * dasinh(yk[R_IF3] / (2 * i0p));
   double Uocpn0 = fUocp(r, en, th0, T), Uocpp3 = fUocp(r, ep, th3, T);
-  double Rfn = en->Rf, Rfp = ep->Rf;
-  (void)negSOC; (void)posSOC;
+  double Rfn = fRf(r, en, negSOC, T), Rfp = fRf(r, ep, posSOC, T); /* OB_step.m:339-340 */
   double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
   V = V - Rc * Iapp;
   s->SOCnAvg = SOCnAvg;
@@ -731,7 +764,7 @@ static double get_variables(const orc_ctx *X, orc_cell *s, double ik, const orc_
   const orc_electrode *en = &r->neg, *ep = &r->pos;
   int nz = r->nz;
   double xSOC = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q));
-  double SOCnAvg = fsoc(en, xSOC), SOCpAvg = fsoc(ep, xSOC);
+  double SOCnAvg = fsoc(r, en, xSOC, T), SOCpAvg = fsoc(r, ep, xSOC, T);
   if (SOCnAvg < 0) { s->warn++; SOCnAvg = 1e-6; }
   if (SOCnAvg > 1) { s->warn++; SOCnAvg = 1 - 1e-6; }
   if (SOCpAvg < 0) { s->warn++; SOCpAvg = 1e-6; }
@@ -773,13 +806,14 @@ static double get_variables(const orc_ctx *X, orc_cell *s, double ik, const orc_
   any = 0;
   for (int k = 0; k < ix->nThetae; ++k) { Z[ix->Thetae[k]] = Z[ix->Thetae[k]] + 1; any |= Z[ix->Thetae[k]] < 0; }
   if (any) { s->warn++; s->status |= ST_ERROR | ST_THETAE_NEG; return NAN; }
-  double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
+  double k0n = fk0(r, en, SOCnAvg, T), k0p = fk0(r, ep, SOCpAvg, T); /* iterEKF.m:392-393 */
   double i0n = k0n * msqrt(Z[ix->Thetae1] * (1 - Z[ix->Thetass0]) * Z[ix->Thetass0]);
   double i0p = k0p * msqrt(Z[ix->ThetaeE] * (1 - Z[ix->Thetass3]) * Z[ix->Thetass3]);
   double negEta0 = 2 * r->R * T / r->F * dasinh(If0 / (2 * i0n));
   double posEta3 = 2 * r->R * T / r->F * dasinh(If3 / (2 * i0p));
   double Uocpn0 = fUocp(r, en, Z[ix->Thetass0], T), Uocpp3 = fUocp(r, ep, Z[ix->Thetass3], T);
-  double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (ep->Rf * Z[ix->Ifdl3] - en->Rf * Z[ix->Ifdl0]);
+  double Rfn = fRf(r, en, SOCnAvg, T), Rfp = fRf(r, ep, SOCpAvg, T); /* iterEKF.m:406-407 */
+  double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (Rfp * Z[ix->Ifdl3] - Rfn * Z[ix->Ifdl0]);
   for (int k = 0; k < ix->nPosPhis; ++k) Z[ix->posPhis[k]] = Z[ix->posPhis[k]] + V;
   *Zsoc = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q));
   return V;
@@ -792,14 +826,13 @@ static void get_chat_v(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, 
   const orc_ind *ix = &X->ix;
   const orc_electrode *en = &r->neg, *ep = &r->pos;
   double xSOC = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q));
-  double SOCnAvg = fsoc(en, xSOC), SOCpAvg = fsoc(ep, xSOC);
-  (void)SOCnAvg; (void)SOCpAvg;
-  double Rfn = en->Rf, Rfp = ep->Rf;
-  double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
+  double SOCnAvg = fsoc(r, en, xSOC, T), SOCpAvg = fsoc(r, ep, xSOC, T); /* iterEKF.m:439-442: unclamped */
+  double Rfn = fRf(r, en, SOCnAvg, T), Rfp = fRf(r, ep, SOCpAvg, T);
+  double k0n = fk0(r, en, SOCnAvg, T), k0p = fk0(r, ep, SOCpAvg, T);
   double i0n = k0n * msqrt(Z[ix->Thetae1] * (1 - Z[ix->Thetass0]) * Z[ix->Thetass0]);
   double i0p = k0p * msqrt(Z[ix->ThetaeE] * (1 - Z[ix->Thetass3]) * Z[ix->Thetass3]);
   double Rctn = r->R * T / (r->F * i0n), Rctp = r->R * T / (r->F * i0p);
-  double dUn0 = fdUocp(en, Z[ix->Thetass0]), dUp3 = fdUocp(ep, Z[ix->Thetass3]);
+  double dUn0 = fdUocp(r, en, Z[ix->Thetass0], T), dUp3 = fdUocp(r, ep, Z[ix->Thetass3], T);
   for (int j = 0; j < 4; ++j) {
     double g = xi->g[j];
     int m = xi->m[j];
@@ -814,7 +847,7 @@ static void get_chat_v(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, 
       Chat[j][k] = v;
     }
   }
-  double dn = fsoc(en, 1) - fsoc(en, 0), dp = fsoc(ep, 1) - fsoc(ep, 0);
+  double dn = fsoc(r, en, 1, T) - fsoc(r, en, 0, T), dp = fsoc(r, ep, 1, T) - fsoc(r, ep, 0, T);
   double res0n = -dUn0 * r->Ts * dn / (3600 * r->Q);
   double res0p = -dUp3 * r->Ts * dp / (3600 * r->Q);
   *Chat0 = res0p - res0n;
@@ -831,12 +864,14 @@ static void get_chat_v_mb(const orc_ctx *X, const orc_cell *s, const orc_xind *x
   const orc_rom *r = X->r;
   const orc_ind *ix = &X->ix;
   const orc_electrode *en = &r->neg, *ep = &r->pos;
-  double Rfn = en->Rf, Rfp = ep->Rf;
-  double k0n = fk0(r, en, T), k0p = fk0(r, ep, T);
+  double xSOC = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q)); /* x0 = xhat(end) (iterEKF.m:449-452) */
+  double SOCnAvg = fsoc(r, en, xSOC, T), SOCpAvg = fsoc(r, ep, xSOC, T);
+  double Rfn = fRf(r, en, SOCnAvg, T), Rfp = fRf(r, ep, SOCpAvg, T);
+  double k0n = fk0(r, en, SOCnAvg, T), k0p = fk0(r, ep, SOCpAvg, T);
   double i0n = k0n * msqrt(Z[ix->Thetae1] * (1 - Z[ix->Thetass0]) * Z[ix->Thetass0]);
   double i0p = k0p * msqrt(Z[ix->ThetaeE] * (1 - Z[ix->Thetass3]) * Z[ix->Thetass3]);
   double Rctn = r->R * T / (r->F * i0n), Rctp = r->R * T / (r->F * i0p);
-  double dUn0 = fdUocp(en, Z[ix->Thetass0]), dUp3 = fdUocp(ep, Z[ix->Thetass3]);
+  double dUn0 = fdUocp(r, en, Z[ix->Thetass0], T), dUp3 = fdUocp(r, ep, Z[ix->Thetass3], T);
   const int rows[7] = {ix->Ifdl3, ix->Ifdl0, ix->If3, ix->If0, ix->PhieE, ix->Thetass3, ix->Thetass0};
   for (int k = 0; k < NX; ++k) {
     double sum[7];
@@ -851,7 +886,7 @@ static void get_chat_v_mb(const orc_ctx *X, const orc_cell *s, const orc_xind *x
     v = v + dUp3 * sum[5] - dUn0 * sum[6];
     ChV[k] = v;
   }
-  double dn = fsoc(en, 1) - fsoc(en, 0), dp = fsoc(ep, 1) - fsoc(ep, 0);
+  double dn = fsoc(r, en, 1, T) - fsoc(r, en, 0, T), dp = fsoc(r, ep, 1, T) - fsoc(r, ep, 0, T);
   double res0n = -dUn0 * r->Ts * dn / (3600 * r->Q);
   double res0p = -dUp3 * r->Ts * dp / (3600 * r->Q);
   ChV[NX] = res0p - res0n;
@@ -958,10 +993,10 @@ static int ekf_step_mb(const orc_ctx *X, orc_cell *s, double vk, double ik, doub
     const orc_electrode *en = &r->neg, *ep = &r->pos;
     double ChVz[NA];
     get_chat_v_mb(X, s, &xi, zk, Tk, ChVz);
-    double res0n = -r->Ts * (fsoc(en, 1) - fsoc(en, 0)) / (3600 * r->Q);
-    double res0p = -r->Ts * (fsoc(ep, 1) - fsoc(ep, 0)) / (3600 * r->Q);
+    double res0n = -r->Ts * (fsoc(r, en, 1, Tk) - fsoc(r, en, 0, Tk)) / (3600 * r->Q);
+    double res0p = -r->Ts * (fsoc(r, ep, 1, Tk) - fsoc(r, ep, 0, Tk)) / (3600 * r->Q);
     double xSOC = s->SOC0 - s->x0 * rs;
-    double dUn = fdUocp(en, fsoc(en, xSOC)), dUp = fdUocp(ep, fsoc(ep, xSOC));
+    double dUn = fdUocp(r, en, fsoc(r, en, xSOC, Tk), Tk), dUp = fdUocp(r, ep, fsoc(r, ep, xSOC, Tk), Tk);
     double Ch[256][NA];
     double c0[256];
     for (int q = 0; q < nz; ++q) {
@@ -1067,10 +1102,10 @@ int orc_ekf_step(const orc_ctx *X, orc_cell *s, double vk, double ik, double Tc,
     double ChV[4][NX], ChV0;
     get_chat_v(X, s, &xi, zk, Tk, ChV, &ChV0);
     const orc_electrode *en = &r->neg, *ep = &r->pos;
-    double res0n = -r->Ts * (fsoc(en, 1) - fsoc(en, 0)) / (3600 * r->Q);
-    double res0p = -r->Ts * (fsoc(ep, 1) - fsoc(ep, 0)) / (3600 * r->Q);
+    double res0n = -r->Ts * (fsoc(r, en, 1, Tk) - fsoc(r, en, 0, Tk)) / (3600 * r->Q);
+    double res0p = -r->Ts * (fsoc(r, ep, 1, Tk) - fsoc(r, ep, 0, Tk)) / (3600 * r->Q);
     double xSOC = s->SOC0 - s->x0 * (r->Ts / (3600 * r->Q));
-    double dUn = fdUocp(en, fsoc(en, xSOC)), dUp = fdUocp(ep, fsoc(ep, xSOC));
+    double dUn = fdUocp(r, en, fsoc(r, en, xSOC, Tk), Tk), dUp = fdUocp(r, ep, fsoc(r, ep, xSOC, Tk), Tk);
     double c0[256];
     for (int q = 0; q < nz; ++q) c0[q] = 0.0;
     for (int k = 0; k < ix->nPosPhis; ++k) c0[ix->posPhis[k]] = ChV0;
@@ -1144,11 +1179,11 @@ void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, c
   L->Dsoc = 0.0;
   double TK = Tc + 273.15;
   double SOCavg = zk[r->nz + 1];
-  double SOCnAvg = fsoc(en, SOCavg); /* EKFmatsHandler.m computes SOCpAvg too; unused on this path */
-  double k0n = fk0(r, en, TK), k0p = fk0(r, ep, TK);
+  double SOCnAvg = fsoc(r, en, SOCavg, TK), SOCpAvg = fsoc(r, ep, SOCavg, TK); /* EKFmatsHandler.m:57-58 */
+  double k0n = fk0(r, en, SOCnAvg, TK), k0p = fk0(r, ep, SOCpAvg, TK);
   double i0n = k0n * msqrt(zk[ix->Thetae1] * (1 - zk[ix->Thetass0]) * zk[ix->Thetass0]);
   double i0p = k0p * msqrt(zk[ix->ThetaeE] * (1 - zk[ix->Thetass3]) * zk[ix->Thetass3]);
-  double Rfn = en->Rf, Rfp = ep->Rf;
+  double Rfn = fRf(r, en, SOCnAvg, TK), Rfp = fRf(r, ep, SOCpAvg, TK); /* EKFmatsHandler.m:68-69 */
   for (int k = 0; k < NX; ++k)
     L->Cv[k] = Rfp * Crow(r, m, ix->Ifdl3)[k] - Rfn * Crow(r, m, ix->Ifdl0)[k] + Crow(r, m, ix->PhieE)[k];
   L->Cv[NX] = 0.0;
@@ -1158,7 +1193,7 @@ void orc_mats_handler(const orc_ctx *X, const orc_cell *s, const orc_xind *xi, c
   double posEta3 = 2 * r->R * TK / r->F * dasinh(zk[ix->If3] / (2 * i0p));
   double b_phi = 0.01 * 0;
   L->bv = (Upos - Uneg) + (posEta3 - negEta0) + b_phi;
-  L->bphi = fUocp(r, en, SOCnAvg, r->Tref); /* one-argument call */
+  L->bphi = fUocp1(r, en, SOCnAvg); /* one-argument call (EKFmatsHandler.m:96) */
   for (int k = 0; k < NX; ++k) L->Cphi[k] = Crow(r, m, ix->negPhise2)[k];
   L->Cphi[NX] = 0.0;
   L->Dphi = Dval(r, m, ix->negPhise2);
@@ -1373,10 +1408,9 @@ static void init_cell(const orc_ctx *X, orc_cell *s, double soc0, double tc) {
   for (size_t m = 0; m < NM; ++m)
     for (int p = 0; p < NX; ++p)
       for (int q = p; q < NX; ++q) s->S[m * NPK + PK[p][q]] = p == q ? c->SigmaX0[p] : 0.0;
-  double Tk1 = tc + 273.15;
-  (void)Tk1;
-  s->SOC0n = fsoc(&r->neg, soc0 / 100);
-  s->SOC0p = fsoc(&r->pos, soc0 / 100);
+  double Tk1 = tc + 273.15; /* OB_step.m:63-65 */
+  s->SOC0n = fsoc(r, &r->neg, soc0 / 100, Tk1);
+  s->SOC0p = fsoc(r, &r->pos, soc0 / 100, Tk1);
   s->SOCnAvg = s->SOC0n;
   s->SOCpAvg = s->SOC0p;
   s->Tc = tc;
@@ -1401,6 +1435,7 @@ typedef struct {
   double *zk, *zbk;                /* [nsteps][ncells][nz+2] zkEst, zkBound                */
   double *J_unc, *J_fin, *norm_du; /* [nsteps][ncells]       J_uncon, J_final, norm_DU     */
   int32_t *nviol;                  /* [nsteps][ncells]       viol                          */
+  const double *tc;                /* [nsteps][ncells] INPUT: TC of each step (degC), or NULL */
 } orc_traj;
 
 static void cell_step(const orc_ctx *X, orc_cell *s, double *u, double *v, double *soc, double *phise, int *nexec,
@@ -1475,6 +1510,7 @@ int orc_run_traj(const orc_rom *r, const orc_cfg *c, int ncells, const double *s
       double *zko = (tr && tr->zk) ? tr->zk + o * nzz : (zk && last) ? zk + (size_t)i * nzz : NULL;
       double *zbo = (tr && tr->zbk) ? tr->zbk + o * nzz : (zbk && last) ? zbk + (size_t)i * nzz : NULL;
       orc_mpc_out mo;
+      if (tr && tr->tc) s.Tc = tr->tc[o]; /* runMPC.m:85-92: the step's TC for all three calls */
       cell_step(&X, &s, &u[o], &v[o], &soc[o], &phise[o], &ne, zko, zbo, &mo,
                 (tr && tr->x) ? tr->x + o * (NX + 1) : NULL);
       if (tr && tr->zk && zk && last) memcpy(zk + (size_t)i * nzz, zko, nzz * sizeof(double));
@@ -1501,4 +1537,4 @@ int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, 
   return orc_run_traj(r, c, ncells, soc0, tc, nsteps, u, v, soc, phise, nexec, status, zk, zbk, NULL, nthreads);
 }
 
-int orc_version(void) { return 1; }
+int orc_version(void) { return 2; }

@@ -24,9 +24,8 @@ _ip = C.POINTER(C.c_int32)
 
 
 class _Electrode(C.Structure):
-    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("Rf", C.c_double),
-                ("k0ref", C.c_double), ("Ea", C.c_double), ("wDL", C.c_double), ("Cdl", C.c_double),
-                ("nDL", C.c_double), ("ntab", C.c_int), ("U", _dp), ("dUdT", _dp), ("dU", _dp)]
+    _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
+                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp)]
 
 
 class _Rom(C.Structure):
@@ -34,6 +33,7 @@ class _Rom(C.Structure):
                 ("T_degC", _dp), ("SOC_pct", _dp), ("Ts", C.c_double), ("A", _dp), ("C", _dp),
                 ("D", _dp), ("tf", _ip), ("xloc", _dp), ("F", C.c_double), ("R", C.c_double),
                 ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double),
+                ("ntheta", C.c_int), ("ntemp", C.c_int), ("TK", _dp),
                 ("neg", _Electrode), ("pos", _Electrode)]
 
 
@@ -116,12 +116,14 @@ class PackedRom:
         r.tf = arr([TF_CODES[n] for n in rom.names], np.int32).ctypes.data_as(_ip)
         r.xloc = _p(arr(rom.xloc))
         r.F, r.R, r.Q, r.Rc, r.Tref = rom.F, rom.R, rom.Q, rom.Rc, rom.Tref
+        r.ntheta, r.ntemp = rom.ntheta, rom.ntemp
+        r.TK = _p(arr(np.atleast_1d(rom.tab_T_K)))
         for side in ("neg", "pos"):
             e = getattr(rom, side)
             s = getattr(r, side)
-            s.theta0, s.theta100, s.Rf, s.k0ref, s.Ea = e.theta0, e.theta100, e.Rf, e.k0ref, e.Ea_k0
-            s.wDL, s.Cdl, s.nDL, s.ntab = e.wDL, e.Cdl, e.nDL, len(e.U)
-            s.U, s.dUdT, s.dU = _p(arr(e.U)), _p(arr(e.dUdT)), _p(arr(e.dU))
+            s.theta0, s.theta100 = e.theta0, e.theta100
+            for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
+                setattr(s, k, _p(arr(getattr(e, k))))
         self.s = r
 
 
@@ -150,14 +152,15 @@ def make_cfg(**kw):
 
 class _Traj(C.Structure):
     _fields_ = [("x", _dp), ("zk", _dp), ("zbk", _dp), ("J_unc", _dp), ("J_fin", _dp), ("norm_du", _dp),
-                ("nviol", _ip)]
+                ("nviol", _ip), ("tc", _dp)]
 
 
-def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, **cfg):
+def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, tc_traj=None, **cfg):
     """Batched closed loop on the CPU. Returns dict of [nsteps, ncells] arrays.
 
     traj=True adds the per-step diagnostics of runMPC.m:106-111 / mpcData.cost:
-    x [nsteps, n, 6], zk_traj / zbk_traj [nsteps, n, nz+2], J_unc, J_fin, norm_du, nviol."""
+    x [nsteps, n, 6], zk_traj / zbk_traj [nsteps, n, nz+2], J_unc, J_fin, norm_du, nviol.
+    tc_traj [nsteps, ncells] (degC): the temperature of each step (tc is the initial one)."""
     soc0 = np.ascontiguousarray(soc0, dtype=np.float64)
     tc = np.ascontiguousarray(tc, dtype=np.float64)
     n = soc0.shape[0]
@@ -169,6 +172,12 @@ def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, **cfg):
     zk = np.zeros((n, rom.nz + 2)) if want_zk else None
     zbk = np.zeros((n, rom.nz + 2)) if want_zk else None
     tr = None
+    tcs = None
+    if tc_traj is not None:
+        tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc_traj, dtype=np.float64).reshape(nsteps, -1),
+                                                   (nsteps, n)))
+        tr = _Traj()
+        tr.tc = _p(tcs)
     if traj:
         out["x"] = np.zeros((nsteps, n, 6))
         out["zk_traj"] = np.zeros((nsteps, n, rom.nz + 2))
@@ -177,7 +186,7 @@ def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, **cfg):
             out[k] = np.zeros((nsteps, n))
         out["nviol"] = np.zeros((nsteps, n), dtype=np.int32)
         tr = _Traj(_p(out["x"]), _p(out["zk_traj"]), _p(out["zbk_traj"]), _p(out["J_unc"]), _p(out["J_fin"]),
-                   _p(out["norm_du"]), out["nviol"].ctypes.data_as(_ip))
+                   _p(out["norm_du"]), out["nviol"].ctypes.data_as(_ip), _p(tcs) if tcs is not None else None)
     rc = lib().orc_run_traj(C.byref(pr.s), C.byref(c), n, _p(soc0), _p(tc), nsteps, _p(out["u"]),
                             _p(out["v"]), _p(out["soc"]), _p(out["phise"]),
                             out["nexec"].ctypes.data_as(_ip), out["status"].ctypes.data_as(_ip),

@@ -161,7 +161,9 @@ def stable_two_nearest(d):
 # cellData.function.* (tabulated semantics, see rom.py)
 # ---------------------------------------------------------------------------
 class Cell:
-    """Reads the ROM *data*; re-implements the function semantics itself."""
+    """Reads the ROM *data*; re-implements the tabulated handle semantics itself
+    (include/mpcekf.h mpcekf_electrode): [ntemp, ntheta] tables, theta interpolated
+    on a uniform [0, 1] grid, then T linearly between the two bracketing grid rows."""
 
     def __init__(self, rom):
         self.rom = rom
@@ -170,6 +172,7 @@ class Cell:
         self.Q = rom.Q
         self.Rc = rom.Rc
         self.Tref = rom.Tref
+        self.TK = [float(t) for t in np.atleast_1d(rom.tab_T_K)]
         self.e = {"neg": rom.neg, "pos": rom.pos}
 
     @staticmethod
@@ -185,25 +188,51 @@ class Cell:
         f = t - i
         return float(tab[i] + f * (tab[i + 1] - tab[i]))
 
-    def soc(self, s, z, T=None):
+    def _tj(self, T):
+        TK = self.TK
+        if len(TK) == 1:
+            return 0, 0.0
+        Tc = min(max(T, TK[0]), TK[-1])
+        j = 0
+        while j < len(TK) - 2 and Tc >= TK[j + 1]:
+            j += 1
+        return j, (Tc - TK[j]) / (TK[j + 1] - TK[j])
+
+    def _tab2(self, tab, th, T):
+        j, g = self._tj(T)
+        a = self._interp(tab[j], th)
+        if len(self.TK) == 1:
+            return a
+        b = self._interp(tab[j + 1], th)
+        return a + g * (b - a)
+
+    def soc(self, s, z, T):
         e = self.e[s]
-        return e.theta0 + z * (e.theta100 - e.theta0)
+        j, g = self._tj(T)
+        if len(self.TK) == 1:
+            s0, s1 = float(e.soc0[0]), float(e.soc100[0])
+        else:
+            s0 = e.soc0[j] + g * (e.soc0[j + 1] - e.soc0[j])
+            s1 = e.soc100[j] + g * (e.soc100[j + 1] - e.soc100[j])
+        return s0 + z * (s1 - s0)
 
     def Uocp(self, s, th, T=None):
-        e = self.e[s]
-        if T is None:
-            T = self.Tref
-        return self._interp(e.U, th) + (T - self.Tref) * self._interp(e.dUdT, th)
+        if T is None:                                  # one-argument call (EKFmatsHandler.m:96)
+            return self._interp(self.e[s].Uocp1, th)
+        return self._tab2(self.e[s].Uocp, th, T)
 
-    def dUocp(self, s, th, T=None):
-        return self._interp(self.e[s].dU, th)
+    def dUocp(self, s, th, T):
+        return self._tab2(self.e[s].dUocp, th, T)
 
     def k0(self, s, th, T):
-        e = self.e[s]
-        return e.k0ref * math.exp(e.Ea_k0 / self.R * (1.0 / self.Tref - 1.0 / T))
+        return self._tab2(self.e[s].k0, th, T)
 
-    def Rf(self, s, th=None, T=None):
-        return self.e[s].Rf
+    def Rf(self, s, th, T):
+        return self._tab2(self.e[s].Rf, th, T)
+
+    def Cdleff(self, s, th, T):
+        """Cdl(th,T)^(2-nDL) * wDL(th,T)^(nDL-1) (OB_step.m:212-219), tabulated by the exporter."""
+        return self._tab2(self.e[s].Cdleff, th, T)
 
 
 # ---------------------------------------------------------------------------
@@ -277,10 +306,8 @@ def ob_step(Iapp, Tc, cs):
     F, R, Q, Rc = cell.F, cell.R, cell.Q, cell.Rc
     e_n, e_p = cell.e["neg"], cell.e["pos"]
     theta0n, theta0p, theta100n, theta100p = e_n.theta0, e_p.theta0, e_n.theta100, e_p.theta100
-    wDLn, wDLp, Cdln, Cdlp = e_n.wDL, e_p.wDL, e_n.Cdl, e_p.Cdl
-    nDLn, nDLp = e_n.nDL, e_p.nDL
-    Cdleffn = (Cdln ** (2 - nDLn)) * (wDLn ** (nDLn - 1))     # OB_step.m:218
-    Cdleffp = (Cdlp ** (2 - nDLp)) * (wDLp ** (nDLp - 1))
+    Cdleffn = cell.Cdleff("neg", cs["SOC0n"], T)               # OB_step.m:212-219 at SOC0n/p
+    Cdleffp = cell.Cdleff("pos", cs["SOC0p"], T)
     SOCnAvg, SOCpAvg = cs["SOCnAvg"], cs["SOCpAvg"]
     negSOC, posSOC = SOCnAvg, SOCpAvg
     cellSOC = (SOCnAvg - theta0n) / (theta100n - theta0n)      # OB_step.m:228
@@ -960,13 +987,15 @@ RUNMPC_DEFAULTS = dict(Ts=1.0, SigmaV=1e-3, SigmaW=1e2, Np=5, Nc=2, targetSOC=95
                        phise_min=0.08, z_max=0.95, z_tol=0.0, constraints=(1, 1, 1))
 
 
-def run_cell(rom, SOC0, TC, nsteps, cfg=None, record_state=False):
-    """Closed loop for ONE cell (runMPC.m:72-112).  Returns dict of trajectories."""
+def run_cell(rom, SOC0, TC, nsteps, cfg=None, record_state=False, tc_traj=None):
+    """Closed loop for ONE cell (runMPC.m:72-112).  Returns dict of trajectories.
+    tc_traj [nsteps] (degC): the temperature passed to OB_step / iterEKF / EKFmatsHandler
+    at each step (runMPC.m:85-92 passes TC); TC is the initial one (initKF, first OB_step)."""
     with np.errstate(all="ignore"):
-        return _run_cell(rom, SOC0, TC, nsteps, cfg, record_state)
+        return _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj)
 
 
-def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state):
+def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
     c = dict(RUNMPC_DEFAULTS)
     if cfg:
         c.update(cfg)
@@ -983,6 +1012,8 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state):
     out["zbk"] = np.full((nsteps, nz + 2), NAN)
     out["status"] = np.zeros(nsteps, dtype=np.int64)
     for k in range(nsteps):
+        if tc_traj is not None:
+            TC = float(tc_traj[k])
         V = ob_step(uk, TC, cs)
         zk, zbk, Xind = iter_ekf(ekf, V, uk, TC)
         if ekf["status"] & ST_ERROR:

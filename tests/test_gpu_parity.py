@@ -334,3 +334,40 @@ def test_json_exchanged_rom_is_bit_identical_on_gpu(rom, M, tmp_path):
     b = M.runMPC(q, soc0, tc, 60)
     for k in ("u", "v", "soc", "phise", "nexec"):
         assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=True), k
+
+
+def test_temperature_profile_matches_oracle_and_golden(P, oc, M):
+    """A temperature per step (runMPC.m:85-92 passes TC to OB_step, iterEKF and
+    EKFmatsHandler every call): bitwise against the C oracle over the fused path, and
+    within 1e-9 of the numpy restatement's fixture."""
+    g = _golden("tprofile4_300")
+    rom = P.make_synth_rom()
+    steps = g["u"].shape[0]
+    out = M.runMPC(rom, g["soc0"], g["tc"], steps, tc_traj=g["tc_traj"])
+    ref = oc.run(rom, g["soc0"], g["tc"], steps, nthreads=4, tc_traj=g["tc_traj"])
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        _bitwise(out[k], ref[k], k)
+    np.testing.assert_array_equal(out["status"], g["status"])
+    for k in ("u", "v", "soc", "phise"):
+        assert _rel(out[k], g[k]).max() <= 1e-9, k
+
+
+def test_temperature_through_stage_entry_points(rom, M):
+    """The stage ABI takes the temperature per call (OB_step(Iapp,Tc,..),
+    iterEKF(vk,ik,Tk,..), EKFmatsHandler(..,Tk)): a varying profile through the stage
+    calls equals the fused step given the same profile, bit for bit."""
+    n, steps = 128, 30
+    soc0, tc = batch_inputs(n, seed=17)
+    prof = tc[None, :] + 3.0 * np.sin(np.arange(steps)[:, None] / 5.0 + np.arange(n)[None, :] / 9.0)
+    fused = M.runMPC(rom, soc0, tc, steps, tc_traj=prof)
+    with M.Context(rom, n) as ctx:
+        ctx.init_cells(soc0, tc)
+        uk = np.zeros(n)
+        for k in range(steps):
+            v = ctx.OB_step(uk, prof[k])
+            zk, zb, xind = ctx.iterEKF(v, uk, prof[k])
+            lin = ctx.EKFmatsHandler(zk, xind, prof[k])
+            uk, ne = ctx.iterMPC(lin, zk[:, -1])
+            np.testing.assert_array_equal(v, fused["v"][k])
+            np.testing.assert_array_equal(uk, fused["u"][k])
+            np.testing.assert_array_equal(ne, fused["nexec"][k])

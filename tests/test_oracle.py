@@ -281,3 +281,20 @@ def test_tail_is_ill_conditioned(rom, oc):
     assert r[:2400].max() <= 1e-9
     assert r.max() > 1e-6
     assert (a["nexec"][2400:] == 100).sum() > 100
+
+
+def test_c_oracle_temperature_profile_matches_golden(P, oc):
+    """A per-step temperature (OB_step(Iapp,Tc,..), iterEKF(vk,ik,Tk,..),
+    EKFmatsHandler(..,Tk) every call) through the C oracle against the numpy
+    restatement's fixture: ramps with a ripple, a profile through set-points and past
+    the table grid ends."""
+    g = load("tprofile4_300")
+    rom = P.make_synth_rom()
+    r = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=4, tc_traj=g["tc_traj"])
+    np.testing.assert_array_equal(r["status"], g["status"])
+    for k in ("u", "v", "soc", "phise"):
+        assert rel(r[k], g[k]).max() <= 1e-12, k
+    np.testing.assert_array_equal(r["nexec"], g["nexec"])
+    # the profile matters: a constant TC gives different trajectories
+    c = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=4)
+    assert rel(c["v"], g["v"]).max() > 1e-4

@@ -56,11 +56,37 @@ def test_rom_npz_roundtrip(rom, tmp_path, P):
 
 
 def test_tabulated_functions(rom):
+    """The defined (theta, T) table semantics (include/mpcekf.h mpcekf_electrode)."""
+    from importlib import import_module
+    R = import_module("mpc-ekf4fastcharge_amd.rom")
     f = rom.fn("neg")
-    assert np.isnan(f.Uocp(float("nan")))
-    assert f.Uocp(-1.0) == f.Uocp(0.0) and f.Uocp(2.0) == f.Uocp(1.0)
-    assert f.Uocp(0.3) == f.Uocp(0.3, rom.Tref)          # 1-arg call = Tref (EKFmatsHandler.m:96)
-    assert f.soc(0.0) == rom.neg.theta0 and f.soc(1.0) == rom.neg.theta100
+    T0, T1 = rom.tab_T_K[0], rom.tab_T_K[-1]
+    assert np.isnan(f.Uocp(float("nan"), 300.0))
+    assert f.Uocp(-1.0, 300.0) == f.Uocp(0.0, 300.0) and f.Uocp(2.0, 300.0) == f.Uocp(1.0, 300.0)
+    # T clamps to the grid ends; a grid temperature reads its own row exactly
+    assert f.k0(0.37, T0 - 50) == f.k0(0.37, T0) and f.k0(0.37, T1 + 50) == f.k0(0.37, T1)
+    assert f.Rf(0.5, rom.tab_T_K[1]) == R.interp_tab(rom.neg.Rf[1], 0.5)
+    # between rows: a + g (b - a) of the two theta interpolations
+    Tm = 0.25 * rom.tab_T_K[0] + 0.75 * rom.tab_T_K[1]
+    a, b = R.interp_tab(rom.neg.Uocp[0], 0.3), R.interp_tab(rom.neg.Uocp[1], 0.3)
+    g = (Tm - rom.tab_T_K[0]) / (rom.tab_T_K[1] - rom.tab_T_K[0])
+    assert f.Uocp(0.3, Tm) == a + g * (b - a)
+    # one-argument call reads its own table (EKFmatsHandler.m:96)
+    assert f.Uocp(0.3) == R.interp_tab(rom.neg.Uocp1, 0.3)
+    assert f.soc(0.0, 300.0) == rom.neg.theta0 and f.soc(1.0, 300.0) == rom.neg.theta100
+    # the synthetic Uocp is linear in T, so the Tref row agrees with the 1-arg table
+    assert abs(f.Uocp(0.3, rom.Tref) - f.Uocp(0.3)) < 1e-15
+
+
+def test_rom_rejects_bad_tables(rom):
+    r = copy.deepcopy(rom)
+    r.neg.k0 = r.neg.k0[:, :-1]
+    with pytest.raises(ValueError, match="k0"):
+        r.validate()
+    r = copy.deepcopy(rom)
+    r.tab_T_K = r.tab_T_K[::-1].copy()
+    with pytest.raises(ValueError, match="ascending"):
+        r.validate()
 
 
 def _matlab_jsonencode_quirks(d):
@@ -68,7 +94,7 @@ def _matlab_jsonencode_quirks(d):
     not: 1-element arrays become bare numbers, trailing singleton dims vanish from
     size(), NaN becomes null."""
     d = copy.deepcopy(d)
-    d["neg"]["U"]["data"][0] = None               # NaN entry -> null
+    d["neg"]["Uocp1"]["data"][0] = None           # NaN entry -> null
     one = {"shape": [1, 1], "order": "F", "data": 2.5}
     d["neg"]["Rf_tab_probe"] = one                # unknown keys are ignored
     return d
@@ -100,7 +126,19 @@ def test_rom_json_matlab_quirks_and_errors(rom):
     ROMc = type(rom)
     d = _matlab_jsonencode_quirks(rom.to_json_dict())
     q = ROMc.from_json_dict(d)
-    assert np.isnan(q.neg.U[0]) and np.array_equal(q.neg.U[1:], rom.neg.U[1:])
+    assert np.isnan(q.neg.Uocp1[0]) and np.array_equal(q.neg.Uocp1[1:], rom.neg.Uocp1[1:])
+    # a one-temperature table grid: MATLAB writes the [1, ntheta] tables and a bare T
+    d2 = rom.to_json_dict()
+    d2["tab_T_K"] = {"shape": [1, 1], "order": "F", "data": 298.15}
+    for side in ("neg", "pos"):
+        for k in ("Uocp", "dUocp", "k0", "Rf", "Cdleff"):
+            row = getattr(rom, side).__dict__[k][1]
+            d2[side][k] = {"shape": [1, row.size], "order": "F", "data": list(row)}
+        for k in ("soc0", "soc100"):
+            d2[side][k] = {"shape": [1, 1], "order": "F", "data": float(getattr(rom, side).__dict__[k][1])}
+    q2 = ROMc.from_json_dict(d2)
+    assert q2.ntemp == 1 and q2.neg.k0.shape == (1, rom.ntheta)
+    q2.validate()
     # nz = 1: MATLAB reports size(D) as [nT nZ] (trailing 1 dropped)
     d1 = rom.to_json_dict()
     nT, nZ = rom.nT, rom.nZ
@@ -147,7 +185,8 @@ def test_matlab_exporter_writes_every_loaded_key():
     for k in ("T_degC", "SOC_pct", "Ts", "A", "C", "D", "names", "xloc", "F", "R", "Q", "Rc", "Tref",
               "neg", "pos"):
         assert f"out.{k} " in src or f"out.{k}=" in src or f"out.{k} =" in src, k
-    for k in ("theta0", "theta100", "Rf", "k0ref", "Ea_k0", "wDL", "Cdl", "nDL", "U", "dUdT", "dU"):
+    assert "out.tab_T_K " in src
+    for k in ("theta0", "theta100", "soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
         assert f"e.{k} " in src, k
-    assert "'mpcekf-rom-v1'" in src and "'order', 'F'" in src
+    assert "'mpcekf-rom-v2'" in src and "'order', 'F'" in src
     assert (root / "mpcekf_pack_models.m").exists() and (root / "mpcekf_check_tables.m").exists()

@@ -31,8 +31,9 @@ def rom_hash(rom):
     return h.hexdigest()
 
 
-def run_cells(rom, soc0, tc, steps, cfg=None):
-    outs = [O.run_cell(rom, s, t, steps, cfg) for s, t in zip(soc0, tc)]
+def run_cells(rom, soc0, tc, steps, cfg=None, tc_traj=None):
+    outs = [O.run_cell(rom, s, t, steps, cfg, tc_traj=None if tc_traj is None else tc_traj[:, i])
+            for i, (s, t) in enumerate(zip(soc0, tc))]
     res = {k: np.stack([o[k] for o in outs], axis=1) for k in ("u", "v", "soc", "phise", "nexec")}
     res["status"] = np.array([o["status"][-1] for o in outs])
     res["zk_last"] = np.stack([o["zk"][-1] for o in outs])
@@ -49,8 +50,29 @@ def make_mb(rom, hsh):
     np.savez_compressed(os.path.join(OUT, "mb_batch4_200.npz"), rom_hash=hsh, soc0=soc0, tc=tc, **r)
 
 
+def tprofile(steps):
+    k = np.arange(steps)[:, None]
+    base = np.array([[20.0, 25.0, 10.0, 30.0]])
+    slope = np.array([[0.02, -0.01, 0.15, 0.05]])
+    ripple = np.array([[1.0, 2.5, 0.5, 0.0]])
+    return base + slope * k + ripple * np.sin(k / 17.0)
+
+
+def make_tprofile(rom, hsh):
+    soc0 = np.array([10.0, 35.0, 20.0, 60.0])
+    steps = 300
+    tct = tprofile(steps)
+    r = run_cells(rom, soc0, tct[0], steps, tc_traj=tct)
+    np.savez_compressed(os.path.join(OUT, "tprofile4_300.npz"), rom_hash=hsh, soc0=soc0, tc=tct[0], tc_traj=tct, **r)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--tprofile-only" in sys.argv:
+        P = importlib.import_module("mpc-ekf4fastcharge_amd")
+        rom = P.make_synth_rom()
+        make_tprofile(rom, rom_hash(rom))
+        return
     if "--mb-only" in sys.argv:
         P = importlib.import_module("mpc-ekf4fastcharge_amd")
         rom = P.make_synth_rom()
@@ -82,6 +104,10 @@ def main():
                         tc=[25.0, 22.0], **r)
     # 5. model-blend EKF variant
     make_mb(rom, hsh)
+    # 5b. a temperature profile per step (OB_step / iterEKF / EKFmatsHandler take Tc every
+    #     call): warming ramps with a ripple, one profile crossing a set-point and the table
+    #     grid ends (0 and 50 degC, clamped), 300 steps
+    make_tprofile(rom, hsh)
     # 6. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
     rng = np.random.default_rng(11)
     n = 24
