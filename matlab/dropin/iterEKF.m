@@ -1,0 +1,16 @@
+function [zk,boundzk,ekfData,Xind] = iterEKF(vk,ik,Tk,ekfData)
+% Drop-in for UTILITY/iterEKF.m:30 over the MI355X library (mpcekf_ekf_step): zk and
+% boundzk are (nz+2) x ncells, Xind.theT / theZ / gamma 4 x ncells (1-based set-point
+% indices as the reference's), Xind.model the library's 0-based model index.
+  S = mpcekf_session('get');
+  n = numel(vk);
+  if any(Tk > 100), Tk = Tk - 273.15; end                    % the library takes degC
+  [zk, boundzk, xm, xg] = mpcekf_mex('ekf', S.h, reshape(vk, 1, n), reshape(ik .* ones(1, n), 1, n), ...
+                                     reshape(Tk .* ones(1, n), 1, n));
+  nZ = numel(ekfData.ROM.xraData.SOC);
+  Xind = struct('gamma', xg, 'theT', double(idivide(xm, int32(nZ))) + 1, 'theZ', double(mod(xm, nZ)) + 1, ...
+                'model', xm);
+  st = mpcekf_mex('get_state', S.h);
+  ekfData.x0 = st.scal(3, :);  ekfData.SigmaX0 = st.scal(4, :);  ekfData.priorI = st.scal(5, :);
+  ekfData.status = st.status;  ekfData.warnCount = st.warn;
+end

@@ -28,35 +28,29 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
 %
 % Every array is written as {"shape": size(X), "order": "F", "data": X(:)'} so the
 % loader needs no knowledge of MATLAB's N-D jsonencode nesting.
-  if nargin < 3 || isempty(ntheta), ntheta = 101; end
+  if nargin < 3, ntheta = []; end
+  if nargin < 4, TdegC = []; end
   S = load(matFile);
   if isfield(S, 'ROM'), ROM = S.ROM; else, f = fieldnames(S); ROM = S.(f{1}); end
-  cd = ROM.cellData;  fn = cd.function;  Tref = 298.15;
-  if nargin < 4 || isempty(TdegC)
-    TdegC = linspace(min(ROM.xraData.T) - 10, max(ROM.xraData.T) + 10, 6);
-  end
-  assert(numel(TdegC) >= 1 && numel(TdegC) <= 8 && all(diff(TdegC) > 0), ...
-         'mpcekf_export_rom: 1..8 ascending table temperatures');
-  TK = TdegC(:)' + 273.15;
-  th = linspace(0, 1, ntheta);
+  R = mpcekf_rom_struct(ROM, ntheta, TdegC);
+  fn = ROM.cellData.function;
+  th = linspace(0, 1, size(R.neg.Uocp, 2));
 
   out = struct();
   out.format = 'mpcekf-rom-v2';
   out.source = matFile;
-  out.T_degC = arr(ROM.xraData.T(:)');
-  out.SOC_pct = arr(ROM.xraData.SOC(:)');
-  out.Ts = ROM.xraData.Tsamp;
-  [A, C, D, names, xloc] = mpcekf_pack_models(ROM);
-  out.A = arr(A);  out.C = arr(C);  out.D = arr(D);
-  out.names = names;                       % cellstr, tfData.names order
-  out.xloc = arr(xloc(:)');
-  out.F = cd.const.F;  out.R = cd.const.R;
-  out.Q = fn.const.Q();  out.Rc = fn.const.Rc();  out.Tref = Tref;
-  out.tab_T_K = arr(TK);
-  out.neg = electrode(fn.neg, th, TK);
-  out.pos = electrode(fn.pos, th, TK);
-  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, out.neg, th, TK), ...
-                         'pos', mpcekf_check_tables(fn.pos, out.pos, th, TK));
+  out.T_degC = arr(R.T_degC);
+  out.SOC_pct = arr(R.SOC_pct);
+  out.Ts = R.Ts;
+  out.A = arr(R.A);  out.C = arr(R.C);  out.D = arr(R.D);
+  out.names = R.names;                     % cellstr, tfData.names order
+  out.xloc = arr(R.xloc);
+  out.F = R.F;  out.R = R.R;  out.Q = R.Q;  out.Rc = R.Rc;  out.Tref = R.Tref;
+  out.tab_T_K = arr(R.tab_T_K);
+  out.neg = jsonify(R.neg);
+  out.pos = jsonify(R.pos);
+  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, out.neg, th, R.tab_T_K), ...
+                         'pos', mpcekf_check_tables(fn.pos, out.pos, th, R.tab_T_K));
 
   fid = fopen(jsonFile, 'w');
   assert(fid > 0, 'mpcekf_export_rom: cannot open %s', jsonFile);
@@ -64,28 +58,12 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
   fclose(fid);
 end
 
-function e = electrode(f, th, TK)
-  nt = numel(TK);  nth = numel(th);
+function e = jsonify(t)
   e = struct();
-  e.theta0 = f.theta0();  e.theta100 = f.theta100();
-  e.soc0 = arr(arrayfun(@(T) f.soc(0, T), TK));
-  e.soc100 = arr(arrayfun(@(T) f.soc(1, T), TK));
-  [U, dU, K0, RF, CDL] = deal(zeros(nt, nth));
-  nDL = f.nDL();
-  for j = 1:nt
-    T = TK(j);
-    U(j, :) = arrayfun(@(t) f.Uocp(t, T), th);
-    dU(j, :) = arrayfun(@(t) f.dUocp(t, T), th);
-    K0(j, :) = arrayfun(@(t) f.k0(t, T), th);
-    RF(j, :) = arrayfun(@(t) f.Rf(t, T), th);
-    CDL(j, :) = arrayfun(@(t) f.Cdl(t, T)^(2 - nDL) * f.wDL(t, T)^(nDL - 1), th);
-  end
-  e.Uocp = arr(U);  e.dUocp = arr(dU);  e.k0 = arr(K0);  e.Rf = arr(RF);  e.Cdleff = arr(CDL);
-  try
-    e.Uocp1 = arr(arrayfun(@(t) f.Uocp(t), th));         % EKFmatsHandler.m:96, one argument
-  catch
-    e.Uocp1 = arr(arrayfun(@(t) f.Uocp(t, 298.15), th)); % a handle that needs T: Tref
-  end
+  e.theta0 = t.theta0;  e.theta100 = t.theta100;
+  e.soc0 = arr(t.soc0);  e.soc100 = arr(t.soc100);
+  e.Uocp = arr(t.Uocp);  e.dUocp = arr(t.dUocp);  e.k0 = arr(t.k0);  e.Rf = arr(t.Rf);
+  e.Cdleff = arr(t.Cdleff);  e.Uocp1 = arr(t.Uocp1);
 end
 
 function a = arr(X)

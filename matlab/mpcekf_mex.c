@@ -1,0 +1,273 @@
+/*
+ * mpcekf_mex.c -- MEX gateway from MATLAB to the MI355X library (include/mpcekf.h).
+ *
+ * Build (on a machine with MATLAB and the built library; not buildable in this
+ * repository's container, which has no MATLAB):
+ *   mex -R2018a -I../include mpcekf_mex.c -L../mpc-ekf4fastcharge_amd/_build -lmpcekf
+ *
+ * One command string per C-ABI entry point, the context kept as a uint64 handle:
+ *   h                 = mpcekf_mex('create', R, cfg, device, ncells)   mpcekf_ctx_create
+ *                       R: struct from mpcekf_rom_struct(ROM); cfg: struct of mpcekf_config
+ *                       fields (missing fields keep the runMPC.m defaults)
+ *                       mpcekf_mex('destroy', h)                       mpcekf_ctx_destroy
+ *                       mpcekf_mex('init', h, soc0_pct, tc_degC)       mpcekf_init_cells
+ *   [u,v,soc,phise,nexec] = mpcekf_mex('step', h, nsteps, tc)          mpcekf_step
+ *                       tc: [] or ncells x nsteps (degC); outputs ncells x nsteps
+ *   v                 = mpcekf_mex('plant', h, iapp, tc)               mpcekf_plant_step   (OB_step.m:1)
+ *   [zk,zbk,xm,xg]    = mpcekf_mex('ekf', h, vk, ik, tk)               mpcekf_ekf_step     (iterEKF.m:30)
+ *   lin               = mpcekf_mex('linearize', h, zk, xm, xg, tk)     mpcekf_linearize    (EKFmatsHandler.m:1)
+ *   [uk,nexec]        = mpcekf_mex('mpc', h, lin, soc_k1)              mpcekf_mpc_step     (iterMPC.m:1)
+ *   [DU,lambda,nexec] = mpcekf_mex('hildreth', E, F, M, gamma, lambda0, maxIter)   (hildreth.m:1)
+ *   [Phi,G]           = mpcekf_mex('predmat', a, C, D, Np, Nc)         (predMat.m:1, A = diag(a), B = 1)
+ *   st                = mpcekf_mex('get_state', h)    /  mpcekf_mex('set_state', h, st)
+ * Per-cell vectors are 1 x ncells or ncells x 1; zk / zbk are (nz+2) x ncells, xm / xg
+ * 4 x ncells (xm: 0-based model index t*nZ+z), lin 35 x ncells -- MATLAB's column-major
+ * k x ncells is the library's cell-major [ncells][k], so no copy is made for them.
+ * Arrays the library reads row-major (the ROM's A/C/D, the electrode tables, hildreth's
+ * E and M) are transposed here from MATLAB's column-major order.
+ * Library failures raise a MATLAB error with mpcekf_last_error(); per-cell soft
+ * failures stay in the status word (get_state), as in the C-ABI.
+ */
+#include <stdint.h>
+#include <string.h>
+
+#include "matrix.h"
+#include "mex.h"
+#include "mpcekf.h"
+
+static void chk(int rc) {
+  if (rc != MPCEKF_OK) mexErrMsgIdAndTxt("mpcekf:lib", "mpcekf error %d: %s", rc, mpcekf_last_error());
+}
+
+static mpcekf_ctx *handle(const mxArray *a) {
+  if (!mxIsUint64(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("mpcekf:arg", "expected a uint64 handle");
+  return (mpcekf_ctx *)(uintptr_t)(*(uint64_t *)mxGetData(a));
+}
+
+static double scalar(const mxArray *a, const char *what) {
+  if (!a || !mxIsDouble(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected a double scalar", what);
+  return mxGetScalar(a);
+}
+
+static const double *dvec(const mxArray *a, size_t n, const char *what) {
+  if (!a || !mxIsDouble(a) || mxIsComplex(a) || mxGetNumberOfElements(a) != n)
+    mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected %zu real doubles", what, n);
+  return mxGetDoubles(a);
+}
+
+/* MATLAB column-major N-D array -> C row-major copy (same dims) */
+static double *rowmajor(const mxArray *a, const char *what) {
+  if (!a || !mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected a real double array", what);
+  const mwSize nd = mxGetNumberOfDimensions(a);
+  const mwSize *dims = mxGetDimensions(a);
+  const size_t n = mxGetNumberOfElements(a);
+  const double *src = mxGetDoubles(a);
+  double *dst = (double *)mxMalloc(n * sizeof(double) + 8);
+  mwSize idx[8] = {0};
+  if (nd > 8) mexErrMsgIdAndTxt("mpcekf:arg", "%s: too many dimensions", what);
+  for (size_t lin = 0; lin < n; ++lin) { /* lin walks the row-major order; idx its subscripts */
+    size_t cm = 0, stride = 1;
+    for (mwSize d = 0; d < nd; ++d) {
+      cm += idx[d] * stride;
+      stride *= dims[d];
+    }
+    dst[lin] = src[cm];
+    for (mwSize d = nd; d-- > 0;) {
+      if (++idx[d] < dims[d]) break;
+      idx[d] = 0;
+    }
+  }
+  return dst;
+}
+
+static const mxArray *field(const mxArray *s, const char *name) {
+  const mxArray *f = mxGetField(s, 0, name);
+  if (!f) mexErrMsgIdAndTxt("mpcekf:arg", "ROM struct: missing field %s", name);
+  return f;
+}
+
+static void electrode(const mxArray *e, mpcekf_electrode *out, int ntemp, int ntheta) {
+  out->theta0 = scalar(field(e, "theta0"), "theta0");
+  out->theta100 = scalar(field(e, "theta100"), "theta100");
+  out->soc0 = dvec(field(e, "soc0"), (size_t)ntemp, "soc0");
+  out->soc100 = dvec(field(e, "soc100"), (size_t)ntemp, "soc100");
+  out->Uocp1 = dvec(field(e, "Uocp1"), (size_t)ntheta, "Uocp1");
+  const char *names[5] = {"Uocp", "dUocp", "k0", "Rf", "Cdleff"};
+  const double **dst[5] = {&out->Uocp, &out->dUocp, &out->k0, &out->Rf, &out->Cdleff};
+  for (int i = 0; i < 5; ++i) { /* ntemp x ntheta in MATLAB -> [ntemp][ntheta] */
+    const mxArray *t = field(e, names[i]);
+    if (mxGetNumberOfElements(t) != (size_t)ntemp * ntheta) mexErrMsgIdAndTxt("mpcekf:arg", "%s: size", names[i]);
+    *dst[i] = rowmajor(t, names[i]);
+  }
+}
+
+static void rom_from_struct(const mxArray *R, mpcekf_rom *r) {
+  memset(r, 0, sizeof(*r));
+  const mxArray *A = field(R, "A"), *C = field(R, "C");
+  const mwSize *da = mxGetDimensions(A), *dc = mxGetDimensions(C);
+  if (mxGetNumberOfDimensions(A) != 3 || mxGetNumberOfDimensions(C) != 4)
+    mexErrMsgIdAndTxt("mpcekf:arg", "ROM: A must be nT x nZ x (n+1), C nT x nZ x nz x (n+1)");
+  r->nT = (int32_t)da[0];
+  r->nZ = (int32_t)da[1];
+  r->n = (int32_t)da[2] - 1;
+  r->nz = (int32_t)dc[2];
+  r->T_degC = dvec(field(R, "T_degC"), (size_t)r->nT, "T_degC");
+  r->SOC_pct = dvec(field(R, "SOC_pct"), (size_t)r->nZ, "SOC_pct");
+  r->Ts = scalar(field(R, "Ts"), "Ts");
+  r->A = rowmajor(A, "A");
+  r->C = rowmajor(C, "C");
+  r->D = rowmajor(field(R, "D"), "D");
+  const mxArray *code = field(R, "tf_code");
+  if (!mxIsInt32(code) || mxGetNumberOfElements(code) != (size_t)r->nz) mexErrMsgIdAndTxt("mpcekf:arg", "tf_code: int32 x nz");
+  r->tf_code = (const int32_t *)mxGetData(code);
+  r->tf_xloc = dvec(field(R, "xloc"), (size_t)r->nz, "xloc");
+  r->F = scalar(field(R, "F"), "F");
+  r->R = scalar(field(R, "R"), "R");
+  r->Q = scalar(field(R, "Q"), "Q");
+  r->Rc = scalar(field(R, "Rc"), "Rc");
+  r->Tref = scalar(field(R, "Tref"), "Tref");
+  const mxArray *TK = field(R, "tab_T_K");
+  r->tab_ntemp = (int32_t)mxGetNumberOfElements(TK);
+  r->tab_T_K = dvec(TK, (size_t)r->tab_ntemp, "tab_T_K");
+  r->tab_ntheta = (int32_t)mxGetNumberOfElements(field(field(R, "neg"), "Uocp1"));
+  electrode(field(R, "neg"), &r->neg, r->tab_ntemp, r->tab_ntheta);
+  electrode(field(R, "pos"), &r->pos, r->tab_ntemp, r->tab_ntheta);
+}
+
+static void cfg_from_struct(const mxArray *s, mpcekf_config *c) {
+  mpcekf_config_defaults(c);
+  if (!s || mxIsEmpty(s)) return;
+  if (!mxIsStruct(s)) mexErrMsgIdAndTxt("mpcekf:arg", "cfg: expected a struct");
+#define GETI(f) if (mxGetField(s, 0, #f)) c->f = (int32_t)scalar(mxGetField(s, 0, #f), #f)
+#define GETD(f) if (mxGetField(s, 0, #f)) c->f = scalar(mxGetField(s, 0, #f), #f)
+  GETI(Np); GETI(Nc); GETD(target_soc); GETD(Crate); GETD(u_max); GETD(du_min); GETD(du_max); GETD(v_min);
+  GETD(v_max); GETD(phise_min); GETD(z_max); GETD(z_tol); GETI(use_current); GETI(use_voltage); GETI(use_eta);
+  GETI(max_hild); GETD(hild_tol); GETD(SigmaV); GETD(SigmaW); GETI(max_warn); GETI(flags);
+#undef GETI
+#undef GETD
+  const mxArray *sx = mxGetField(s, 0, "SigmaX0");
+  if (sx) {
+    const double *v = dvec(sx, 6, "SigmaX0 (diagonal, 6)");
+    for (int i = 0; i < 6; ++i) c->SigmaX0[i] = v[i];
+  }
+}
+
+static mxArray *dmat(size_t r, size_t c) { return mxCreateDoubleMatrix((mwSize)r, (mwSize)c, mxREAL); }
+static mxArray *imat(size_t r, size_t c) { return mxCreateNumericMatrix((mwSize)r, (mwSize)c, mxINT32_CLASS, mxREAL); }
+
+static const double *opt_vec(const mxArray *a, size_t n, const char *what) {
+  return (!a || mxIsEmpty(a)) ? NULL : dvec(a, n, what);
+}
+
+void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
+  char cmd[32];
+  if (nrhs < 1 || mxGetString(prhs[0], cmd, sizeof cmd)) mexErrMsgIdAndTxt("mpcekf:arg", "first argument: command");
+  if (!strcmp(cmd, "create")) {
+    if (nrhs != 5) mexErrMsgIdAndTxt("mpcekf:arg", "create(R, cfg, device, ncells)");
+    mpcekf_rom r;
+    mpcekf_config c;
+    rom_from_struct(prhs[1], &r);
+    cfg_from_struct(prhs[2], &c);
+    mpcekf_ctx *h = NULL;
+    chk(mpcekf_ctx_create(&r, &c, (int)scalar(prhs[3], "device"), (int64_t)scalar(prhs[4], "ncells"), &h));
+    plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
+    *(uint64_t *)mxGetData(plhs[0]) = (uint64_t)(uintptr_t)h;
+    return; /* the row-major copies are mxMalloc'd: MATLAB frees them (the context copied the ROM) */
+  }
+  if (!strcmp(cmd, "hildreth")) {
+    if (nrhs != 7) mexErrMsgIdAndTxt("mpcekf:arg", "hildreth(E, F, M, gamma, lambda0, maxIter)");
+    const size_t Nc = mxGetM(prhs[1]), nC = mxGetM(prhs[3]);
+    double *E = rowmajor(prhs[1], "E"), *M = rowmajor(prhs[3], "M");
+    const double *F = dvec(prhs[2], Nc, "F"), *g = dvec(prhs[4], nC, "gamma");
+    plhs[1] = dmat(nC, 1);
+    memcpy(mxGetDoubles(plhs[1]), dvec(prhs[5], nC, "lambda0"), nC * sizeof(double));
+    plhs[0] = dmat(Nc, 1);
+    mxArray *ne = imat(1, 1);
+    chk(mpcekf_hildreth(0, 1, (int32_t)Nc, (int32_t)nC, E, F, M, g, mxGetDoubles(plhs[1]),
+                        (int32_t)scalar(prhs[6], "maxIter"), 1e-6, mxGetDoubles(plhs[0]), (int32_t *)mxGetData(ne)));
+    plhs[2] = mxCreateDoubleScalar((double)*(int32_t *)mxGetData(ne));
+    mxDestroyArray(ne);
+    return;
+  }
+  if (!strcmp(cmd, "predmat")) {
+    if (nrhs != 6) mexErrMsgIdAndTxt("mpcekf:arg", "predmat(a, C, D, Np, Nc)");
+    const int Np = (int)scalar(prhs[4], "Np"), Nc = (int)scalar(prhs[5], "Nc");
+    double *P = (double *)mxMalloc((size_t)Np * 7 * sizeof(double)), *G = (double *)mxMalloc((size_t)Np * Nc * sizeof(double));
+    chk(mpcekf_predmat(0, 1, Np, Nc, dvec(prhs[1], 6, "a"), dvec(prhs[2], 6, "C"), dvec(prhs[3], 1, "D"), P, G));
+    plhs[0] = dmat((size_t)Np, 7);
+    plhs[1] = dmat((size_t)Np, (size_t)Nc);
+    for (int i = 0; i < Np; ++i) { /* row-major -> column-major */
+      for (int k = 0; k < 7; ++k) mxGetDoubles(plhs[0])[i + (size_t)Np * k] = P[i * 7 + k];
+      for (int k = 0; k < Nc; ++k) mxGetDoubles(plhs[1])[i + (size_t)Np * k] = G[i * Nc + k];
+    }
+    return;
+  }
+  if (nrhs < 2) mexErrMsgIdAndTxt("mpcekf:arg", "%s: missing handle", cmd);
+  mpcekf_ctx *h = handle(prhs[1]);
+  int64_t n = 0;
+  int32_t NM = 0, nz = 0, ncon = 0;
+  chk(mpcekf_ctx_info(h, &n, &NM, &nz, &ncon));
+  const size_t nc = (size_t)n, nzz = (size_t)nz + 2;
+  if (!strcmp(cmd, "destroy")) {
+    chk(mpcekf_ctx_destroy(h));
+  } else if (!strcmp(cmd, "init")) {
+    chk(mpcekf_init_cells(h, dvec(prhs[2], nc, "soc0"), dvec(prhs[3], nc, "tc")));
+  } else if (!strcmp(cmd, "step")) {
+    const int32_t ns = (int32_t)scalar(prhs[2], "nsteps");
+    const double *tc = nrhs > 3 ? opt_vec(prhs[3], nc * (size_t)ns, "tc (ncells x nsteps)") : NULL;
+    for (int i = 0; i < 4; ++i) plhs[i] = dmat(nc, (size_t)ns);
+    plhs[4] = imat(nc, (size_t)ns);
+    chk(mpcekf_step(h, ns, tc, mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]), mxGetDoubles(plhs[2]),
+                    mxGetDoubles(plhs[3]), (int32_t *)mxGetData(plhs[4]), 0));
+  } else if (!strcmp(cmd, "plant")) {
+    plhs[0] = dmat(1, nc);
+    chk(mpcekf_plant_step(h, dvec(prhs[2], nc, "iapp"), nrhs > 3 ? opt_vec(prhs[3], nc, "tc") : NULL,
+                          mxGetDoubles(plhs[0])));
+  } else if (!strcmp(cmd, "ekf")) {
+    plhs[0] = dmat(nzz, nc);
+    plhs[1] = dmat(nzz, nc);
+    plhs[2] = imat(4, nc);
+    plhs[3] = dmat(4, nc);
+    chk(mpcekf_ekf_step(h, dvec(prhs[2], nc, "vk"), dvec(prhs[3], nc, "ik"),
+                        nrhs > 4 ? opt_vec(prhs[4], nc, "tk") : NULL, mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]),
+                        (int32_t *)mxGetData(plhs[2]), mxGetDoubles(plhs[3])));
+  } else if (!strcmp(cmd, "linearize")) {
+    if (!mxIsInt32(prhs[3]) || mxGetNumberOfElements(prhs[3]) != 4 * nc) mexErrMsgIdAndTxt("mpcekf:arg", "xm: int32 4 x ncells");
+    plhs[0] = dmat(MPCEKF_LIN_SIZE, nc);
+    chk(mpcekf_linearize(h, dvec(prhs[2], nzz * nc, "zk"), (const int32_t *)mxGetData(prhs[3]),
+                         dvec(prhs[4], 4 * nc, "xg"), nrhs > 5 ? opt_vec(prhs[5], nc, "tk") : NULL,
+                         mxGetDoubles(plhs[0])));
+  } else if (!strcmp(cmd, "mpc")) {
+    plhs[0] = dmat(1, nc);
+    plhs[1] = imat(1, nc);
+    chk(mpcekf_mpc_step(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
+                        mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1])));
+  } else if (!strcmp(cmd, "get_state") || !strcmp(cmd, "set_state")) {
+    const char *f[] = {"bigX", "ekf", "scal", "lambda", "warn", "status"};
+    const size_t rows[] = {(size_t)NM * 6, (size_t)NM * 20, MPCEKF_NSCAL, (size_t)ncon, 1, 1};
+    mpcekf_state st;
+    if (cmd[0] == 'g') {
+      plhs[0] = mxCreateStructMatrix(1, 1, 6, f);
+      mxArray *a[6];
+      for (int i = 0; i < 6; ++i) {
+        a[i] = i < 4 ? dmat(rows[i], nc) : imat(1, nc);
+        mxSetField(plhs[0], 0, f[i], a[i]);
+      }
+      st.bigX = mxGetDoubles(a[0]); st.ekf = mxGetDoubles(a[1]); st.scal = mxGetDoubles(a[2]);
+      st.lambda = mxGetDoubles(a[3]); st.warn = (int32_t *)mxGetData(a[4]); st.status = (int32_t *)mxGetData(a[5]);
+      chk(mpcekf_get_state(h, &st));
+    } else {
+      const mxArray *s = prhs[2];
+      st.bigX = (double *)dvec(field(s, "bigX"), rows[0] * nc, "bigX");
+      st.ekf = (double *)dvec(field(s, "ekf"), rows[1] * nc, "ekf");
+      st.scal = (double *)dvec(field(s, "scal"), rows[2] * nc, "scal");
+      st.lambda = (double *)dvec(field(s, "lambda"), rows[3] * nc, "lambda");
+      st.warn = (int32_t *)mxGetData(field(s, "warn"));
+      st.status = (int32_t *)mxGetData(field(s, "status"));
+      chk(mpcekf_set_state(h, &st));
+    }
+  } else {
+    mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
+  }
+  (void)nlhs;
+}

@@ -57,3 +57,47 @@ def test_build_id_is_the_source_hash(P):
     L = import_module("mpc-ekf4fastcharge_amd._lib").load()
     b = import_module("mpc-ekf4fastcharge_amd.build")
     assert L.mpcekf_build_id().decode() == b.source_hash()
+
+
+# The reference's MATLAB signatures; the drop-in wrappers in
+# matlab/dropin must keep them so runMPC.m runs unchanged with that folder first on
+# the path.
+DROPIN_SIGNATURES = {
+    "OB_step": "function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)",
+    "iterEKF": "function [zk,boundzk,ekfData,Xind] = iterEKF(vk,ik,Tk,ekfData)",
+    "EKFmatsHandler": "function [MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)",
+    "iterMPC": "function [uk, mpcData] = iterMPC(xk, cellState, mpcData)",
+    "hildreth": "function [DU, lambda, nexec] = hildreth(E, F, M, gamma, lambda0, maxIter)",
+    "predMat": "function [Phi, G, aug] = predMat(A, B, C, D, Np, Nc)",
+    "initKF": "function kfData = initKF(SOC0,T0,SigmaX0,SigmaV,SigmaW,blend,ROMs)",
+    "initMPC": "function mpcData = initMPC(SOC0, Np, Nc, targetSOC, opts)",
+}
+
+
+def test_matlab_dropin_wrappers_keep_reference_signatures():
+    import re
+    d = os.path.join(ROOT, "matlab", "dropin")
+    norm = lambda s: re.sub(r"\s+", "", s)
+    for name, sig in DROPIN_SIGNATURES.items():
+        first = open(os.path.join(d, name + ".m")).readline().strip()
+        assert norm(first) == norm(sig), (name, first)
+
+
+def test_mex_gateway_calls_only_declared_entry_points():
+    """matlab/mpcekf_mex.c (built on a MATLAB machine, not here) binds the C-ABI: every
+    mpcekf_* it calls is declared in include/mpcekf.h, and every MATLAB-facing stage
+    entry point is reachable from it."""
+    import re
+    src = open(os.path.join(ROOT, "matlab", "mpcekf_mex.c")).read()
+    src_code = re.sub(r"/\*.*?\*/", "", src, flags=re.S)  # comments name MATLAB helpers too
+    called = set(re.findall(r"\b(mpcekf_[a-z_]+)\s*\(", src_code)) - {"mpcekf_mex"}
+    assert called <= set(declared_symbols()), called - set(declared_symbols())
+    for sym in ("mpcekf_ctx_create", "mpcekf_init_cells", "mpcekf_step", "mpcekf_plant_step", "mpcekf_ekf_step",
+                "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_hildreth", "mpcekf_predmat", "mpcekf_get_state",
+                "mpcekf_set_state", "mpcekf_ctx_destroy"):
+        assert sym in called, sym
+    drop = " ".join(open(os.path.join(ROOT, "matlab", "dropin", f)).read()
+                    for f in os.listdir(os.path.join(ROOT, "matlab", "dropin")))
+    cmds = set(re.findall(r"mpcekf_mex\('([a-z_]+)'", drop))
+    for c in cmds:
+        assert f'"{c}"' in src, c
