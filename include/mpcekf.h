@@ -120,7 +120,11 @@ typedef struct {
   double SigmaX0[6];       /* diagonal of SigmaX0 (runMPC.m:17)                  */
   int32_t max_warn;        /* lock-out threshold (iterEKF.m:55: > 10)            */
   int32_t flags;           /* MPCEKF_CF_*                                        */
+  int32_t method;          /* initKF.m:44-49 blend: MPCEKF_METHOD_OB (runMPC.m) or _MB */
 } mpcekf_config;
+
+#define MPCEKF_METHOD_OB 0 /* output blend: every local model filtered (iterEKF.m 'OB')      */
+#define MPCEKF_METHOD_MB 1 /* model blend: one blended model per cell (iterEKF.m:90-102 'MB') */
 
 /* Layout of one linearisation record (EKFmatsHandler outputs), doubles: */
 #define MPCEKF_LIN_A 0     /* [6] diag(A)              */
@@ -261,7 +265,11 @@ typedef struct {
   double *lambda;  /* [ncells][ncon]    mpcData.lambda                               */
   int32_t *warn;   /* [ncells]          iterEKF warnCount                            */
   int32_t *status; /* [ncells]          MPCEKF_ST_*                                   */
+  double *mb;      /* [ncells][MPCEKF_MB_SIZE] method MB: ekfData.xhat(1:5), 0, SigmaX
+                      6x6 row-major (xhat(end) is MPCEKF_S_X0); may be NULL          */
 } mpcekf_state;
+
+#define MPCEKF_MB_SIZE 42
 
 #define MPCEKF_S_SOCNAVG 0 /* cellState.SOCnAvg          */
 #define MPCEKF_S_SOCPAVG 1 /* cellState.SOCpAvg          */

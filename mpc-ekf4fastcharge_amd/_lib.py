@@ -19,6 +19,8 @@ ST_ERROR, ST_LOCKOUT, ST_THETAE_NEG = 1, 2, 4
 CF_BOUNDS = 1
 LIN_SIZE = 35
 NSCAL = 8
+MB_SIZE = 42
+METHOD_OB, METHOD_MB = 0, 1
 S_SOCNAVG, S_SOCPAVG, S_X0, S_SIGMAX0, S_PRIORI, S_UK_1, S_UK, S_VK = range(8)
 
 _dp = C.POINTER(C.c_double)
@@ -45,11 +47,13 @@ class Config(C.Structure):
                 ("z_max", C.c_double), ("z_tol", C.c_double), ("use_current", C.c_int32),
                 ("use_voltage", C.c_int32), ("use_eta", C.c_int32), ("max_hild", C.c_int32),
                 ("hild_tol", C.c_double), ("SigmaV", C.c_double), ("SigmaW", C.c_double),
-                ("SigmaX0", C.c_double * 6), ("max_warn", C.c_int32), ("flags", C.c_int32)]
+                ("SigmaX0", C.c_double * 6), ("max_warn", C.c_int32), ("flags", C.c_int32),
+                ("method", C.c_int32)]
 
 
 class State(C.Structure):
-    _fields_ = [("bigX", _dp), ("ekf", _dp), ("scal", _dp), ("lam", _dp), ("warn", _ip), ("status", _ip)]
+    _fields_ = [("bigX", _dp), ("ekf", _dp), ("scal", _dp), ("lam", _dp), ("warn", _ip), ("status", _ip),
+                ("mb", _dp)]
 
 
 class Traj(C.Structure):

@@ -67,6 +67,8 @@ struct mpcekf_ctx {
   // device buffers owned by the context
   double *d_cell_blob = nullptr, *d_plant_blob = nullptr, *d_bulk = nullptr;
   double *d_const = nullptr;  // 8 per-cell constant arrays
+  double *d_mb = nullptr;     // model-blend EKF state [n][MBREC] (method MB)
+  bool mb = false;
   double *d_scal = nullptr;   // 8 scalar state arrays + J_unc, J_fin
   int *d_int = nullptr;       // warn, status, nviol, hflag
   double *d_prob = nullptr;   // k_cell -> k_hild problem records
@@ -140,6 +142,7 @@ void mpcekf_config_defaults(mpcekf_config *c) {
   c->SigmaX0[5] = 2e6;        // runMPC.m:17
   c->max_warn = 10;           // iterEKF.m:55
   c->flags = 0;
+  c->method = MPCEKF_METHOD_OB;  // runMPC.m:16 blend = 'OutB'
 }
 
 // ---------------------------------------------------------------------------
@@ -371,6 +374,8 @@ static int check_cfg(const mpcekf_config *c) {
   if (!c->use_current || !c->use_voltage || !c->use_eta)
     return fail(MPCEKF_E_UNSUPPORTED, "constraint switches must all be on (runMPC.m:33) in this build");
   if (c->max_hild < 1) return fail(MPCEKF_E_ARG, "max_hild < 1");
+  if (c->method != MPCEKF_METHOD_OB && c->method != MPCEKF_METHOD_MB)
+    return fail(MPCEKF_E_ARG, "method %d: expected MPCEKF_METHOD_OB or _MB (initKF.m:44-49)", c->method);
   return MPCEKF_OK;
 }
 
@@ -388,7 +393,7 @@ static void fill_kcfg(const mpcekf_config *c, double Q, KCfg &k) {
   k.hild_tol = c->hild_tol;
   k.max_warn = c->max_warn;
   k.max_hild = c->max_hild;
-  k.flags = c->flags;
+  k.flags = c->flags | (c->method == MPCEKF_METHOD_MB ? KF_MB : 0);
 }
 
 int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int device, int64_t ncells,
@@ -408,6 +413,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   X->cfg = *cfg;
   X->ncon = ncon_of(cfg->Np, cfg->Nc);
   X->wide = wide_supported(cfg->Np, cfg->Nc);
+  X->mb = cfg->method == MPCEKF_METHOD_MB;
   if ((rc = build_rom(X, rom))) { mpcekf_ctx_destroy(X); return rc; }
   fill_kcfg(cfg, rom->Q, X->k);
   // Diagnostic override (tests/test_gpu_parity.py shows results do not depend on it):
@@ -429,7 +435,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
       (rc = dalloc(&X->d_zk, n * (X->nz + 2))) || (rc = dalloc(&X->d_zbk, n * (X->nz + 2))) ||
       (rc = dalloc(&X->d_bnd, n * NBND)) || (rc = dalloc(&X->d_xg, n * 4)) ||
       (rc = hipMalloc((void **)&X->d_xm, n * 4 * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) ||
-      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2))
+      (rc = dalloc(&X->d_ts, n * NM * 2)) || (rc = dalloc(&X->d_hist, n * LAZY_H * 2)) ||
+      (X->mb && (rc = dalloc(&X->d_mb, n * MBREC)))
 #ifdef MPCEKF_STAMPS
       || (rc = dalloc(&X->d_stamps, n * NSTAMPS))
 #endif
@@ -446,6 +453,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.prob = X->d_prob;
   s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
+  s.mb = X->d_mb;
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n;
   if (X->wide) {
@@ -475,7 +483,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
-                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc};
+                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);
@@ -550,6 +558,13 @@ int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_de
   HIPCHK(hipMemsetAsync(X->d_ts, 0, n * X->NM * 2 * sizeof(int), X->stream));  // every model current
   int rc = launch_init_state(X->n, X->NM, X->s.ekf, X->s.bigx, X->cfg.SigmaX0, X->stream);
   if (rc) return fail(MPCEKF_E_HIP, "init kernel: %s", hipGetErrorString((hipError_t)rc));
+  if (X->mb) {  // initKF.m:47-48,111-112: xhat = 0, SigmaX = SigmaX0 (6x6)
+    std::vector<double> mbs(n * MBREC, 0.0);
+    for (size_t c = 0; c < n; ++c)
+      for (int p = 0; p <= NX; ++p) mbs[c * MBREC + 6 + p * (NX + 1) + p] = X->cfg.SigmaX0[p];
+    HIPCHK(hipMemcpyAsync(X->d_mb, mbs.data(), mbs.size() * 8, hipMemcpyHostToDevice, X->stream));
+    HIPCHK(hipStreamSynchronize(X->stream));
+  }
   HIPCHK(hipStreamSynchronize(X->stream));
   X->initialized = true;
   return MPCEKF_OK;
@@ -681,7 +696,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       return rc;
     }
     if (E) HIPCHK(hipEventRecord(E[2], X->stream));
-    if (bounds && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
+    // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
+    if (bounds && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
     if (E) HIPCHK(hipEventRecord(E[3], X->stream));
     if (X->wide) {
       if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
@@ -807,7 +823,8 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   HIPCHK(hipMemcpyAsync(dik, ik, n * 8, hipMemcpyHostToDevice, X->stream));
   // iterEKF.m:55 lock-out must see the state before the time update: the bulk
   // update of a locked-out cell is harmless because the cell is stopped.
-  if ((rc = lerr(launch_bulk(X->r, X->k, X->s, nullptr, 0, 1, X->stream), "bulk"))) return rc;
+  // OB: the all-model time update (iterEKF.m:73-84); MB updates only its blended model (in k_cell)
+  if (!X->mb && (rc = lerr(launch_bulk(X->r, X->k, X->s, nullptr, 0, 1, X->stream), "bulk"))) return rc;
   KIO io{};
   io.mode = MODE_EKF;
   io.vk_in = dvk;
@@ -818,7 +835,7 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   io.xm_out = dxm;
   io.xg_out = dxg;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-  if (boundzk && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
+  if (boundzk && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
   HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));
@@ -1048,6 +1065,7 @@ int mpcekf_get_state(mpcekf_ctx *X, mpcekf_state *st) {
   const size_t n = (size_t)X->n, NM = (size_t)X->NM, nc = (size_t)X->ncon;
   if (st->bigX) HIPCHK(hipMemcpyAsync(st->bigX, X->s.bigx, n * NM * 6 * 8, hipMemcpyDeviceToHost, X->stream));
   if (st->ekf) HIPCHK(hipMemcpyAsync(st->ekf, X->s.ekf, n * NM * REC * 8, hipMemcpyDeviceToHost, X->stream));
+  if (st->mb && X->mb) HIPCHK(hipMemcpyAsync(st->mb, X->d_mb, n * MBREC * 8, hipMemcpyDeviceToHost, X->stream));
   std::vector<double> sc(n * 8), lam(n * nc);
   std::vector<int> iv(n * 2);
   HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
@@ -1072,6 +1090,7 @@ int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
   const size_t n = (size_t)X->n, NM = (size_t)X->NM, nc = (size_t)X->ncon;
   if (st->bigX) HIPCHK(hipMemcpyAsync(X->s.bigx, st->bigX, n * NM * 6 * 8, hipMemcpyHostToDevice, X->stream));
   if (st->ekf) HIPCHK(hipMemcpyAsync(X->s.ekf, st->ekf, n * NM * REC * 8, hipMemcpyHostToDevice, X->stream));
+  if (st->mb && X->mb) HIPCHK(hipMemcpyAsync(X->d_mb, st->mb, n * MBREC * 8, hipMemcpyHostToDevice, X->stream));
   std::vector<double> sc(n * 8), lam(n * nc);
   std::vector<int> iv(n * 2);
   HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));

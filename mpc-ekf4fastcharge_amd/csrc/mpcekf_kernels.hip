@@ -589,7 +589,7 @@ using MpcSetup = MpcSetupT<NP, NC>;
 // EKFmatsHandler.m:26-114.  zTE1.. are the role rows of zk, Zsoc = zk(end).
 template <int NZ>
 __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
-                                             double Zsoc, double TK, Lin &L) {
+                                             double Zsoc, double TK, Lin &L, double xend = 0.0) {
   int imax = 0;
 #pragma unroll
   for (int j = 1; j < 4; ++j)
@@ -605,7 +605,7 @@ __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, c
   load_x(cc.erec + (size_t)m * REC, x);
 #pragma unroll
   for (int k = 0; k < NX; ++k) { L.xhat[k] = x[k]; L.a[k] = am[k]; }
-  L.xhat[NX] = 0.0;
+  L.xhat[NX] = xend;  // ekfData.xhat(end) (EKFmatsHandler.m:33): 0 in 'OB', the MB integrator
   L.a[NX] = 1.0;
   double rr = -r.Ts / (3600 * r.Q);
 #pragma unroll
@@ -1331,7 +1331,9 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
     for (int64_t c = w0; c < s.n; c += nw) {
       const double hpl = s.hist_p[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
       const double hul = s.hist_u[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
-      const int tse = act ? s.ts_ekf[c * NM + m] : t, tsp = act ? s.ts_plant[c * NM + m] : t;
+      // MB never time-updates the per-model EKF records (iterEKF.m:90-102)
+      const int tse = (act && !(cf.flags & KF_MB)) ? s.ts_ekf[c * NM + m] : t;
+      const int tsp = act ? s.ts_plant[c * NM + m] : t;
       double2 *re = reinterpret_cast<double2 *>(s.ekf + ((size_t)c * NM + mm) * REC);
       double2 *rp = reinterpret_cast<double2 *>(s.bigx + ((size_t)c * NM + mm) * 6);
       double xe[REC], xp[6];
@@ -1450,9 +1452,176 @@ __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc
 }
 
 // ---------------------------------------------------------------------------
+// Model blend ('MB', initKF.m:44-49): one blended model per cell, its (n+1) state and
+// full 6x6 covariance in s.mb [n][MBREC] = xhat[0..4], -, Sigma 6x6 row-major; the
+// integrator xhat(end) lives in s.x0.  The sequence is oracle/mpcekf_oracle.c
+// ekf_step_mb / meas_cov_mb / get_chat_v_mb, operation for operation.
+// ---------------------------------------------------------------------------
+constexpr int NA6 = NX + 1;
+constexpr int NPK6 = NA6 * (NA6 + 1) / 2;
+__device__ __forceinline__ int pk6(int r, int c) {
+  return r <= c ? r * NA6 - (r * (r - 1)) / 2 + (c - r) : c * NA6 - (c * (c - 1)) / 2 + (r - c);
+}
+
+// getChatV 'MB' (iterEKF.m:448-459, 475-479, 489-491, 512-517): the gamma-weighted sums
+// of the four corners' rows, then the terms; the integrator entry last.
+template <int NZ>
+__device__ __forceinline__ void chat_mb(const KRom &r, const CellCtx &cc, const XI &xi, double xSOC, double zTE1,
+                                        double zTH0, double zTEE, double zTH3, double ChV[NA6]) {
+  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
+  constexpr int rows[7] = {R_IFDL3, R_IFDL0, R_IF3, R_IF0, R_PHIE, R_TH3, R_TH0};
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    double sum[7];
+#pragma unroll
+    for (int t = 0; t < 7; ++t) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a = a + xi.g[j] * cc.L[xi.m[j] * cc.stride + rows[t] * NX + k];
+      sum[t] = a;
+    }
+    double v = K.Rfp * sum[0] - K.Rfn * sum[1];
+    v = v + K.Rctp * sum[2] - K.Rctn * sum[3];
+    v = v + sum[4];
+    v = v + K.dUp3 * sum[5] - K.dUn0 * sum[6];
+    ChV[k] = v;
+  }
+  ChV[NX] = chat0(r, K);
+}
+
+// row' * Sigma * row on the full 6x6 (orc qform_full): t_c = sum_k fma(S_kc, row_k),
+// acc = sum_c fma(t_c, row_c)
+__device__ __forceinline__ double qform6(const double S[NA6 * NA6], const double row[NA6]) {
+  double acc = 0.0;
+#pragma unroll
+  for (int cI = 0; cI < NA6; ++cI) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < NA6; ++k) t = __builtin_fma(S[k * NA6 + cI], row[k], t);
+    acc = __builtin_fma(t, row[cI], acc);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ bool is_pd6(const double a[NPK6]) {  // orc is_pd_n(6)
+  double l[NA6][NA6], d[NA6];
+  bool pd = true;
+#pragma unroll
+  for (int j = 0; j < NA6; ++j) {
+    double sj = a[pk6(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) sj = __builtin_fma(-(l[j][k] * l[j][k]), d[k], sj);
+    pd = pd && (sj > 0);
+    d[j] = sj;
+    const double inv = 1.0 / sj;
+#pragma unroll
+    for (int i = j + 1; i < NA6; ++i) {
+      double t = a[pk6(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t = __builtin_fma(-(l[i][k] * l[j][k]), d[k], t);
+      l[i][j] = t * inv;
+    }
+  }
+  return pd;
+}
+
+__device__ __noinline__ void jacobi6(double a[NPK6], double V[NA6 * NA6]) {  // orc_jacobi(6), packed
+#pragma unroll
+  for (int i = 0; i < NA6 * NA6; ++i) V[i] = (i % (NA6 + 1)) == 0 ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    double off = 0.0, dg = 0.0;
+#pragma unroll
+    for (int p = 0; p < NA6; ++p) {
+      dg = dg + a[pk6(p, p)] * a[pk6(p, p)];
+#pragma unroll
+      for (int q = p + 1; q < NA6; ++q) off = off + a[pk6(p, q)] * a[pk6(p, q)];
+    }
+    if (!(off > 1e-36 * dg)) break;
+#pragma unroll
+    for (int p = 0; p < NA6 - 1; ++p) {
+#pragma unroll
+      for (int q = p + 1; q < NA6; ++q) {
+        double apq = a[pk6(p, q)];
+        if (apq != 0.0) {
+          double theta = (a[pk6(q, q)] - a[pk6(p, p)]) / (2.0 * apq);
+          double t;
+          if (fabs(theta) > 1e150) {
+            t = 0.5 / theta;
+          } else {
+            t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+            if (theta < 0) t = -t;
+          }
+          double c = 1.0 / sqrt(t * t + 1.0), sn = t * c, tau = sn / (1.0 + c);
+          a[pk6(p, p)] = a[pk6(p, p)] - t * apq;
+          a[pk6(q, q)] = a[pk6(q, q)] + t * apq;
+          a[pk6(p, q)] = 0.0;
+#pragma unroll
+          for (int rr = 0; rr < NA6; ++rr) {
+            if (rr == p || rr == q) continue;
+            double g = a[pk6(rr, p)], h = a[pk6(rr, q)];
+            a[pk6(rr, p)] = g - sn * (h + g * tau);
+            a[pk6(rr, q)] = h + sn * (g - h * tau);
+          }
+#pragma unroll
+          for (int rr = 0; rr < NA6; ++rr) {
+            double g = V[rr * NA6 + p], h = V[rr * NA6 + q];
+            V[rr * NA6 + p] = g - sn * (h + g * tau);
+            V[rr * NA6 + q] = h + sn * (g - h * tau);
+          }
+        }
+      }
+    }
+  }
+}
+
+// iterEKF.m:164-173 on the full MB covariance (orc meas_cov_mb)
+__device__ __forceinline__ void meas_cov_mb(double S[NA6 * NA6], const double L[NA6], double St, bool bump) {
+  double P[NA6 * NA6], a[NPK6];
+#pragma unroll
+  for (int rr = 0; rr < NA6; ++rr)
+#pragma unroll
+    for (int cI = 0; cI < NA6; ++cI) P[rr * NA6 + cI] = __builtin_fma(-(L[rr] * St), L[cI], S[rr * NA6 + cI]);
+#pragma unroll
+  for (int rr = 0; rr < NA6; ++rr)
+#pragma unroll
+    for (int cI = rr; cI < NA6; ++cI) a[pk6(rr, cI)] = (P[rr * NA6 + cI] + P[cI * NA6 + rr]) * 0.5;
+  if (is_pd6(a)) {
+#pragma unroll
+    for (int rr = 0; rr < NA6; ++rr)
+#pragma unroll
+      for (int cI = rr; cI < NA6; ++cI) {
+        double v = (((P[rr * NA6 + cI] + P[cI * NA6 + rr]) + a[pk6(rr, cI)]) + a[pk6(rr, cI)]) / 4.0;
+        if (bump) v = v * 2.0;
+        S[rr * NA6 + cI] = v;
+        S[cI * NA6 + rr] = v;
+      }
+    return;
+  }
+  double V[NA6 * NA6], w[NA6];
+  jacobi6(a, V);
+#pragma unroll
+  for (int k = 0; k < NA6; ++k) w[k] = fabs(a[pk6(k, k)]);
+#pragma unroll
+  for (int rr = 0; rr < NA6; ++rr)
+#pragma unroll
+    for (int cI = rr; cI < NA6; ++cI) {
+      double hrc = 0.0, hcr = 0.0;
+#pragma unroll
+      for (int k = 0; k < NA6; ++k) {
+        hrc = hrc + (V[rr * NA6 + k] * w[k]) * V[cI * NA6 + k];
+        hcr = hcr + (V[cI * NA6 + k] * w[k]) * V[rr * NA6 + k];
+      }
+      double v = (((P[rr * NA6 + cI] + P[cI * NA6 + rr]) + hrc) + hcr) / 4.0;
+      if (bump) v = v * 2.0;
+      S[rr * NA6 + cI] = v;
+      S[cI * NA6 + rr] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_cell: iterEKF measurement update + EKFmatsHandler + iterMPC (lane per cell)
 // ---------------------------------------------------------------------------
-template <int NZ, int PARTS>
+template <int NZ, int PARTS, bool MB = false>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
   stage_lds(lds, r.cell_blob, r.cell_len);
@@ -1520,6 +1689,143 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       fail_outputs();
       return;
     }
+    if constexpr (MB) {
+    // iterEKF.m:90-102 ('MB' time update), 106-108, 125-128 (gain), 160-176 (update),
+    // 181-183, 199-203 (boundzk); the per-model records are never touched
+    const double rs = r.Ts / (3600 * r.Q);
+    const double SOC0 = s.SOC0[c];
+    const double pri = s.priorI[c];
+    double xm[NX], Sf[NA6 * NA6];
+    {
+      const double2 *p = reinterpret_cast<const double2 *>(s.mb + (size_t)c * MBREC);
+      double v[MBREC];
+#pragma unroll
+      for (int i = 0; i < MBREC / 2; ++i) { const double2 q = p[i]; v[2 * i] = q.x; v[2 * i + 1] = q.y; }
+#pragma unroll
+      for (int k = 0; k < NX; ++k) xm[k] = v[k];
+#pragma unroll
+      for (int i = 0; i < NA6 * NA6; ++i) Sf[i] = v[6 + i];
+    }
+    double x0 = s.x0[c];  // xhat(end)
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC0 - x0 * rs, xi);  // iterEKF.m:92-93
+    double amb[NA6];
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      double a = 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a = a + cc.L[xi.m[j] * cc.stride + NZ * NX + NZ + k] * xi.g[j];
+      amb[k] = a;
+    }
+    amb[NX] = 1.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xm[k] = amb[k] * xm[k] + pri;
+    x0 = x0 + pri;
+#pragma unroll
+    for (int pp = 0; pp < NA6; ++pp)
+#pragma unroll
+      for (int q = 0; q < NA6; ++q) Sf[pp * NA6 + q] = (amb[pp] * Sf[pp * NA6 + q]) * amb[q] + cf.SigmaW;
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC0 - x0 * rs, xi);
+    double xr[4][NX];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < NX; ++k) xr[j][k] = xm[k];
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr);
+    if (st & ST_ERROR) {
+      s.status[c] = st;
+      s.warn[c] = warn;
+      if (fused) s.uk[c] = NaN;
+      fail_outputs();
+      return;
+    }
+    double ChV[NA6], Lk[NA6];
+    chat_mb<NZ>(r, cc, xi, SOC0 - x0 * rs, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChV);
+    const double St = qform6(Sf, ChV) + cf.SigmaV;
+#pragma unroll
+    for (int pp = 0; pp < NA6; ++pp) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NA6; ++k) acc = __builtin_fma(Sf[pp * NA6 + k], ChV[k], acc);
+      Lk[pp] = acc / St;
+    }
+    const double res = vk - vhat;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xm[k] = __builtin_fma(Lk[k], res, xm[k]);
+    x0 = __builtin_fma(Lk[NX], res, x0);
+    meas_cov_mb(Sf, Lk, St, res * res > 9 * St);
+    get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC0 - x0 * rs, xi);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < NX; ++k) xr[j][k] = xm[k];
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr);
+    s.warn[c] = warn;
+    {
+      double2 *p = reinterpret_cast<double2 *>(s.mb + (size_t)c * MBREC);
+      double v[MBREC];
+#pragma unroll
+      for (int k = 0; k < NX; ++k) v[k] = xm[k];
+      v[NX] = 0.0;
+#pragma unroll
+      for (int i = 0; i < NA6 * NA6; ++i) v[6 + i] = Sf[i];
+#pragma unroll
+      for (int i = 0; i < MBREC / 2; ++i) p[i] = make_double2(v[2 * i], v[2 * i + 1]);
+    }
+    s.x0[c] = x0;
+    if (st & ST_ERROR) {
+      s.status[c] = st;
+      if (fused) s.uk[c] = NaN;
+      fail_outputs();
+      return;
+    }
+    s.priorI[c] = ik;  // iterEKF.m:210
+    if (io.zbk) {  // getChatZ 'MB' (iterEKF.m:537-538, 554-558, 575-576, 596-600) + iterEKF.m:199-203
+      const double xSOC = SOC0 - x0 * rs;
+      double ChVz[NA6];
+      chat_mb<NZ>(r, cc, xi, xSOC, Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChVz);
+      const double res0n = -r.Ts * (cc.et.soc(0, 1) - cc.et.soc(0, 0)) / (3600 * r.Q);
+      const double res0p = -r.Ts * (cc.et.soc(1, 1) - cc.et.soc(1, 0)) / (3600 * r.Q);
+      const double dUn = cc.et.f(0, EF_DU, cc.et.soc(0, xSOC)), dUp = cc.et.f(1, EF_DU, cc.et.soc(1, xSOC));
+      const double c0v[7] = {0.0, ChVz[NX], res0n, res0p, dUn * res0n, dUp * res0p, -dUn * res0n};
+      auto chrow = [&](int q, double row[NA6]) {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) {
+          double a = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a = a + xi.g[j] * cc.L[xi.m[j] * cc.stride + q * NX + k];
+          if (r.flags[q] & G_PPHIS) a = a + ChVz[k];
+          row[k] = a;
+        }
+      };
+      double ph0[NA6];
+      chrow(R_PHISE0, ph0);
+      double *zo = io.zbk + c * (nz + 2);
+#pragma unroll 1
+      for (int q = 0; q < nz; ++q) {
+        double row[NA6];
+        chrow(q, row);
+        if (r.flags[q] & G_PHIE)
+#pragma unroll
+          for (int k = 0; k < NX; ++k) row[k] = row[k] - ph0[k];
+        row[NX] = c0v[r.c0k[q]];
+        zo[r.perm[q]] = 3 * sqrt(qform6(Sf, row));
+      }
+      zo[nz] = 3 * sqrt(qform6(Sf, ChVz));
+      zo[nz + 1] = 3 * sqrt(rs * Sf[NA6 * NA6 - 1] * rs);
+    }
+    if (io.zk) {
+#pragma unroll
+      for (int q = 0; q < NZ; ++q)
+        if (q < nz) io.zk[c * (nz + 2) + r.perm[q]] = Z[q];
+      io.zk[c * (nz + 2) + nz] = vhat;
+      io.zk[c * (nz + 2) + nz + 1] = Zsoc;
+    }
+    if (io.bnd) io.bnd[BD_M * s.n + c] = -1.0;  // no k_bounds record in MB
+    if (io.xm_out) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
+    }
+    } else {
     double x0 = s.x0[c] + s.priorI[c];  // iterEKF.m:85-86 (models: k_bulk)
     double S0 = s.S0[c] + cf.SigmaW;
     const double SOC0 = s.SOC0[c];
@@ -1672,6 +1978,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
     }
+    }  // OB
   }
   if (!(PARTS & (P_MPC | P_LIN))) return;
   // The fused step's second kernel: cells the iterEKF kernel failed are finished.
@@ -1694,7 +2001,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { xi.m[j] = io.xm_in[c * 4 + j]; xi.g[j] = io.xg_in[c * 4 + j]; }
     }
-    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L);
+    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
     if (io.x_out)
 #pragma unroll
@@ -2303,25 +2610,32 @@ int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iap
   return (int)hipGetLastError();
 }
 
-template <int NZ, int PARTS>
+template <int NZ, int PARTS, bool MB>
 static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   int lds = cell_lds_bytes(r);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_cell<NZ, PARTS>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
 }
 
 template <int NZ>
 static int launch_cell_nz(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st, int parts) {
+  if (c.flags & KF_MB) {  // the model-blend EKF ('MB'): fused 5/2, wide (EKF + linearisation) and all stages
+    switch (parts) {
+      case P_ALL: launch_cell_t<NZ, P_ALL, true>(r, c, s, io, st); return 0;
+      case P_EKF | P_LIN: launch_cell_t<NZ, P_EKF | P_LIN, true>(r, c, s, io, st); return 0;
+      default: return -1;
+    }
+  }
   switch (parts) {
-    case P_EKF: launch_cell_t<NZ, P_EKF>(r, c, s, io, st); return 0;
-    case P_MPC: launch_cell_t<NZ, P_MPC>(r, c, s, io, st); return 0;
-    case P_ALL: launch_cell_t<NZ, P_ALL>(r, c, s, io, st); return 0;
-    case P_EKF | P_LIN: launch_cell_t<NZ, P_EKF | P_LIN>(r, c, s, io, st); return 0;
+    case P_EKF: launch_cell_t<NZ, P_EKF, false>(r, c, s, io, st); return 0;
+    case P_MPC: launch_cell_t<NZ, P_MPC, false>(r, c, s, io, st); return 0;
+    case P_ALL: launch_cell_t<NZ, P_ALL, false>(r, c, s, io, st); return 0;
+    case P_EKF | P_LIN: launch_cell_t<NZ, P_EKF | P_LIN, false>(r, c, s, io, st); return 0;
     default: return -1;
   }
 }

@@ -17,7 +17,9 @@ constexpr int MAXROWS = 64;
 constexpr int NPLANT = 9;  // role rows the plant needs (OB_step.m:289-344)
 constexpr int PREC = NPLANT * NX + NPLANT + NPLANT + 6;  // plant blob record per model: C[9][5], res0[9], D[9], a[6]
 constexpr int LAZY_H = 32;  // deferred time update: input ring length = flush period (steps)
-constexpr int MAXTT = 8;    // max electrode-table temperatures (mpcekf_rom.tab_ntemp)
+constexpr int MAXTT = 8;
+constexpr int MBREC = 42;   // model-blend state per cell: xhat[5], pad, Sigma 6x6 row-major
+constexpr int KF_MB = 1 << 8;  // KCfg.flags: model-blend EKF (mpcekf_config.method == 1)    // max electrode-table temperatures (mpcekf_rom.tab_ntemp)
 
 // role slots = the first rows of the permuted output vector (rom.py ROLE_NAMES)
 enum { R_IFDL0 = 0, R_IFDL3, R_IF0, R_IF3, R_TH0, R_TH3, R_TE1, R_TEE, R_PHIE, R_PHISE0, R_NPHISE2, NROLE };
@@ -66,6 +68,7 @@ struct KState {
   int *hflag;      // [n] 1: hildreth.m must run this step (2: k_hild_slow finishes it)
   int *hslow;      // [1] waves of the current step with a k_hild_slow lane (k_plant zeroes it)
   double *prob;    // [PB_N][n] problem records (mpcekf_kernels.hip PB_*)
+  double *mb;      // [n][MBREC] model-blend EKF state (method 'MB' only)
   // deferred all-model time update (fused mpcekf_step only): each local
   // model's record is current through step ts[c][m] of the running call; the inputs
   // of the last LAZY_H steps sit in per-cell rings

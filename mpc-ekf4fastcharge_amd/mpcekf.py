@@ -46,15 +46,11 @@ def make_config(**kw) -> _lib.Config:
             for i in range(6):
                 c.SigmaX0[i] = float(v[i])
         elif k == "method":
-            # initKF.m:44-49 blend selector.  Only the output blend ('OB', runMPC.m's choice)
-            # is built into the library; the model blend ('MB') exists in the oracle only
-            # (oracle/oracle_np.py) -- refuse it loudly rather than run something else.
+            # initKF.m:44-49 blend selector: 'OB'/'OutB' (runMPC.m:16) or 'MB'/'MdlB'
             m = str(v).upper()
             if m not in ("OB", "OUTB", "MB", "MDLB"):
                 raise ValueError(f"method {v!r}: expected 'OB' or 'MB' (initKF.m:44-49)")
-            if m in ("MB", "MDLB"):
-                raise NotImplementedError("model-blend EKF ('MB', iterEKF.m:90-102) is not built into "
-                                          "libmpcekf yet (DESIGN.md §7)")
+            c.method = _lib.METHOD_MB if m in ("MB", "MDLB") else _lib.METHOD_OB
         elif k == "bounds":
             c.flags = (c.flags | _lib.CF_BOUNDS) if v else (c.flags & ~_lib.CF_BOUNDS)
         else:
@@ -264,8 +260,10 @@ class Context:
         n, NM = self.n, self.NM
         st = dict(bigX=np.empty((n, NM, 6)), ekf=np.empty((n, NM, 20)), scal=np.empty((n, _lib.NSCAL)),
                   lam=np.empty((n, self.ncon)), warn=np.empty(n, np.int32), status=np.empty(n, np.int32))
+        if self.cfg.method == _lib.METHOD_MB:
+            st["mb"] = np.empty((n, _lib.MB_SIZE))
         s = _lib.State(dptr(st["bigX"]), dptr(st["ekf"]), dptr(st["scal"]), dptr(st["lam"]),
-                       iptr(st["warn"]), iptr(st["status"]))
+                       iptr(st["warn"]), iptr(st["status"]), dptr(st.get("mb")))
         check(self.L.mpcekf_get_state(self.h, C.byref(s)))
         return st
 
@@ -273,7 +271,7 @@ class Context:
         a = {k: (np.ascontiguousarray(v, dtype=np.int32 if k in ("warn", "status") else np.float64)
                  if v is not None else None) for k, v in st.items()}
         s = _lib.State(dptr(a.get("bigX")), dptr(a.get("ekf")), dptr(a.get("scal")), dptr(a.get("lam")),
-                       iptr(a.get("warn")), iptr(a.get("status")))
+                       iptr(a.get("warn")), iptr(a.get("status")), dptr(a.get("mb")))
         check(self.L.mpcekf_set_state(self.h, C.byref(s)))
 
 

@@ -371,3 +371,55 @@ def test_temperature_through_stage_entry_points(rom, M):
             np.testing.assert_array_equal(v, fused["v"][k])
             np.testing.assert_array_equal(uk, fused["u"][k])
             np.testing.assert_array_equal(ne, fused["nexec"][k])
+
+
+@pytest.mark.parametrize("Np,Nc", [(5, 2), (20, 10)])
+def test_model_blend_matches_oracle_and_golden(P, oc, M, Np, Nc):
+    """The model-blend EKF ('MB', iterEKF.m:90-102,125-128,160-176,199-203; initKF.m:47-48,
+    111-112) on the GPU: bitwise against the C oracle's ekf_step_mb over the closed loop
+    (zk / boundzk and every runMPC.m store included), within 1e-9 of the numpy
+    restatement's golden fixture at Np = 5."""
+    rom = P.make_synth_rom()
+    n, steps = 48, 250
+    soc0, tc = batch_inputs(n, seed=23)
+    soc0[5] = 130.0                      # thetae < 0 error cell
+    cfg = M.make_config(method="MB", bounds=True, Np=Np, Nc=Nc)
+    names = ("u", "v", "soc", "phise", "nexec", "x", "zk", "zbk", "J_unc", "J_fin", "norm_du", "nviol")
+    with M.Context(rom, n, cfg) as ctx:
+        ctx.init_cells(soc0, tc)
+        out = ctx.step(steps, outputs=names)
+        st = ctx.get_state()
+    ref = oc.run(rom, soc0, tc, steps, nthreads=4, traj=True, method="MB", Np=Np, Nc=Nc)
+    pairs = dict(u="u", v="v", soc="soc", phise="phise", nexec="nexec", x="x", zk="zk_traj",
+                 zbk="zbk_traj", J_unc="J_unc", J_fin="J_fin", norm_du="norm_du", nviol="nviol")
+    for k, rk in pairs.items():
+        _bitwise(out[k], ref[rk], k)
+    np.testing.assert_array_equal(st["status"], ref["status"])
+    assert st["status"][5] & 1 and (st["status"][np.arange(n) != 5] == 0).all()
+    # the per-model records are never touched by MB (EKFmatsHandler.m:33 reads them)
+    assert not st["ekf"][:, :, :5].any()
+    assert np.isfinite(st["mb"][st["status"] == 0]).all()
+    if (Np, Nc) == (5, 2):
+        g = _golden("mb_batch4_200")
+        out_g = M.runMPC(rom, g["soc0"], g["tc"], g["u"].shape[0], cfg=M.make_config(method="MB"))
+        for k in ("u", "v", "soc", "phise"):
+            assert _rel(out_g[k], g[k]).max() <= 1e-9, k
+        np.testing.assert_array_equal(out_g["nexec"], g["nexec"])
+
+
+def test_model_blend_stage_entry_points_match_fused(rom, M):
+    n, steps = 64, 20
+    soc0, tc = batch_inputs(n, seed=29)
+    cfg = M.make_config(method="MB")
+    fused = M.runMPC(rom, soc0, tc, steps, cfg=cfg)
+    with M.Context(rom, n, cfg) as ctx:
+        ctx.init_cells(soc0, tc)
+        uk = np.zeros(n)
+        for k in range(steps):
+            v = ctx.OB_step(uk)
+            zk, zb, xind = ctx.iterEKF(v, uk)
+            lin = ctx.EKFmatsHandler(zk, xind)
+            uk, ne = ctx.iterMPC(lin, zk[:, -1])
+            np.testing.assert_array_equal(v, fused["v"][k])
+            np.testing.assert_array_equal(uk, fused["u"][k])
+            np.testing.assert_array_equal(ne, fused["nexec"][k])

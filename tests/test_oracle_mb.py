@@ -88,11 +88,14 @@ def test_mb_closed_loop_tracks_ob(rom):
     assert all(not m["xhat"].any() for m in b["ekf"]["M"].values())
 
 
-def test_gpu_library_refuses_mb(P):
+def test_library_config_selects_the_blend(P):
+    """make_config(method=...) maps initKF.m:44-49's names onto mpcekf_config.method."""
     M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
-    M.make_config(method="OB")
-    with pytest.raises(NotImplementedError, match="MB"):
-        M.make_config(method="MB")
+    L = importlib.import_module("mpc-ekf4fastcharge_amd._lib")
+    assert M.make_config().method == L.METHOD_OB
+    assert M.make_config(method="OutB").method == L.METHOD_OB
+    assert M.make_config(method="MB").method == L.METHOD_MB
+    assert M.make_config(method="MdlB").method == L.METHOD_MB
     with pytest.raises(ValueError):
         M.make_config(method="UKF")
 
