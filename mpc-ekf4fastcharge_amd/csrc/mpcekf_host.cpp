@@ -77,6 +77,8 @@ struct mpcekf_ctx {
   int *d_xm = nullptr;        // fused step: Xind hand-off iterEKF kernel -> EKFmatsHandler kernel
   double *d_xg = nullptr;
   bool split_cell = false;    // fused step: k_cell as two kernels (MPCEKF_SPLIT_CELL=1; slower, 0.125 vs 0.118 ms)
+  bool quad = false;          // fused step: iterEKF in k_ekf4 (lane quad per cell), then k_cell<P_MPC>
+  int ekf4_block = 512;       // k_ekf4 block size (MPCEKF_EKF4_BLOCK=1024: 4 waves per SIMD, 128 VGPRs)
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
@@ -424,6 +426,15 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   }
   // MPCEKF_SPLIT_CELL=1: the fused step's k_cell as two kernels (results identical).
   if (const char *e = std::getenv("MPCEKF_SPLIT_CELL")) X->split_cell = std::atoi(e) != 0;
+  // k_ekf4 (a lane quad per cell for iterEKF; needs four distinct corners: nT > 1, nZ > 1)
+  // is kept as an option, off by default: measured against k_cell it loses at every batch
+  // size (0.080 vs 0.075 ms at 1,024 cells, 0.098 vs 0.090 at 16,384, 0.20 vs 0.11 at 65,536;
+  // profiles/r02g_*): the per-cell scalar work is replicated four times and the 512-thread
+  // blocks run two rounds per CU.  MPCEKF_QUAD=1 turns it on (results identical).
+  const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide;
+  X->quad = false;
+  if (const char *e = std::getenv("MPCEKF_QUAD")) X->quad = quad_ok && std::atoi(e) != 0;
+  if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) X->ekf4_block = std::atoi(e) == 1024 ? 1024 : 512;
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
   const size_t n = (size_t)ncells, NM = (size_t)X->NM;
@@ -678,17 +689,21 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       iow.normdu_out = io.normdu_out;
       iow.nviol_out = io.nviol_out;
       if ((rc = lerr(launch_mpc_wide(X->k, X->s, iow, X->w, X->stream), "mpc_wide"))) return rc;
-    } else if (X->split_cell) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
+    } else if (X->split_cell || X->quad) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
       io.xm_out = X->d_xm;
       io.xg_out = X->d_xg;
-      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) return rc;
+      if (X->quad) {
+        if ((rc = lerr(launch_ekf4(X->r, X->k, X->s, io, X->stream, X->ekf4_block), "ekf4"))) return rc;
+      } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) {
+        return rc;
+      }
       KIO io2 = io;
       io2.zk = nullptr;
       io2.zbk = nullptr;
       io2.bnd = nullptr;
       io2.xm_out = nullptr;
       io2.xg_out = nullptr;
-      io2.zk_in = X->d_zk;
+      io2.zk_in = io.zk;
       io2.xm_in = X->d_xm;
       io2.xg_in = X->d_xg;
       if ((rc = lerr(launch_cell(X->r, X->k, X->s, io2, X->stream, P_MPC), "cell"))) return rc;

@@ -95,6 +95,25 @@ __device__ __forceinline__ double dasinh(double x) {
   return x < 0 ? -t : t;
 }
 
+// v from the quad lane selected by DPP quad_perm control CTRL.
+template <int CTRL>
+__device__ __forceinline__ double qperm(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+template <int Q>
+__device__ __forceinline__ double qbc(double v) {  // lane Q's v in every lane of the quad
+  return qperm<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v);
+}
+__device__ __forceinline__ double shfl64(double v, int lane) {  // v of lane (runtime), ds_bpermute
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(lane << 2, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(lane << 2, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 __device__ __forceinline__ double tabi(const double *t, int n, double x) {
   if (x != x) return __builtin_nan("");
   double xc = fmin(fmax(x, 0.0), 1.0);
@@ -325,8 +344,44 @@ __device__ __forceinline__ bool is_pd5(const double a[NPK]) {
   return pd;
 }
 
+// The symmetrisation of meas_update_regs when some lane of the wave is not positive
+// definite: HH = V|Lambda|V' by Jacobi (out of line: rare, and its registers would
+// otherwise weigh on every caller).
+template <bool INL>
+__device__ __forceinline__ void meas_polar(const double Ps[NPK], double a[NPK], double S[NPK], bool pd, bool bump) {
+  double H[NPK];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) H[i] = a[i];
+  double V[NX * NX];
+  jacobi5(a, V);
+  double w[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) w[k] = fabs(a[pk(k, k)]);
+#pragma unroll
+  for (int r = 0; r < NX; ++r)
+#pragma unroll
+    for (int c = r; c < NX; ++c) {
+      double hrc = 0.0, hcr = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) {
+        hrc = hrc + (V[r * NX + k] * w[k]) * V[c * NX + k];
+        hcr = hcr + (V[c * NX + k] * w[k]) * V[r * NX + k];
+      }
+      if (pd) { hrc = H[pk(r, c)]; hcr = H[pk(r, c)]; }
+      double v = ((Ps[pk(r, c)] + hrc) + hcr) / 4.0;
+      if (bump) v = v * 2.0;
+      S[pk(r, c)] = v;
+    }
+}
+
+__device__ __noinline__ void meas_polar_slow(const double Ps[NPK], double a[NPK], double S[NPK], bool pd,
+                                             bool bump) {
+  meas_polar<false>(Ps, a, S, pd, bump);
+}
+
 // iterEKF.m:137-153 on one corner record (orc_meas_cov + state update).
 // P = Sigma - (L*St)*L' is only ever used as P + P', so only that sum is kept.
+template <bool OUTLINE = false>  // OUTLINE: the Jacobi branch as a call (k_ekf4's 128/256-VGPR budget)
 __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], const double L[NX], double St,
                                                  double res) {
 #pragma unroll
@@ -342,8 +397,10 @@ __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], co
       double prc = __builtin_fma(-LS[r], L[c], S[pk(r, c)]);
       double pcr = __builtin_fma(-LS[c], L[r], S[pk(r, c)]);
       Ps[pk(r, c)] = prc + pcr;
-      a[pk(r, c)] = (prc + pcr) * 0.5;
     }
+  // a = (P + P')/2: the same operation on the same sum, formed where it is used
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) a[i] = Ps[i] * 0.5;
   const bool bump = res * res > 9 * St;
   // HH = VV*SS*VV' (iterEKF.m:145-146) is the polar factor of the symmetric part a:
   // a itself when a is positive definite (the usual case), else V|Lambda|V' (Jacobi).
@@ -356,30 +413,10 @@ __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], co
       if (bump) v = v * 2.0;
       S[i] = v;
     }
+  } else if constexpr (OUTLINE) {
+    meas_polar_slow(Ps, a, S, pd, bump);
   } else {
-    double H[NPK];
-#pragma unroll
-    for (int i = 0; i < NPK; ++i) H[i] = a[i];
-    double V[NX * NX];
-    jacobi5(a, V);
-    double w[NX];
-#pragma unroll
-    for (int k = 0; k < NX; ++k) w[k] = fabs(a[pk(k, k)]);
-#pragma unroll
-    for (int r = 0; r < NX; ++r)
-#pragma unroll
-      for (int c = r; c < NX; ++c) {
-        double hrc = 0.0, hcr = 0.0;
-#pragma unroll
-        for (int k = 0; k < NX; ++k) {
-          hrc = hrc + (V[r * NX + k] * w[k]) * V[c * NX + k];
-          hcr = hcr + (V[c * NX + k] * w[k]) * V[r * NX + k];
-        }
-        if (pd) { hrc = H[pk(r, c)]; hcr = H[pk(r, c)]; }
-        double v = ((Ps[pk(r, c)] + hrc) + hcr) / 4.0;
-        if (bump) v = v * 2.0;
-        S[pk(r, c)] = v;
-      }
+    meas_polar<true>(Ps, a, S, pd, bump);
   }
 }
 
@@ -403,10 +440,12 @@ struct CellCtx {
 };
 
 // getVariables (iterEKF.m:259-417).  Z is the permuted output vector.
-template <int NZ>
+// QUAD: a lane quad per cell (k_ekf4): this lane's corner is qj with state xr[0]; the
+// corner sums Z = fma(z_j, g_j, Z), j = 0..3 in order, take z_j from lane j by DPP.
+template <int NZ, bool QUAD = false>
 __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, const XI &xi, double ik, double x0,
                                            double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc,
-                                           const double (*xr)[NX] = nullptr) {
+                                           const double (*xr)[NX] = nullptr, int qj = 0) {
   double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
   double SOCnAvg = cc.et.soc(0, xSOC);
   double SOCpAvg = cc.et.soc(1, xSOC);
@@ -416,8 +455,38 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   if (SOCpAvg > 0.998) { warn++; SOCpAvg = 0.998; }
 #pragma unroll
   for (int q = 0; q < NZ; ++q) Z[q] = 0.0;
+  if constexpr (QUAD) {
+    const double *Cm = cc.L + xi.m[qj] * cc.stride;
+    const double *Dm = Cm + NZ * NX;
+    double cr[NX + 1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+    for (int k = 0; k < NX; ++k) cr[k] = Cm[k];
+    cr[NX] = Dm[0];
+#pragma unroll
+    for (int q = 0; q < NZ; ++q) {
+      double cn[NX + 1];
+      if (q + 1 < NZ) {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) cn[k] = Cm[(q + 1) * NX + k];
+        cn[NX] = Dm[q + 1];
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) acc = __builtin_fma(cr[k], xr[0][k], acc);
+      const double zj = __builtin_fma(cr[NX], ik, acc);
+      double zz = __builtin_fma(qbc<0>(zj), xi.g[0], 0.0);
+      zz = __builtin_fma(qbc<1>(zj), xi.g[1], zz);
+      zz = __builtin_fma(qbc<2>(zj), xi.g[2], zz);
+      Z[q] = __builtin_fma(qbc<3>(zj), xi.g[3], zz);
+      launder(Z[q]);  // rows in order: the next row's operands are the only ones in flight
+      if (q + 1 < NZ) {
+#pragma unroll
+        for (int k = 0; k <= NX; ++k) cr[k] = cn[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < (QUAD ? 0 : 4); ++j) {
     double x[NX];
     if (xr) {
 #pragma unroll
@@ -454,6 +523,7 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  __builtin_amdgcn_sched_barrier(0);
   double If0 = Z[R_IF0], If3 = Z[R_IF3];
   bool any = false;
 #pragma unroll
@@ -579,6 +649,38 @@ __device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, cons
 #pragma unroll
   for (int j = 0; j < 4; ++j) chat_row(r, K, cc.L + xi.m[j] * cc.stride, xi.g[j], Chat[j]);
   Chat0 = chat0(r, K);
+}
+
+// getChatZ's scalars at the updated state (iterEKF.m:190, 543, 562-580): for k_bounds
+struct BoundK {
+  ChatK K;
+  double C0, r0n, r0p, dUn, dUp;
+};
+__device__ __forceinline__ BoundK bound_k(const KRom &r, const CellCtx &cc, double xSOC, double zTE1, double zTH0,
+                                          double zTEE, double zTH3) {
+  BoundK b;
+  b.K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
+  b.C0 = chat0(r, b.K);
+  b.r0n = -r.Ts * b.K.dn / (3600 * r.Q);  // iterEKF.m:562-565
+  b.r0p = -r.Ts * b.K.dp / (3600 * r.Q);
+  b.dUn = cc.et.f(0, EF_DU, cc.et.soc(0, xSOC));  // iterEKF.m:576-580
+  b.dUp = cc.et.f(1, EF_DU, cc.et.soc(1, xSOC));
+  return b;
+}
+__device__ __forceinline__ double bound_field(const BoundK &b, int i) {  // BD_K + i, i < 11
+  switch (i) {
+    case 0: return b.K.Rfn;
+    case 1: return b.K.Rfp;
+    case 2: return b.K.Rctn;
+    case 3: return b.K.Rctp;
+    case 4: return b.K.dUn0;
+    case 5: return b.K.dUp3;
+    case 6: return b.C0;
+    case 7: return b.r0n;
+    case 8: return b.r0p;
+    case 9: return b.dUn;
+    default: return b.dUp;
+  }
 }
 
 // MPC pieces (predMat.m, constraintsMPC.m, iterMPC.m) live in mpcekf_mpc.hpp,
@@ -1956,11 +2058,9 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
         bd[(BD_G + j) * n + c] = xi.g[j];
         bd[(BD_M + j) * n + c] = xi.m[j];
       }
-      bd[(BD_Z + 0) * n + c] = Z[R_TE1];
-      bd[(BD_Z + 1) * n + c] = Z[R_TH0];
-      bd[(BD_Z + 2) * n + c] = Z[R_TEE];
-      bd[(BD_Z + 3) * n + c] = Z[R_TH3];
-      bd[BD_X0 * n + c] = x0;
+      const BoundK b = bound_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3]);
+#pragma unroll
+      for (int i = 0; i < 11; ++i) bd[(BD_K + i) * n + c] = bound_field(b, i);
       bd[BD_S0 * n + c] = S0;
     }
     STAMP(9);
@@ -2087,23 +2187,210 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 }
 
 // ---------------------------------------------------------------------------
+// k_ekf4: the fused step's iterEKF ('OB', iterEKF.m:55-210) with a lane quad per cell,
+// lane j = corner j of getXind: its record's catch-up, its getVariables term, its
+// getChatV row, gain and measurement update run in parallel; the corner sums keep the
+// one-lane order through DPP broadcasts (get_vars<NZ, true>), so every result is
+// k_cell's to the bit.  EKFmatsHandler + iterMPC follow in k_cell<NZ, P_MPC> from the
+// zk / Xind hand-off.  Needs distinct corners (nT > 1 and nZ > 1; host checks).
+// 1024-thread blocks (256 cells): the ~130 KB ROM blob is staged once per CU and the
+// CU runs 4 waves per SIMD.
+// ---------------------------------------------------------------------------
+template <int NZ, int BLOCK>
+__global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, const KState s, const KIO io) {
+  extern __shared__ double lds[];
+  stage_lds(lds, r.cell_blob, r.cell_len);
+  __syncthreads();
+  const double *Tp = lds + r.cell_tab + r.cell_tablen;
+  const double *Zp = Tp + MAXT;
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = s.n;
+  const int j = (int)(gt & 3);
+  const int64_t cq = gt >> 2;
+  const bool live = cq < n;
+  const int64_t c = live ? cq : n - 1;  // lanes past n ride along (quad exchanges), write nothing
+  const int nz = r.nz;
+  const double NaN = __builtin_nan("");
+  CellCtx cc;
+  cc.L = lds;
+  cc.Tp = Tp;
+  cc.Zp = Zp;
+  cc.erec = s.ekf + (size_t)c * r.NM * REC;
+  cc.stride = r.cell_stride;
+  const double Tc = s.Tc[c];
+  cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
+  cc.et = etab(r, lds + r.cell_tab, cc.T);
+  int st = s.status[c];
+  const int t = io.lazy_t;
+  if (live && j == 0) s.hflag[c] = 0;
+  auto fail_outputs = [&]() {
+    if (!live) return;
+    if (j == 0) {
+      if (io.u) io.u[c] = NaN;
+      if (io.v) io.v[c] = NaN;
+      if (io.soc) io.soc[c] = NaN;
+      if (io.phise) io.phise[c] = NaN;
+      if (io.nexec) io.nexec[c] = 0;
+      if (io.bnd) io.bnd[BD_M * n + c] = -1.0;
+      if (io.x_out)
+        for (int q = 0; q < 6; ++q) io.x_out[c * 6 + q] = NaN;
+      if (io.junc_out) io.junc_out[c] = NaN;
+      if (io.jfin_out) io.jfin_out[c] = NaN;
+      if (io.normdu_out) io.normdu_out[c] = NaN;
+      if (io.nviol_out) io.nviol_out[c] = 0;
+    }
+    if (io.zk)
+      for (int q = j; q < nz + 2; q += 4) io.zk[c * (nz + 2) + q] = NaN;
+    if (io.zbk)
+      for (int q = j; q < nz + 2; q += 4) io.zbk[c * (nz + 2) + q] = NaN;
+    if (io.xm_out) { io.xm_out[c * 4 + j] = -1; io.xg_out[c * 4 + j] = NaN; }
+  };
+  if (st & ST_ERROR) {
+    fail_outputs();
+    return;
+  }
+  const double ik = s.uk[c], vk = s.vk[c];
+  int warn = s.warn[c];
+  if (warn > cf.max_warn) {  // iterEKF.m:55-59
+    st |= ST_LOCKOUT | ST_ERROR;
+    if (live && j == 0) { s.status[c] = st; s.uk[c] = NaN; }
+    fail_outputs();
+    return;
+  }
+  double x0 = s.x0[c] + s.priorI[c];  // iterEKF.m:85-86
+  double S0 = s.S0[c] + cf.SigmaW;
+  const double SOC0 = s.SOC0[c];
+  XI xi;
+  get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC0 - x0 * (r.Ts / (3600 * r.Q)), xi);
+  // this lane's corner: record, caught up over the steps its time update skipped
+  const int mj = xi.m[j];
+  double *rec = cc.erec + (size_t)mj * REC;
+  const double *am = cc.L + mj * cc.stride + NZ * NX + NZ;  // diag(A), then a_p a_q
+  double xr[1][NX];
+  load_x(rec, xr[0]);
+  const int tsj = s.ts_ekf[c * r.NM + mj];
+  const double pt = s.hist_p[(size_t)(t % LAZY_H) * n + c];
+  replay_x(xr[0], am, tsj, t, pt, s, c);
+  __builtin_amdgcn_sched_barrier(0);
+  double Z[NZ], Zsoc;
+  double vhat = get_vars<NZ, true>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr, j);
+  if (st & ST_ERROR) {
+    if (live && j == 0) { s.status[c] = st; s.warn[c] = warn; s.uk[c] = NaN; }
+    fail_outputs();
+    return;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // getChatV (iterEKF.m:421-519): this corner's row; gains against corner 1's Sigma
+  const ChatK K = chat_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3]);
+  double Ch[NX];
+  chat_row(r, K, cc.L + mj * cc.stride, xi.g[j], Ch);
+  const double C0 = chat0(r, K);
+  double Sj[NPK];
+  load_S(rec, Sj);
+  replay_S(Sj, am, tsj, t, cf.SigmaW);
+  double S1[NPK];
+#pragma unroll
+  for (int i = 0; i < NPK; ++i) S1[i] = qbc<0>(Sj[i]);
+  double row[NX];
+#pragma unroll
+  for (int cI = 0; cI < NX; ++cI) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) acc = __builtin_fma(S1[pk(k, cI)], Ch[k], acc);
+    row[cI] = acc;
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int cI = 0; cI < NX; ++cI) acc = __builtin_fma(row[cI], Ch[cI], acc);
+  const double Stj = acc + cf.SigmaV;
+  double Lg[NX];
+#pragma unroll
+  for (int k = 0; k < NX; ++k) Lg[k] = row[k] / Stj;
+  const double St0 = C0 * S0 * C0 + cf.SigmaV;
+  const double L0 = S0 * C0 / St0;
+  const double res = vk - vhat;
+  __builtin_amdgcn_sched_barrier(0);
+  // iterEKF.m:137-153: corner j's record (distinct corners: the updates are independent)
+  meas_update_regs<true>(xr[0], Sj, Lg, Stj, res);
+  if (live) {
+    store_rec(rec, xr[0], Sj);
+    s.ts_ekf[c * r.NM + mj] = t;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  x0 = __builtin_fma(L0, res, x0);
+  S0 = S0 - L0 * St0 * L0;
+  int mold[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mold[i] = xi.m[i];
+  get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC0 - x0 * (r.Ts / (3600 * r.Q)), xi);
+  // the new corner j: one this step just updated (its state comes from that lane's
+  // registers), or an untouched model whose record is caught up to step t here
+  // (ekf_catch_up4)
+  const int mn = xi.m[j];
+  int src = -1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (mold[i] == mn) src = i;
+  {
+    const int from = (threadIdx.x & ~3) + (src < 0 ? j : src);
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xr[0][k] = shfl64(xr[0][k], from);
+  }
+  if (src < 0) {
+    double *recn = cc.erec + (size_t)mn * REC;
+    const int tsn = s.ts_ekf[c * r.NM + mn];
+    double Sn[NPK];
+    load_rec(recn, xr[0], Sn);
+    if (tsn < t) {
+      const double *an = cc.L + mn * cc.stride + NZ * NX + NZ;
+      replay_x(xr[0], an, tsn, t, pt, s, c);
+      replay_S(Sn, an, tsn, t, cf.SigmaW);
+      if (live) {
+        store_rec(recn, xr[0], Sn);
+        s.ts_ekf[c * r.NM + mn] = t;
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  vhat = get_vars<NZ, true>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr, j);
+  __builtin_amdgcn_sched_barrier(0);
+  if (!live) return;
+  if (j == 0) s.warn[c] = warn;
+  if (st & ST_ERROR) {
+    if (j == 0) { s.status[c] = st; s.x0[c] = x0; s.S0[c] = S0; s.uk[c] = NaN; }
+    fail_outputs();
+    return;
+  }
+  if (io.bnd) {  // boundzk (iterEKF.m:186-205) runs in k_bounds from this record
+    io.bnd[(BD_G + j) * n + c] = xi.g[j];
+    io.bnd[(BD_M + j) * n + c] = xi.m[j];
+    const BoundK b = bound_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3]);
+#pragma unroll
+    for (int i = 0; i < 11; ++i)
+      if ((i & 3) == j) io.bnd[(BD_K + i) * n + c] = bound_field(b, i);
+    if (j == 3) io.bnd[BD_S0 * n + c] = S0;
+  }
+  if (j == 0) {
+    s.x0[c] = x0;
+    s.S0[c] = S0;
+    s.priorI[c] = ik;  // iterEKF.m:210
+  }
+  if (io.zk) {
+#pragma unroll
+    for (int q = 0; q < NZ; ++q)
+      if (q < nz && (q & 3) == j) io.zk[c * (nz + 2) + r.perm[q]] = Z[q];
+    if (j == 1) io.zk[c * (nz + 2) + nz] = vhat;
+    if (j == 2) io.zk[c * (nz + 2) + nz + 1] = Zsoc;
+  }
+  if (io.xm_out) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
+}
+
+// ---------------------------------------------------------------------------
 // k_bounds: boundzk (iterEKF.m:186-205; getChatZ iterEKF.m:523-602), diagonal only.
 // A lane quad per cell, lane j = corner j: its getChatV row, its 26 quadratic forms
 // row' * Sigma1 * row; the corner sums keep k_cell's order ((((0 + q0) + q1) + q2)
 // + q3) through DPP broadcasts, so the result is the one-lane form's bits.
 // ---------------------------------------------------------------------------
-// v from the quad lane selected by DPP quad_perm control CTRL.
-template <int CTRL>
-__device__ __forceinline__ double qperm(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-template <int Q>
-__device__ __forceinline__ double qbc(double v) {  // lane Q's v in every lane of the quad
-  return qperm<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v);
-}
 __device__ __forceinline__ double quad_sum_seq(double v) {  // (((0 + v0) + v1) + v2) + v3
   return (((0.0 + qbc<0>(v)) + qbc<1>(v)) + qbc<2>(v)) + qbc<3>(v);
 }
@@ -2111,7 +2398,8 @@ __device__ __forceinline__ double quad_sum_seq(double v) {  // (((0 + v0) + v1) 
 // 256 cells per block: the ~90 KB model blob leaves room for one block per CU, so the
 // block is the CU's whole occupancy (4 waves per SIMD) and stages the blob once.
 constexpr int BOUNDS_BLOCK = 1024;
-__host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.cell_len + 1; }  // after the blob
+// k_bounds stages only the models of the cell blob (its getChatV scalars come from k_cell)
+__host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.cell_tab + 1; }
 // row' * Sigma * row in symmetric form: T = Sigma with doubled off-diagonals,
 // u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, explicit fma at every step
 // (orc qform: 20 operations instead of the 60 of Sigma*row then row'*(.)).
@@ -2130,7 +2418,7 @@ __device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]
 template <int NZ>
 __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KState s, const double *bd, double *zbk) {
   extern __shared__ double lds[];
-  stage_lds(lds, r.cell_blob, r.cell_len);
+  stage_lds(lds, r.cell_blob, r.cell_tab);
   __syncthreads();
   const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
@@ -2139,18 +2427,10 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   const int64_t c = cq < n ? cq : n - 1;  // lanes past n ride along (quad exchanges)
   const int nz = r.nz;
   const bool valid = cq < n && bd[BD_M * n + c] >= 0.0;
-  CellCtx cc;
-  cc.L = lds;
-  cc.stride = r.cell_stride;
-  const double Tc = s.Tc[c];
-  cc.T = Tc > 100 ? Tc : Tc + 273.15;
-  cc.et = etab(r, lds + r.cell_tab, cc.T);
   const double g = bd[(BD_G + j) * n + c];
   const int m = valid ? (int)bd[(BD_M + j) * n + c] : 0;
-  const double *Cm = cc.L + m * cc.stride;
-  const double zTE1 = bd[(BD_Z + 0) * n + c], zTH0 = bd[(BD_Z + 1) * n + c];
-  const double zTEE = bd[(BD_Z + 2) * n + c], zTH3 = bd[(BD_Z + 3) * n + c];
-  const double x0 = bd[BD_X0 * n + c], S0 = bd[BD_S0 * n + c];
+  const double *Cm = lds + m * r.cell_stride;
+  const double S0 = bd[BD_S0 * n + c];
   // SigmaX of the first corner for all four (iterEKF.m:191)
   double S1b[NPK];
   load_S(s.ekf + ((size_t)c * r.NM + (valid ? (int)bd[BD_M * n + c] : 0)) * REC, S1b);
@@ -2158,15 +2438,19 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   for (int k = 0; k < NX; ++k)
 #pragma unroll
     for (int l = k + 1; l < NX; ++l) S1b[pk(k, l)] = 2 * S1b[pk(k, l)];
-  const double xSOC = s.SOC0[c] - x0 * (r.Ts / (3600 * r.Q));
-  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
+  // getChatV's scalars at the updated state, from k_cell (bound_k)
+  ChatK K;
+  K.Rfn = bd[(BD_K + 0) * n + c];
+  K.Rfp = bd[(BD_K + 1) * n + c];
+  K.Rctn = bd[(BD_K + 2) * n + c];
+  K.Rctp = bd[(BD_K + 3) * n + c];
+  K.dUn0 = bd[(BD_K + 4) * n + c];
+  K.dUp3 = bd[(BD_K + 5) * n + c];
   double ChV[NX];
   chat_row(r, K, Cm, g, ChV);
-  const double ChV0 = chat0(r, K);
-  const double res0n = -r.Ts * K.dn / (3600 * r.Q);  // iterEKF.m:562-565
-  const double res0p = -r.Ts * K.dp / (3600 * r.Q);
-  const double dUn = cc.et.f(0, EF_DU, cc.et.soc(0, xSOC));  // iterEKF.m:576-580
-  const double dUp = cc.et.f(1, EF_DU, cc.et.soc(1, xSOC));
+  const double ChV0 = bd[BD_C0 * n + c];
+  const double res0n = bd[BD_R0N * n + c], res0p = bd[BD_R0P * n + c];
+  const double dUn = bd[BD_DUN * n + c], dUp = bd[BD_DUP * n + c];
   const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
   double cph0[NX];
 #pragma unroll
@@ -2650,6 +2934,31 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
     default: return -1;
   }
   if (rc) return rc;
+  return (int)hipGetLastError();
+}
+
+template <int NZ, int BLOCK>
+static void launch_ekf4_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void *)k_ekf4<NZ, BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_ekf4<NZ, BLOCK>), dim3(grid_for(s.n * 4, BLOCK)), dim3(BLOCK), cell_lds_bytes(r), st, r, c,
+                     s, io);
+}
+
+// block = 512 (128 cells, 256 VGPRs, 2 waves per SIMD) or 1024 (256 cells, 128 VGPRs, 4 waves per SIMD)
+int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int block) {
+  if (s.n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const bool big = block == 1024;
+  switch (r.nzp) {
+    case 26: big ? launch_ekf4_t<26, 1024>(r, c, s, io, st) : launch_ekf4_t<26, 512>(r, c, s, io, st); break;
+    case 32: big ? launch_ekf4_t<32, 1024>(r, c, s, io, st) : launch_ekf4_t<32, 512>(r, c, s, io, st); break;
+    default: return -1;
+  }
   return (int)hipGetLastError();
 }
 

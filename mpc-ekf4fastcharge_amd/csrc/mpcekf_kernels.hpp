@@ -100,9 +100,11 @@ struct KIO {
   int *nviol_out;         // [n] viol
 };
 constexpr int NSTAMPS = 12;
-// k_cell -> k_bounds record: g[4], m[4], Z(te1, th0, tee, th3), x0, S0.  k_bounds reads
-// corner 1's Sigma from the EKF record k_cell stored (nothing writes it before the next k_cell).
-enum { BD_G = 0, BD_M = 4, BD_Z = 8, BD_X0 = 12, BD_S0 = 13, NBND = 14 };
+// k_cell -> k_bounds record: g[4], m[4], getChatZ's getChatV scalars at the updated state
+// (Rfn, Rfp, Rctn, Rctp, dUn0, dUp3 of chat_k; its Chat0), res0n, res0p, dUn, dUp
+// (iterEKF.m:562-580), SigmaX0.  k_bounds reads corner 1's Sigma from the EKF record
+// k_cell stored (nothing writes it before the next k_cell).
+enum { BD_G = 0, BD_M = 4, BD_K = 8, BD_C0 = 14, BD_R0N, BD_R0P, BD_DUN, BD_DUP, BD_S0, NBND };
 
 enum { MODE_EKF = 1, MODE_LIN = 2, MODE_MPC = 4, MODE_FUSED = 8 };
 // Which blocks of k_cell an instantiation compiles: the fused step launches the iterEKF
@@ -131,6 +133,9 @@ int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_t
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
 int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int parts = P_ALL);
+// the fused step's iterEKF ('OB') with a lane quad per cell (nT > 1 and nZ > 1): zk /
+// Xind hand-off in io.zk / io.xm_out / io.xg_out for k_cell<P_MPC>, boundzk record in io.bnd
+int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int block = 512);
 // boundzk (iterEKF.m:186-205) from k_cell's hand-off record, a lane quad per cell
 int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk, void *stream);
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream);

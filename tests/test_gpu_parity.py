@@ -423,3 +423,16 @@ def test_model_blend_stage_entry_points_match_fused(rom, M):
             np.testing.assert_array_equal(v, fused["v"][k])
             np.testing.assert_array_equal(uk, fused["u"][k])
             np.testing.assert_array_equal(ne, fused["nexec"][k])
+
+
+def test_lane_quad_ekf_kernel_is_exact(rom, M):
+    """k_ekf4 (iterEKF with a lane quad per cell, MPCEKF_QUAD=1) gives the bits of the
+    lane-per-cell k_cell path over a closed loop, state included."""
+    n = 700
+    soc0, tc = batch_inputs(n, seed=31)
+    a = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=0)
+    b = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=1)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    for k in ("ekf", "bigX", "scal", "lam"):
+        np.testing.assert_array_equal(a["state"][k], b["state"][k], err_msg=k)
