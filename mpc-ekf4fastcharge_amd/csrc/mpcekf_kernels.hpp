@@ -120,6 +120,9 @@ struct KWide {
   double *X;       // [ncon][n][Nc]  X(:,i) = E\M(i,:)'
   double *K, *hii; // [ncon][n]
   int *it;         // [n] hildreth.m sweeps (nexec)
+  int *q;          // [2] work list: cells listed by k_hild_prep, next one k_hild_wide takes
+  int *list;       // [n] the cells whose QP runs on the fast path this step
+  int cus;         // compute units of the device (persistent grid size)
   double *smin;    // [Nc*Nc + 1] GsocT*Gsoc of the configuration and its sigma_min
 };
 

@@ -22,6 +22,7 @@
 // Arithmetic is oracle/mpcekf_oracle.c's defined order, bit for bit.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -127,6 +128,7 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
   if (c >= n) return;
   const bool fused = io.mode & MODE_FUSED;
   s.hflag[c] = 0;
+  if (c == 0) { w.q[0] = 0; w.q[1] = 0; }  // k_hild_prep lists, k_hild_wide takes (this step's QPs)
   if (s.status[c] & ST_ERROR) {  // the fused step's iterEKF kernel already wrote NaN outputs
     if (!fused) {
       if (io.uk_out) io.uk_out[c] = __builtin_nan("");
@@ -354,6 +356,7 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
     if (i < NC || (i >= 2 * NC && i < 3 * NC)) w.hii[(size_t)c * NCON + i + NC] = h;
   }
   if (!fin) s.hflag[c] = 2;
+  else w.list[atomicAdd(&w.q[0], 1)] = (int)c;  // k_hild_wide's work list (any order: cells are independent)
 }
 
 // ---------------------------------------------------------------------------
@@ -409,6 +412,40 @@ __device__ __forceinline__ double row_m(int i, const double *mp) {
   return mp[blk * W<NP, NC>::HPW + r];
 }
 
+// Persistent: a grid of two blocks per CU (two waves per SIMD) takes the cells k_hild_prep
+// listed (w.list, w.q[0] of them) from a global counter (w.q[1]), a 16-lane group at a
+// time.  A group that converges, hits maxIter or leaves the fast form's domain returns
+// its cell and takes the next one at the following sweep start, so the waves work on live
+// cells only (a static cell-to-wave map kept every wave busy until its slowest cell,
+// mean 58 sweeps per wave against 40 per cell).  Each cell's sweeps are the same
+// operations in the same order whichever group runs them, so the results are the
+// order-independent bits of the static kernel.
+template <int NP, int NC>
+__device__ __forceinline__ bool hild_wide_load(const KState &s, const KWide &w, int64_t c, int k, double *lam,
+                                               double *Kl, double2 *hr, double *hp, double X[W<NP, NC>::NX_ROWS]) {
+  using T = W<NP, NC>;
+  constexpr int NCON = T::NCON, HPW = T::HPW;
+  const int64_t n = s.n;
+  bool ok = true;
+  for (int i = k; i < NCON; i += 16) {
+    const double li = s.lam[(size_t)i * n + c];
+    const double hii = w.hii[(size_t)c * NCON + i];
+    const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
+    const double ay = fabs(hii);
+    ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
+    lam[i] = li;
+    Kl[i] = w.K[(size_t)c * NCON + i];
+    hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
+  }
+  for (int j = k; j < 3 * HPW; j += 16) {
+    const int b = j / HPW, q = j % HPW;
+    hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
+  }
+#pragma unroll
+  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
+  return ok;
+}
+
 template <int NP, int NC>
 __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
   using T = W<NP, NC>;
@@ -416,111 +453,108 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
   extern __shared__ double lds[];
   double *zero = lds;  // NCON zeros: lanes that add no K_i / no M entry read these
   const int g = threadIdx.x >> 4, k = threadIdx.x & 15;
-  const int64_t n = s.n, c = (int64_t)blockIdx.x * T::GROUPS + g;
+  const int64_t n = s.n;
   double *base = lds + NCON + g * T::CELL_LDS;
   double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
   double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
-  const bool act = c < n && s.hflag[c] == 1;
-  bool ok = true;
-  if (act) {
-    for (int i = k; i < NCON; i += 16) {
-      const double li = s.lam[(size_t)i * n + c];
-      const double hii = w.hii[(size_t)c * NCON + i];
-      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
-      const double ay = fabs(hii);
-      ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
-      lam[i] = li;
-      Kl[i] = w.K[(size_t)c * NCON + i];
-      hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
-    }
-    for (int j = k; j < 3 * HPW; j += 16) {
-      const int b = j / HPW, q = j % HPW;
-      hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
-    }
-  }
   __syncthreads();
-  if (!act) return;
   const int gshift = 16 * (g & 3);
-  if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
-    if (k == 0) s.hflag[c] = 2;
-    return;
-  }
+  const int ncells = w.q[0];
   const double *kp = k == 0 ? Kl : zero;
   const double *mp = k < NC ? hp + (NC - 1) - k : zero;
-  double X[T::NX_ROWS];
-#pragma unroll
-  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
-  int it;
-  bool slow = false;
-  for (it = 1; it <= maxIter; ++it) {
-    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
-    // of the loop they would need ~400 more registers
-    asm volatile("" ::: "memory");
-    double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
-#pragma unroll
-    for (int j = 0; j < NCON; ++j) {
-      if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
-      const double x = X[xslot<NP, NC>(j)];
-      v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
-    }
-    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
-    // row i's LDS operands are read one row ahead (ds_read latency off the chain)
-    double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
-    double2 h = hr[0];
-#pragma unroll
-    for (int i = 0; i < NCON; ++i) {
-      asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
-      double kzn = kz, lin = li, mn = m;
-      double2 hn = h;
-      if (i + 1 < NCON) {
-        kzn = kp[i + 1];
-        lin = lam[i + 1];
-        hn = hr[i + 1];
-        mn = row_m<NP, NC>(i + 1, mp);
+  double X[T::NX_ROWS];
+  int64_t c = -1;      // the group's cell (-1: none)
+  bool drained = false;  // the list is exhausted for this group
+  int it = 0;
+  for (;;) {
+    if (c < 0 && !drained) {  // take the next listed cell (group-uniform)
+      int idx = 0;
+      if (k == 0) idx = atomicAdd(&w.q[1], 1);
+      idx = __shfl(idx, 0, 16);
+      if (idx < ncells) {
+        const int64_t cn = w.list[idx];
+        const bool ok = hild_wide_load<NP, NC>(s, w, cn, k, lam, Kl, hr, hp, X);
+        if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
+          if (k == 0) s.hflag[cn] = 2;
+        } else {
+          c = cn;
+          it = 0;
+        }
+      } else {
+        drained = true;
       }
-      const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
-      // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
-      // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
-      // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
-      const double num = __builtin_fma(h.x, li, -t);
-      const double q0 = num * h.y;
-      const double e2 = __builtin_fma(-h.x, q0, num);
-      const double wf = __builtin_fma(e2, h.y, q0);
-      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
-      const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
-      xmax = fmax(xmax, fabs(num));
-      xmin = fmin(xmin, fabs(num));
-      const double nl = wv > 0 ? wv : 0.0;
-      const double d = nl - li;
-      dmax = fmax(dmax, fabs(d));
-      lam[i] = nl;
-      const double x = X[xslot<NP, NC>(i)];
-      v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
-      kz = kzn;
-      li = lin;
-      h = hn;
-      m = mn;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
-    // the fast division's domain: the exact path redoes this cell from its warm start,
-    // still in s.lam (every sweep before was bit-identical to the exact form)
-    const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
-    if ((__ballot(bad) >> gshift) & 0xFFFFull) {
-      slow = true;
-      break;
+    if (!__any(c >= 0 || !drained)) break;  // every group of the wave is done
+    if (c >= 0) {
+      ++it;
+      // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
+      // of the loop they would need ~400 more registers
+      asm volatile("" ::: "memory");
+      double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
+#pragma unroll
+      for (int j = 0; j < NCON; ++j) {
+        if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
+        const double x = X[xslot<NP, NC>(j)];
+        v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
+      }
+      double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+      // row i's LDS operands are read one row ahead (ds_read latency off the chain)
+      double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
+      double2 h = hr[0];
+#pragma unroll
+      for (int i = 0; i < NCON; ++i) {
+        asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
+        double kzn = kz, lin = li, mn = m;
+        double2 hn = h;
+        if (i + 1 < NCON) {
+          kzn = kp[i + 1];
+          lin = lam[i + 1];
+          hn = hr[i + 1];
+          mn = row_m<NP, NC>(i + 1, mp);
+        }
+        const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
+        // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
+        // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
+        // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
+        const double num = __builtin_fma(h.x, li, -t);
+        const double q0 = num * h.y;
+        const double e2 = __builtin_fma(-h.x, q0, num);
+        const double wf = __builtin_fma(e2, h.y, q0);
+        const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
+        const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
+        xmax = fmax(xmax, fabs(num));
+        xmin = fmin(xmin, fabs(num));
+        const double nl = wv > 0 ? wv : 0.0;
+        const double d = nl - li;
+        dmax = fmax(dmax, fabs(d));
+        lam[i] = nl;
+        const double x = X[xslot<NP, NC>(i)];
+        v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
+        kz = kzn;
+        li = lin;
+        h = hn;
+        m = mn;
+      }
+      // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
+      // the fast division's domain: the exact path redoes this cell from its warm start,
+      // still in s.lam (every sweep before was bit-identical to the exact form)
+      const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
+      if ((__ballot(bad) >> gshift) & 0xFFFFull) {
+        if (k == 0) s.hflag[c] = 2;
+        c = -1;
+      } else if (dmax < tol || it >= maxIter) {
+        for (int i = k; i < NCON; i += 16) s.lam[(size_t)i * n + c] = lam[i];
+        if (k == 0) w.it[c] = it;
+        c = -1;
+      }
     }
-    if (dmax < tol) break;
   }
-  if (slow) {
-    if (k == 0) s.hflag[c] = 2;
-    return;
-  }
-  if (it > maxIter) it = maxIter;
-  for (int i = k; i < NCON; i += 16) s.lam[(size_t)i * n + c] = lam[i];
-  if (k == 0) w.it[c] = it;
 }
 
 // ---------------------------------------------------------------------------
@@ -871,8 +905,9 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
     attr = true;
   }
   hipLaunchKernelGGL((k_hild_prep<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, s, w);
-  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)), dim3(256), lds,
-                     st, c, s, w);
+  // persistent: two 4-wave blocks per CU (the register file holds two waves per SIMD)
+  const int blocks = std::min(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS), 2 * std::max(w.cus, 1));
+  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(blocks), dim3(256), lds, st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
   hipLaunchKernelGGL((k_mpc_wide_finish<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, io, w);
   return (int)hipGetLastError();
