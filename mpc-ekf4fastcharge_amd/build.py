@@ -46,13 +46,16 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def build(force=False, verbose=False, variant=""):
-    """variant "stamps": profiling build _build/libmpcekf_stamps.so (-DMPCEKF_STAMPS)."""
+def build(force=False, verbose=False, variant="", defines=()):
+    """variant "stamps": profiling build _build/libmpcekf_stamps.so (-DMPCEKF_STAMPS);
+    any other variant name with ``defines`` (["NAME=VAL", ..]) builds an A/B library
+    _build/libmpcekf_<variant>.so that bench.py loads through MPCEKF_LIB."""
     os.makedirs(OUT, exist_ok=True)
     jobs = []
     objs = []
     sfx = f"_{variant}" if variant else ""
     extra = ["-DMPCEKF_STAMPS"] if variant == "stamps" else []
+    extra += [f"-D{d}" for d in defines]
     extra.append(f'-DMPCEKF_SRC_HASH="{source_hash()}"')
     lib = os.path.join(OUT, f"libmpcekf{sfx}.so")
     for s in SOURCES:
@@ -78,4 +81,11 @@ def build(force=False, verbose=False, variant=""):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, variant="stamps" if "--stamps" in sys.argv else ""))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--stamps", action="store_true")
+    ap.add_argument("--variant", default="")
+    ap.add_argument("-D", dest="defines", action="append", default=[])
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, variant="stamps" if a.stamps else a.variant, defines=a.defines))

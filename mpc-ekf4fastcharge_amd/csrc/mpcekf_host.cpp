@@ -474,14 +474,14 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
     if ((rc = dalloc(&w.prob, n * wide_prob_doubles(w.Np, w.Nc))) || (rc = dalloc(&w.X, nc * n * w.Nc)) ||
         (rc = dalloc(&w.K, nc * n)) || (rc = dalloc(&w.hii, nc * n)) || (rc = dalloc(&w.it, n)) ||
         (rc = dalloc(&w.smin, (size_t)w.Nc * w.Nc + 1)) || (rc = dalloc(&X->d_lin, n * MPCEKF_LIN_SIZE)) ||
-        (rc = hipMalloc((void **)&w.q, 2 * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) ||
-        (rc = hipMalloc((void **)&w.list, (n + 1) * sizeof(int)) == hipSuccess ? 0 : MPCEKF_E_HIP) ||
+        (rc = dalloc(&w.q, 1)) || (rc = dalloc(&w.list, n)) || (rc = dalloc(&w.hist, 128)) ||
         (rc = dalloc(&X->d_zsoc, n))) {
       mpcekf_ctx_destroy(X);
       return rc;
     }
-    HIPCHK(hipMemset(w.q, 0, 2 * sizeof(int)));
-    HIPCHK(hipDeviceGetAttribute(&w.cus, hipDeviceAttributeMultiprocessorCount, device));
+    HIPCHK(hipMemset(w.q, 0, sizeof(int)));
+    HIPCHK(hipMemset(w.hist, 0, 128 * sizeof(int)));
+    HIPCHK(hipMemset(w.it, 0, n * sizeof(int)));  // the first step's sweep prediction
     // mpc_setup's sigma_min cache: GsocT*Gsoc for Csoc = [0 0 0 0 0 -Ts/(3600 Q)] (EKFmatsHandler.m:43-45)
     rc = launch_wide_smin(w, -rom->Ts / (3600 * rom->Q), rom->A, X->stream);
     if (rc) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "smin kernel: %s", hipGetErrorString((hipError_t)rc)); }
@@ -499,7 +499,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb,
-                  X->w.q, X->w.list};
+                  X->w.q, X->w.list, X->w.hist};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   if (X->stream) (void)hipStreamDestroy(X->stream);

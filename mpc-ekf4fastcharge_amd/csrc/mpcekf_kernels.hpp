@@ -120,9 +120,9 @@ struct KWide {
   double *X;       // [ncon][n][Nc]  X(:,i) = E\M(i,:)'
   double *K, *hii; // [ncon][n]
   int *it;         // [n] hildreth.m sweeps (nexec)
-  int *q;          // [2] work list: cells listed by k_hild_prep, next one k_hild_wide takes
-  int *list;       // [n] the cells whose QP runs on the fast path this step
-  int cus;         // compute units of the device (persistent grid size)
+  int *q;          // [1] fast-path cells this step (k_hild_sort)
+  int *list;       // [n] those cells, longest predicted sweep count first (k_hild_list)
+  int *hist;       // [2 * 64] k_hild_count's histogram of last step's counts | list offsets
   double *smin;    // [Nc*Nc + 1] GsocT*Gsoc of the configuration and its sigma_min
 };
 

@@ -23,6 +23,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+
+#ifndef MPCEKF_WIDE_JUNK
+#define MPCEKF_WIDE_JUNK 1
+#endif
+#ifndef MPCEKF_WIDE_SORT
+#define MPCEKF_WIDE_SORT 1
+#endif
 #include <cmath>
 #include <cstdint>
 
@@ -45,9 +52,23 @@ struct W {
   // never reaches a result: every sum they enter starts from +0).
   static constexpr int NX_ROWS = 2 * NC + 3 * NP;
   static constexpr int HPW = NC - 1 + NP;             // one Toeplitz block, NC - 1 leading zeros
-  static constexpr int CELL_LDS = 4 * NCON + 3 * HPW;  // k_hild_wide doubles per cell
+  // k_hild_wide doubles per cell, even: each group's (H_ii, 1/H_ii) pairs are read with
+  // ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
+  // (tools/micro/lds_micro.hip)
+  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1) & ~1;
+  static constexpr int ZERO_LDS = (NCON + 1) & ~1;    // the zero row ahead of the groups
   static constexpr int GROUPS = 16;                   // cells per 256-thread block
+  static constexpr int JUNK = 64 + NCON;              // per-wave sink of the lanes k != 0's lambda stores
 };
+
+// k_hild_sort's bins over last step's sweep count (0 .. maxIter)
+constexpr int SWEEP_BINS = 64;
+__device__ __forceinline__ int sweep_bin(int it, int maxIter) {
+  if (!MPCEKF_WIDE_SORT) return 0;
+  const int m = maxIter > 0 ? maxIter : 1;
+  const int t = it < 0 ? 0 : it > m ? m : it;
+  return (int)(((long long)t * SWEEP_BINS) / (m + 1));
+}
 
 // distinct-row slot of constraint row i, and whether row i is the negated copy
 template <int NP, int NC>
@@ -128,7 +149,6 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
   if (c >= n) return;
   const bool fused = io.mode & MODE_FUSED;
   s.hflag[c] = 0;
-  if (c == 0) { w.q[0] = 0; w.q[1] = 0; }  // k_hild_prep lists, k_hild_wide takes (this step's QPs)
   if (s.status[c] & ST_ERROR) {  // the fused step's iterEKF kernel already wrote NaN outputs
     if (!fused) {
       if (io.uk_out) io.uk_out[c] = __builtin_nan("");
@@ -356,7 +376,59 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
     if (i < NC || (i >= 2 * NC && i < 3 * NC)) w.hii[(size_t)c * NCON + i + NC] = h;
   }
   if (!fin) s.hflag[c] = 2;
-  else w.list[atomicAdd(&w.q[0], 1)] = (int)c;  // k_hild_wide's work list (any order: cells are independent)
+}
+
+// ---------------------------------------------------------------------------
+// k_hild_count / k_hild_sort / k_hild_list: the fast-path cells listed by predicted sweeps
+// ---------------------------------------------------------------------------
+// k_hild_wide runs 4 cells per wave and a wave lasts as long as its slowest cell; a
+// cell's count changes little from one control step to the next, so listing cells by
+// last step's count (longest first) puts cells of like length in one wave.  The order
+// only decides which group runs which cell: each cell's sweeps are the same operations
+// whichever group runs them, so the results are the bits of any other order.
+// ctr[bin] += (lanes of the wave with that bin); returns each active lane's slot (the
+// counter before the add plus its rank among those lanes).  One atomic per distinct bin
+// in the wave: per-cell atomics on a few hot bins serialised at the L2 (~0.5 ms a step).
+__device__ __forceinline__ int wave_bin_add(int *ctr, int bin, bool active) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt = (1ull << lane) - 1;
+  unsigned long long rem = __ballot(active);
+  int pos = -1;
+  while (rem) {
+    const int leader = __ffsll((long long)rem) - 1;
+    const int b = __shfl(bin, leader);
+    const unsigned long long m = __ballot(active && bin == b);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&ctr[b], __popcll(m));
+    base = __shfl(base, leader);
+    if (active && bin == b) pos = base + __popcll(m & lt);
+    rem &= ~m;
+  }
+  return pos;
+}
+
+__global__ void __launch_bounds__(64) k_hild_count(const KCfg cf, const KState s, const KWide w) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = c < s.n && s.hflag[c] == 1;
+  (void)wave_bin_add(w.hist, act ? sweep_bin(w.it[c], cf.max_hild) : 0, act);
+}
+
+__global__ void __launch_bounds__(64) k_hild_sort(const KWide w) {
+  if (threadIdx.x != 0) return;
+  int acc = 0;
+  for (int b = SWEEP_BINS - 1; b >= 0; --b) {  // descending: longest first
+    w.hist[SWEEP_BINS + b] = acc;
+    acc += w.hist[b];
+    w.hist[b] = 0;  // ready for the next step's k_hild_count
+  }
+  w.q[0] = acc;
+}
+
+__global__ void __launch_bounds__(64) k_hild_list(const KCfg cf, const KState s, const KWide w) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = c < s.n && s.hflag[c] == 1;
+  const int pos = wave_bin_add(w.hist + SWEEP_BINS, act ? sweep_bin(w.it[c], cf.max_hild) : 0, act);
+  if (act) w.list[pos] = (int)c;
 }
 
 // ---------------------------------------------------------------------------
@@ -412,40 +484,6 @@ __device__ __forceinline__ double row_m(int i, const double *mp) {
   return mp[blk * W<NP, NC>::HPW + r];
 }
 
-// Persistent: a grid of two blocks per CU (two waves per SIMD) takes the cells k_hild_prep
-// listed (w.list, w.q[0] of them) from a global counter (w.q[1]), a 16-lane group at a
-// time.  A group that converges, hits maxIter or leaves the fast form's domain returns
-// its cell and takes the next one at the following sweep start, so the waves work on live
-// cells only (a static cell-to-wave map kept every wave busy until its slowest cell,
-// mean 58 sweeps per wave against 40 per cell).  Each cell's sweeps are the same
-// operations in the same order whichever group runs them, so the results are the
-// order-independent bits of the static kernel.
-template <int NP, int NC>
-__device__ __forceinline__ bool hild_wide_load(const KState &s, const KWide &w, int64_t c, int k, double *lam,
-                                               double *Kl, double2 *hr, double *hp, double X[W<NP, NC>::NX_ROWS]) {
-  using T = W<NP, NC>;
-  constexpr int NCON = T::NCON, HPW = T::HPW;
-  const int64_t n = s.n;
-  bool ok = true;
-  for (int i = k; i < NCON; i += 16) {
-    const double li = s.lam[(size_t)i * n + c];
-    const double hii = w.hii[(size_t)c * NCON + i];
-    const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
-    const double ay = fabs(hii);
-    ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
-    lam[i] = li;
-    Kl[i] = w.K[(size_t)c * NCON + i];
-    hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
-  }
-  for (int j = k; j < 3 * HPW; j += 16) {
-    const int b = j / HPW, q = j % HPW;
-    hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
-  }
-#pragma unroll
-  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
-  return ok;
-}
-
 template <int NP, int NC>
 __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
   using T = W<NP, NC>;
@@ -453,108 +491,119 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
   extern __shared__ double lds[];
   double *zero = lds;  // NCON zeros: lanes that add no K_i / no M entry read these
   const int g = threadIdx.x >> 4, k = threadIdx.x & 15;
-  const int64_t n = s.n;
-  double *base = lds + NCON + g * T::CELL_LDS;
+  const int64_t n = s.n, slot = (int64_t)blockIdx.x * T::GROUPS + g;
+  static_assert(T::ZERO_LDS % 2 == 0 && T::CELL_LDS % 2 == 0, "16-byte aligned (H_ii, 1/H_ii) pairs");
+  double *base = lds + T::ZERO_LDS + g * T::CELL_LDS;
   double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
   double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
-  __syncthreads();
-  const int gshift = 16 * (g & 3);
-  const int ncells = w.q[0];
-  const double *kp = k == 0 ? Kl : zero;
-  const double *mp = k < NC ? hp + (NC - 1) - k : zero;
-  const double tol = cf.hild_tol;
-  const int maxIter = cf.max_hild;
-  double X[T::NX_ROWS];
-  int64_t c = -1;      // the group's cell (-1: none)
-  bool drained = false;  // the list is exhausted for this group
-  int it = 0;
-  for (;;) {
-    if (c < 0 && !drained) {  // take the next listed cell (group-uniform)
-      int idx = 0;
-      if (k == 0) idx = atomicAdd(&w.q[1], 1);
-      idx = __shfl(idx, 0, 16);
-      if (idx < ncells) {
-        const int64_t cn = w.list[idx];
-        const bool ok = hild_wide_load<NP, NC>(s, w, cn, k, lam, Kl, hr, hp, X);
-        if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
-          if (k == 0) s.hflag[cn] = 2;
-        } else {
-          c = cn;
-          it = 0;
-        }
-      } else {
-        drained = true;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const bool act = slot < w.q[0];            // k_hild_sort's count
+  const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_list's order
+  bool ok = true;
+  if (act) {
+    for (int i = k; i < NCON; i += 16) {
+      const double li = s.lam[(size_t)i * n + c];
+      const double hii = w.hii[(size_t)c * NCON + i];
+      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
+      const double ay = fabs(hii);
+      ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
+      lam[i] = li;
+      Kl[i] = w.K[(size_t)c * NCON + i];
+      hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
     }
-    if (!__any(c >= 0 || !drained)) break;  // every group of the wave is done
-    if (c >= 0) {
-      ++it;
-      // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
-      // of the loop they would need ~400 more registers
-      asm volatile("" ::: "memory");
-      double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
-#pragma unroll
-      for (int j = 0; j < NCON; ++j) {
-        if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
-        const double x = X[xslot<NP, NC>(j)];
-        v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
-      }
-      double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
-      // row i's LDS operands are read one row ahead (ds_read latency off the chain)
-      double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
-      double2 h = hr[0];
-#pragma unroll
-      for (int i = 0; i < NCON; ++i) {
-        asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
-        double kzn = kz, lin = li, mn = m;
-        double2 hn = h;
-        if (i + 1 < NCON) {
-          kzn = kp[i + 1];
-          lin = lam[i + 1];
-          hn = hr[i + 1];
-          mn = row_m<NP, NC>(i + 1, mp);
-        }
-        const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
-        // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
-        // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
-        // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
-        const double num = __builtin_fma(h.x, li, -t);
-        const double q0 = num * h.y;
-        const double e2 = __builtin_fma(-h.x, q0, num);
-        const double wf = __builtin_fma(e2, h.y, q0);
-        const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
-        const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
-        xmax = fmax(xmax, fabs(num));
-        xmin = fmin(xmin, fabs(num));
-        const double nl = wv > 0 ? wv : 0.0;
-        const double d = nl - li;
-        dmax = fmax(dmax, fabs(d));
-        lam[i] = nl;
-        const double x = X[xslot<NP, NC>(i)];
-        v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
-        kz = kzn;
-        li = lin;
-        h = hn;
-        m = mn;
-      }
-      // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
-      // the fast division's domain: the exact path redoes this cell from its warm start,
-      // still in s.lam (every sweep before was bit-identical to the exact form)
-      const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
-      if ((__ballot(bad) >> gshift) & 0xFFFFull) {
-        if (k == 0) s.hflag[c] = 2;
-        c = -1;
-      } else if (dmax < tol || it >= maxIter) {
-        for (int i = k; i < NCON; i += 16) s.lam[(size_t)i * n + c] = lam[i];
-        if (k == 0) w.it[c] = it;
-        c = -1;
-      }
+    for (int j = k; j < 3 * HPW; j += 16) {
+      const int b = j / HPW, q = j % HPW;
+      hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
     }
   }
+  __syncthreads();
+  if (!act) return;
+  const int gshift = 16 * (g & 3);
+  if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
+    if (k == 0) s.hflag[c] = 2;
+    return;
+  }
+  const double *kp = k == 0 ? Kl : zero;
+  const double *mp = k < NC ? hp + (NC - 1) - k : zero;
+  // lambda_i store: lane k = 0 writes lam[i]; the other lanes write their own slot of a
+  // per-wave sink (16 lanes storing one address serialise in one LDS bank, and the next
+  // rows' operand reads queue behind that store)
+  double *lst = lam;
+  if (MPCEKF_WIDE_JUNK && k != 0)
+    lst = lds + T::ZERO_LDS + T::GROUPS * T::CELL_LDS + (threadIdx.x >> 6) * T::JUNK + (threadIdx.x & 63);
+  double X[T::NX_ROWS];
+#pragma unroll
+  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
+  const double tol = cf.hild_tol;
+  const int maxIter = cf.max_hild;
+  int it;
+  bool slow = false;
+  for (it = 1; it <= maxIter; ++it) {
+    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
+    // of the loop they would need ~400 more registers
+    asm volatile("" ::: "memory");
+    double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
+#pragma unroll
+    for (int j = 0; j < NCON; ++j) {
+      if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
+      const double x = X[xslot<NP, NC>(j)];
+      v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
+    }
+    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+    // row i's LDS operands are read one row ahead (ds_read latency off the chain)
+    double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
+    double2 h = hr[0];
+#pragma unroll
+    for (int i = 0; i < NCON; ++i) {
+      asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
+      double kzn = kz, lin = li, mn = m;
+      double2 hn = h;
+      if (i + 1 < NCON) {
+        kzn = kp[i + 1];
+        lin = lam[i + 1];
+        hn = hr[i + 1];
+        mn = row_m<NP, NC>(i + 1, mp);
+      }
+      const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
+      // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
+      // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
+      // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
+      const double num = __builtin_fma(h.x, li, -t);
+      const double q0 = num * h.y;
+      const double e2 = __builtin_fma(-h.x, q0, num);
+      const double wf = __builtin_fma(e2, h.y, q0);
+      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
+      const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
+      xmax = fmax(xmax, fabs(num));
+      xmin = fmin(xmin, fabs(num));
+      const double nl = wv > 0 ? wv : 0.0;
+      const double d = nl - li;
+      dmax = fmax(dmax, fabs(d));
+      lst[i] = nl;
+      const double x = X[xslot<NP, NC>(i)];
+      v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
+      kz = kzn;
+      li = lin;
+      h = hn;
+      m = mn;
+    }
+    // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
+    // the fast division's domain: the exact path redoes this cell from its warm start,
+    // still in s.lam (every sweep before was bit-identical to the exact form)
+    const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
+    if ((__ballot(bad) >> gshift) & 0xFFFFull) {
+      slow = true;
+      break;
+    }
+    if (dmax < tol) break;
+  }
+  if (slow) {
+    if (k == 0) s.hflag[c] = 2;
+    return;
+  }
+  if (it > maxIter) it = maxIter;
+  for (int i = k; i < NCON; i += 16) s.lam[(size_t)i * n + c] = lam[i];
+  if (k == 0) w.it[c] = it;
 }
 
 // ---------------------------------------------------------------------------
@@ -864,7 +913,8 @@ int grid(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
 template <int NP, int NC>
 int hild_lds_bytes_w() {
-  return (W<NP, NC>::NCON + W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS) * (int)sizeof(double);
+  return (W<NP, NC>::ZERO_LDS + W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS + (MPCEKF_WIDE_JUNK ? 4 * W<NP, NC>::JUNK : 0)) *
+         (int)sizeof(double);
 }
 
 }  // namespace
@@ -905,9 +955,11 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
     attr = true;
   }
   hipLaunchKernelGGL((k_hild_prep<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, s, w);
-  // persistent: two 4-wave blocks per CU (the register file holds two waves per SIMD)
-  const int blocks = std::min(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS), 2 * std::max(w.cus, 1));
-  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(blocks), dim3(256), lds, st, c, s, w);
+  hipLaunchKernelGGL(k_hild_count, dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
+  hipLaunchKernelGGL(k_hild_sort, dim3(1), dim3(64), 0, st, w);
+  hipLaunchKernelGGL(k_hild_list, dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
+  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)), dim3(256), lds,
+                     st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
   hipLaunchKernelGGL((k_mpc_wide_finish<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, io, w);
   return (int)hipGetLastError();
