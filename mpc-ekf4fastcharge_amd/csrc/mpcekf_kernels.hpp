@@ -121,8 +121,8 @@ struct KWide {
   double *K, *hii; // [ncon][n]
   int *it;         // [n] hildreth.m sweeps (nexec)
   int *q;          // [1] fast-path cells this step (k_hild_sort)
-  int *list;       // [n] those cells, longest predicted sweep count first (k_hild_list)
-  int *hist;       // [2 * 64] k_hild_count's histogram of last step's counts | list offsets
+  int *list;       // [n] those cells, longest predicted sweep count first (k_hild_bin)
+  int *hist;       // [2 * 64] k_hild_bin's histogram of last step's counts | list offsets
   double *smin;    // [Nc*Nc + 1] GsocT*Gsoc of the configuration and its sigma_min
 };
 

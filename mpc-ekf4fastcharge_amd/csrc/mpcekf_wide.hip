@@ -55,7 +55,9 @@ struct W {
   // k_hild_wide doubles per cell, even: each group's (H_ii, 1/H_ii) pairs are read with
   // ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
   // (tools/micro/lds_micro.hip)
-  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1) & ~1;
+  // padded to 12 (mod 32) doubles: groups 0/1 (and 2/3) of a wave, which share a ds_read_b64
+  // lane half, then put their Nc M entries in disjoint banks
+  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1 - 12 + 31) / 32 * 32 + 12;
   static constexpr int ZERO_LDS = (NCON + 1) & ~1;    // the zero row ahead of the groups
   static constexpr int GROUPS = 16;                   // cells per 256-thread block
   static constexpr int JUNK = 64 + NCON;              // per-wave sink of the lanes k != 0's lambda stores
@@ -379,38 +381,43 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
 }
 
 // ---------------------------------------------------------------------------
-// k_hild_count / k_hild_sort / k_hild_list: the fast-path cells listed by predicted sweeps
+// k_hild_bin / k_hild_sort: the fast-path cells listed by predicted sweeps
 // ---------------------------------------------------------------------------
 // k_hild_wide runs 4 cells per wave and a wave lasts as long as its slowest cell; a
 // cell's count changes little from one control step to the next, so listing cells by
 // last step's count (longest first) puts cells of like length in one wave.  The order
 // only decides which group runs which cell: each cell's sweeps are the same operations
 // whichever group runs them, so the results are the bits of any other order.
-// ctr[bin] += (lanes of the wave with that bin); returns each active lane's slot (the
-// counter before the add plus its rank among those lanes).  One atomic per distinct bin
-// in the wave: per-cell atomics on a few hot bins serialised at the L2 (~0.5 ms a step).
-__device__ __forceinline__ int wave_bin_add(int *ctr, int bin, bool active) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1;
-  unsigned long long rem = __ballot(active);
-  int pos = -1;
-  while (rem) {
-    const int leader = __ffsll((long long)rem) - 1;
-    const int b = __shfl(bin, leader);
-    const unsigned long long m = __ballot(active && bin == b);
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&ctr[b], __popcll(m));
-    base = __shfl(base, leader);
-    if (active && bin == b) pos = base + __popcll(m & lt);
-    rem &= ~m;
+// A 1024-thread block takes LIST_CPB cells, bins them in LDS and adds its bin totals to
+// the global counters with one atomic per nonzero bin (per-cell global atomics on the
+// few hot bins serialised at the L2: ~0.5 ms a step).  LIST = false: the
+// histogram; LIST = true: the list, each cell's slot = its block's range in the bin
+// (reserved on the offsets k_hild_sort left) + its rank in the block.
+constexpr int LIST_CPB = 4096;
+template <bool LIST>
+__global__ void __launch_bounds__(1024) k_hild_bin(const KCfg cf, const KState s, const KWide w) {
+  __shared__ int lh[SWEEP_BINS], gb[SWEEP_BINS];
+  const int t = threadIdx.x;
+  if (t < SWEEP_BINS) lh[t] = 0;
+  __syncthreads();
+  constexpr int CPT = LIST_CPB / 1024;
+  int bin[CPT], rank[CPT];
+  const int64_t c0 = (int64_t)blockIdx.x * LIST_CPB + t;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int64_t c = c0 + j * 1024;
+    const bool act = c < s.n && s.hflag[c] == 1;
+    bin[j] = act ? sweep_bin(w.it[c], cf.max_hild) : -1;
+    rank[j] = act ? atomicAdd(&lh[bin[j]], 1) : 0;
   }
-  return pos;
-}
-
-__global__ void __launch_bounds__(64) k_hild_count(const KCfg cf, const KState s, const KWide w) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = c < s.n && s.hflag[c] == 1;
-  (void)wave_bin_add(w.hist, act ? sweep_bin(w.it[c], cf.max_hild) : 0, act);
+  __syncthreads();
+  int *ctr = LIST ? w.hist + SWEEP_BINS : w.hist;
+  if (t < SWEEP_BINS) gb[t] = lh[t] ? atomicAdd(&ctr[t], lh[t]) : 0;
+  if (!LIST) return;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < CPT; ++j)
+    if (bin[j] >= 0) w.list[gb[bin[j]] + rank[j]] = (int)(c0 + j * 1024);
 }
 
 __global__ void __launch_bounds__(64) k_hild_sort(const KWide w) {
@@ -419,17 +426,11 @@ __global__ void __launch_bounds__(64) k_hild_sort(const KWide w) {
   for (int b = SWEEP_BINS - 1; b >= 0; --b) {  // descending: longest first
     w.hist[SWEEP_BINS + b] = acc;
     acc += w.hist[b];
-    w.hist[b] = 0;  // ready for the next step's k_hild_count
+    w.hist[b] = 0;  // ready for the next step's k_hild_bin<false>
   }
   w.q[0] = acc;
 }
 
-__global__ void __launch_bounds__(64) k_hild_list(const KCfg cf, const KState s, const KWide w) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = c < s.n && s.hflag[c] == 1;
-  const int pos = wave_bin_add(w.hist + SWEEP_BINS, act ? sweep_bin(w.it[c], cf.max_hild) : 0, act);
-  if (act) w.list[pos] = (int)c;
-}
 
 // ---------------------------------------------------------------------------
 // k_hild_wide: hildreth.m:32-42 with a 16-lane group per cell
@@ -476,6 +477,45 @@ __device__ __forceinline__ double row_term(int i, int k, double v, double kz, do
   const int blk = (i - 4 * NC) / NP;
   return blk == 1 ? __builtin_fma(-m, v, kz) : __builtin_fma(m, v, kz);
 }
+// The I / -I rows (one M entry, +-1 in column j): the butterfly of hild_row_t adds K_i and
+// +-v_j to zeros only, which is exact, so t = K_i +- v_j in one rounding (the sign of a
+// zero t aside, which cannot reach lambda: num = fma(H_ii, lambda_i, -t) then has the
+// same magnitude and nl = max(w, +0)).  v_j comes from lane j of the DPP row by one
+// 64-bit row_newbcast move instead of the 4-level tree; kz holds K_i in every lane.
+template <int NC>
+__device__ __forceinline__ constexpr bool unit_row(int i) {
+  return i >= 2 * NC && i < 4 * NC;
+}
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xF, 0xF, false);  // row_newbcast:J
+}
+__device__ __forceinline__ double row_bcast(double v, int j) {  // j a constant after unrolling
+  switch (j) {
+    case 0: return row_bcast<0>(v);
+    case 1: return row_bcast<1>(v);
+    case 2: return row_bcast<2>(v);
+    case 3: return row_bcast<3>(v);
+    case 4: return row_bcast<4>(v);
+    case 5: return row_bcast<5>(v);
+    case 6: return row_bcast<6>(v);
+    case 7: return row_bcast<7>(v);
+    case 8: return row_bcast<8>(v);
+    case 9: return row_bcast<9>(v);
+    case 10: return row_bcast<10>(v);
+    case 11: return row_bcast<11>(v);
+    case 12: return row_bcast<12>(v);
+    case 13: return row_bcast<13>(v);
+    case 14: return row_bcast<14>(v);
+    default: return row_bcast<15>(v);
+  }
+}
+template <int NC>
+__device__ __forceinline__ double unit_t(int i, double v, double K) {
+  static_assert(NC <= 16, "one DPP row per cell");
+  const double vj = row_bcast(v, (i - 2 * NC) % NC);
+  return i < 3 * NC ? K + vj : K - vj;
+}
 // lane k's M entry of Toeplitz row i (0 for the constant rows, which row_term builds)
 template <int NP, int NC>
 __device__ __forceinline__ double row_m(int i, const double *mp) {
@@ -498,7 +538,7 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
   double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
   const bool act = slot < w.q[0];            // k_hild_sort's count
-  const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_list's order
+  const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_bin<true>'s order
   bool ok = true;
   if (act) {
     for (int i = k; i < NCON; i += 16) {
@@ -524,7 +564,9 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
     return;
   }
   const double *kp = k == 0 ? Kl : zero;
-  const double *mp = k < NC ? hp + (NC - 1) - k : zero;
+  // lanes >= Nc read lane Nc-1's entry (a broadcast, no bank of their own): their v_k
+  // is +0 for good (X there is 0 and lambda >= 0), so fma(+-m, +0, +0) = +0 as before
+  const double *mp = hp + (NC - 1) - (k < NC ? k : NC - 1);
   // lambda_i store: lane k = 0 writes lam[i]; the other lanes write their own slot of a
   // per-wave sink (16 lanes storing one address serialise in one LDS bank, and the next
   // rows' operand reads queue behind that store)
@@ -551,7 +593,7 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
     }
     double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
     // row i's LDS operands are read one row ahead (ds_read latency off the chain)
-    double kz = kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
+    double kz = unit_row<NC>(0) ? Kl[0] : kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
     double2 h = hr[0];
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
@@ -559,12 +601,12 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
       double kzn = kz, lin = li, mn = m;
       double2 hn = h;
       if (i + 1 < NCON) {
-        kzn = kp[i + 1];
+        kzn = unit_row<NC>(i + 1) ? Kl[i + 1] : kp[i + 1];
         lin = lam[i + 1];
         hn = hr[i + 1];
         mn = row_m<NP, NC>(i + 1, mp);
       }
-      const double t = tree16(row_term<NP, NC>(i, k, v, kz, m));
+      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v, kz) : tree16(row_term<NP, NC>(i, k, v, kz, m));
       // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
       // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
       // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
@@ -955,9 +997,9 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
     attr = true;
   }
   hipLaunchKernelGGL((k_hild_prep<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, s, w);
-  hipLaunchKernelGGL(k_hild_count, dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
+  hipLaunchKernelGGL(k_hild_bin<false>, dim3(grid(s.n, LIST_CPB)), dim3(1024), 0, st, c, s, w);
   hipLaunchKernelGGL(k_hild_sort, dim3(1), dim3(64), 0, st, w);
-  hipLaunchKernelGGL(k_hild_list, dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
+  hipLaunchKernelGGL(k_hild_bin<true>, dim3(grid(s.n, LIST_CPB)), dim3(1024), 0, st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)), dim3(256), lds,
                      st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
