@@ -174,6 +174,9 @@ int mpcekf_step(mpcekf_ctx *ctx, int32_t nsteps, const double *tc_degC, double *
  *   [nsteps][ncells]       u, v, soc, phise, nexec, J_unc, J_fin, norm_du, nviol
  *   [nsteps][ncells][6]    x    (x_store: the EKFmatsHandler xhat, integrator state last)
  *   [nsteps][ncells][nz+2] zk, zbk (zkEst / zkBound; zbk needs MPCEKF_CF_BOUNDS)
+ *   [nsteps][ncells][7][2] poles (mpcData.poles = eig(CL), iterMPC.m:53-59: re, im;
+ *                          sorted by descending real, then imaginary part)
+ *   [nsteps][ncells][7]    sv    (mpcData.sv = svd(CL), iterMPC.m:60, descending)
  * A cell in error has NaN floating outputs and zero nexec / nviol from its failing step on. */
 typedef struct {
   double *u, *v, *soc, *phise;     /* u_store, voltage_store, SOC_store, phise_store    */
@@ -182,6 +185,7 @@ typedef struct {
   double *zk, *zbk;                /* zkEst, zkBound                                    */
   double *J_unc, *J_fin, *norm_du; /* mpcData.cost.J_uncon / J_final / norm_DU          */
   int32_t *nviol;                  /* mpcData.cost.viol                                 */
+  double *poles, *sv;              /* mpcData.poles, mpcData.sv (stability diagnostics) */
 } mpcekf_traj;
 int mpcekf_step_ex(mpcekf_ctx *ctx, int32_t nsteps, const double *tc_degC, const mpcekf_traj *traj,
                    int32_t outputs_on_device);
@@ -189,6 +193,12 @@ int mpcekf_step_ex(mpcekf_ctx *ctx, int32_t nsteps, const double *tc_degC, const
 /* Optional per-step EKF output of the LAST mpcekf_step call: zk and boundzk
  * ([ncells][nz+2], boundzk only with MPCEKF_CF_BOUNDS). */
 int mpcekf_get_zk(mpcekf_ctx *ctx, double *zk, double *boundzk);
+
+/* eig / svd of one n x n (n <= 8) row-major matrix on the host, as the fused step
+ * computes mpcData.poles / mpcData.sv (iterMPC.m:57-60): re/im sorted by descending real
+ * then imaginary part, sv descending; any output may be NULL.  Returns MPCEKF_E_ARG for
+ * n outside 1..8; non-finite input gives NaN outputs. */
+int mpcekf_cl_eig(int32_t n, const double *a, double *re, double *im, double *sv);
 
 /* ---- stage entry points (one MATLAB function each; all batched over cells) ----
  * The temperature argument (Tc of OB_step.m:1, Tk of iterEKF.m:30 / EKFmatsHandler.m:1,

@@ -60,7 +60,8 @@ class Traj(C.Structure):
     """mpcekf_traj: per-step output pointers of mpcekf_step_ex (any may be NULL)."""
     _fields_ = [("u", C.c_void_p), ("v", C.c_void_p), ("soc", C.c_void_p), ("phise", C.c_void_p),
                 ("nexec", C.c_void_p), ("x", C.c_void_p), ("zk", C.c_void_p), ("zbk", C.c_void_p),
-                ("J_unc", C.c_void_p), ("J_fin", C.c_void_p), ("norm_du", C.c_void_p), ("nviol", C.c_void_p)]
+                ("J_unc", C.c_void_p), ("J_fin", C.c_void_p), ("norm_du", C.c_void_p), ("nviol", C.c_void_p),
+                ("poles", C.c_void_p), ("sv", C.c_void_p)]
 
 
 class MpcekfError(RuntimeError):
@@ -73,7 +74,7 @@ EXPORTS = [
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
-    "mpcekf_build_id",
+    "mpcekf_build_id", "mpcekf_cl_eig",
 ]
 
 _lib = None
@@ -115,6 +116,7 @@ def load():
     L.mpcekf_get_timing.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     L.mpcekf_get_hild_problems.argtypes = [vp, _dp, _ip]
     L.mpcekf_get_stamps.argtypes = [vp, C.POINTER(C.c_int64), _ip]
+    L.mpcekf_cl_eig.argtypes = [C.c_int32, _dp, _dp, _dp, _dp]
     L.mpcekf_hildreth_structured.argtypes = [C.c_int, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int32,
                                              C.c_double, _dp, _ip]
     for nm in EXPORTS:

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/mpcekf.h"
+#include "mpcekf_eig.hpp"
 #include "mpcekf_kernels.hpp"
 
 using namespace mk;
@@ -86,6 +87,7 @@ struct mpcekf_ctx {
   bool wide = false;
   KWide w{};
   double *d_lin = nullptr, *d_zsoc = nullptr;  // [n][35], [n]
+  double *d_uk1p = nullptr;                      // [n] uk_1 before the step (poles / sv)
   int flush_period = LAZY_H;      // steps between all-model flushes (<= LAZY_H)
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
@@ -99,6 +101,11 @@ struct mpcekf_ctx {
   // soc(z,T) ends and the table temperatures, for SOC0n/p at init (OB_step.m:63-65)
   std::vector<double> tabT, soc_end[2][2];
 
+  int diag_bufs() {  // the linearisation records and uk_1 copy of the poles / sv diagnostics
+    if (!d_lin) HIPCHK(hipMalloc((void **)&d_lin, (size_t)n * MPCEKF_LIN_SIZE * sizeof(double)));
+    if (!d_uk1p) HIPCHK(hipMalloc((void **)&d_uk1p, (size_t)n * sizeof(double)));
+    return MPCEKF_OK;
+  }
   int tmp(size_t bytes) {
     if (bytes <= tmp_bytes) return MPCEKF_OK;
     if (d_tmp) (void)hipFree(d_tmp);
@@ -498,7 +505,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
-                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb,
+                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
                   X->w.q, X->w.list, X->w.hist};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
@@ -619,7 +626,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   } f[] = {{tr->u, 8, 1, nullptr},       {tr->v, 8, 1, nullptr},      {tr->soc, 8, 1, nullptr},
            {tr->phise, 8, 1, nullptr},   {tr->nexec, 4, 1, nullptr},  {tr->x, 8, 6, nullptr},
            {tr->zk, 8, nzz, nullptr},    {tr->zbk, 8, nzz, nullptr},  {tr->J_unc, 8, 1, nullptr},
-           {tr->J_fin, 8, 1, nullptr},   {tr->norm_du, 8, 1, nullptr}, {tr->nviol, 4, 1, nullptr}};
+           {tr->J_fin, 8, 1, nullptr},   {tr->norm_du, 8, 1, nullptr}, {tr->nviol, 4, 1, nullptr},
+           {tr->poles, 8, 2 * NA, nullptr}, {tr->sv, 8, NA, nullptr}};
   constexpr int NF = sizeof(f) / sizeof(f[0]);
   const double *dtc = tc_degC;  // [nsteps][n] device copy of the per-step temperatures
   if (outputs_on_device) {
@@ -639,6 +647,10 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   auto row = [&](int i, int k) -> char * {  // step k's [ncells][width] block of field i
     return f[i].dev ? f[i].dev + (size_t)k * n * f[i].width * f[i].esz : nullptr;
   };
+  // iterMPC.m:53-60 diagnostics: k_cl_diag after the step from its linearisation records
+  // and the uk_1 the step's iterMPC used
+  const bool diag = f[12].dev || f[13].dev;
+  if (diag && (rc = X->diag_bufs())) return rc;
   constexpr int NEV = 6;  // events per step: plant | cell | bounds | hild | flush |
   if (X->timing && X->ev.size() < (size_t)nsteps * NEV) {
     size_t old = X->ev.size();
@@ -657,6 +669,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     const bool sample = X->timing && ((k + 1) % X->timing_every == 0 || k == nsteps - 1);
     hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
     if (E) HIPCHK(hipEventRecord(E[0], X->stream));
+    if (diag) HIPCHK(hipMemcpyAsync(X->d_uk1p, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
     if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
                    "plant")))
       return rc;
@@ -679,6 +692,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     io.jfin_out = (double *)row(9, k);
     io.normdu_out = (double *)row(10, k);
     io.nviol_out = (int *)row(11, k);
+    if (diag) io.lin_out = X->d_lin;
     KIO iow{};  // wide horizons: iterMPC in mpcekf_wide.hip from the linearisation record
     if (X->wide) {
       io.lin_out = X->d_lin;
@@ -724,6 +738,12 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     } else if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
       return rc;
     }
+    if (diag) {
+      double *pk = (double *)row(12, k), *sk = (double *)row(13, k);
+      rc = X->wide ? launch_cl_diag_wide(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream)
+                   : launch_cl_diag(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream);
+      if ((rc = lerr(rc, "cl_diag"))) return rc;
+    }
     if (E) HIPCHK(hipEventRecord(E[4], X->stream));
     if (t % X->flush_period == 0 || t == nsteps) {
       if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
@@ -752,6 +772,19 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         X->t_ms[slot[j]] += ms;
         X->t_n[slot[j]] += 1;
       }
+  }
+  return MPCEKF_OK;
+}
+
+int mpcekf_cl_eig(int32_t n, const double *a, double *re, double *im, double *sv) {
+  if (n < 1 || n > mk::eig::MAXN || !a) return fail(MPCEKF_E_ARG, "cl_eig: n must be 1..%d", mk::eig::MAXN);
+  double r[mk::eig::MAXN], m[mk::eig::MAXN], s[mk::eig::MAXN];
+  if (re || im) mk::eig::eigvals(n, a, r, m);
+  if (sv) mk::eig::singvals(n, a, s);
+  for (int i = 0; i < n; ++i) {
+    if (re) re[i] = r[i];
+    if (im) im[i] = m[i];
+    if (sv) sv[i] = s[i];
   }
   return MPCEKF_OK;
 }

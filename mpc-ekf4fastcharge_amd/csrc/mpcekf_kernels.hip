@@ -2989,6 +2989,14 @@ static int hild_lds_bytes() {  // 4 waves per block; one block per CU (147 KiB o
   return 4 * HILD_LDS_PER_WAVE;
 }
 
+int launch_cl_diag(const KCfg &c, int64_t n, const double *lin, const double *uk1, double *poles, double *sv,
+                   void *stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL((k_cl_diag<NP, NC>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, c, n, lin,
+                     uk1, poles, sv);
+  return (int)hipGetLastError();
+}
+
 int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
   if (s.n == 0) return 0;
   static bool attr = false;

@@ -163,6 +163,12 @@ int wide_prob_doubles(int Np, int Nc);
 int launch_wide_smin(const KWide &w, double rr, const double *a6, void *stream);
 // iterMPC setup from the linearisation records io.lin_in [n][35] and io.soc_k1_in [n]
 int launch_mpc_wide(const KCfg &c, const KState &s, const KIO &io, const KWide &w, void *stream);
+// iterMPC.m:53-60 poles / sv from this step's linearisation records and pre-step uk_1
+// (Np = 5 / Nc = 2 here, the wide horizons in mpcekf_wide.hip)
+int launch_cl_diag(const KCfg &c, int64_t n, const double *lin, const double *uk1, double *poles, double *sv,
+                   void *stream);
+int launch_cl_diag_wide(const KCfg &c, int64_t n, const double *lin, const double *uk1, double *poles, double *sv,
+                        void *stream);
 // hildreth.m (16-lane groups, exact lane-per-cell path for the rest) and iterMPC.m:75-95
 int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide &w, void *stream);
 // context-free predMat / constraintsMPC / hildreth at the wide horizons

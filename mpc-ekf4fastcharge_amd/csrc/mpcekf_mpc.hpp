@@ -10,6 +10,7 @@
 
 #include <cmath>
 
+#include "mpcekf_eig.hpp"
 #include "mpcekf_kernels.hpp"
 
 #pragma clang fp contract(off)
@@ -361,15 +362,15 @@ struct MpcSetupT {
 // smin_cache (optional): GsocT*Gsoc and its sigma_min for one Gsoc; when this cell's
 // GsocT*Gsoc is bitwise the cached one, the cached sigma_min is the value
 // sigma_min_n would return (same inputs, same code), so the Jacobi is skipped.
+// iterMPC.m:17-48 up to E: predictions, F, GsocT*Gsoc and its sigma_min, Ru, E
 template <int NP, int NC>
-__device__ __forceinline__ bool mpc_setup(const KCfg &cf, const Lin &L, double uk_1, double SOCk_1,
-                                          MpcSetupT<NP, NC> &P, MpcOut &o, const double *smin_cache = nullptr) {
-  constexpr int NCON = 4 * NC + 3 * NP;
-  double dx[NA];
+__device__ __forceinline__ void mpc_core(const KCfg &cf, const Lin &L, double uk_1, double (&dx)[NA],
+                                         double (&Phis)[NP][NA], double (&Hs)[NP], MpcSetupT<NP, NC> &P,
+                                         double (&GtG)[NC][NC], const double *smin_cache) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) dx[k] = L.xhat[k];
   dx[6] = uk_1;
-  double Phis[NP][NA], Hs[NP], Cb[7];
+  double Cb[7];
 #pragma unroll
   for (int k = 0; k < 6; ++k) Cb[k] = L.Csoc[k];
   Cb[6] = L.Dsoc;
@@ -388,7 +389,6 @@ __device__ __forceinline__ bool mpc_setup(const KCfg &cf, const Lin &L, double u
     for (int i = 0; i < NP; ++i) acc = acc + (-2 * (j <= i ? Hs[i - j] : 0.0)) * P.e[i];
     P.F[j] = acc;
   }
-  double GtG[NC][NC];
 #pragma unroll
   for (int a = 0; a < NC; ++a)
 #pragma unroll
@@ -415,14 +415,23 @@ __device__ __forceinline__ bool mpc_setup(const KCfg &cf, const Lin &L, double u
   for (int j = 0; j < NC; ++j) nF = nF + P.F[j] * P.F[j];
   nF = sqrt(nF);
   P.Ru = (nF / (2 * cf.du_max * sqrt((double)NC))) - smin;
+#pragma unroll
+  for (int a = 0; a < NC; ++a)
+#pragma unroll
+    for (int b = 0; b < NC; ++b) P.E[a][b] = 2 * (GtG[a][b] + P.Ru * (a == b ? 1.0 : 0.0));
+}
+
+template <int NP, int NC>
+__device__ __forceinline__ bool mpc_setup(const KCfg &cf, const Lin &L, double uk_1, double SOCk_1,
+                                          MpcSetupT<NP, NC> &P, MpcOut &o, const double *smin_cache = nullptr) {
+  constexpr int NCON = 4 * NC + 3 * NP;
+  double dx[NA], Phis[NP][NA], Hs[NP], GtG[NC][NC];
+  mpc_core<NP, NC>(cf, L, uk_1, dx, Phis, Hs, P, GtG, smin_cache);
   double mE[NC][NC];
 #pragma unroll
   for (int a = 0; a < NC; ++a)
 #pragma unroll
-    for (int b = 0; b < NC; ++b) {
-      P.E[a][b] = 2 * (GtG[a][b] + P.Ru * (a == b ? 1.0 : 0.0));
-      mE[a][b] = -P.E[a][b];
-    }
+    for (int b = 0; b < NC; ++b) mE[a][b] = -P.E[a][b];
   lu_solve_n<NC>(mE, P.F, P.DU);
   o.J_unc = mpc_cost<NP, NC>(Hs, P.e, P.Ru, P.DU);
   constraints_s<NP, NC>(cf, L, dx, uk_1, SOCk_1, Phis, Hs, P.Cn);
@@ -455,6 +464,72 @@ __device__ __forceinline__ void mpc_finish(const ConsT<NP, NC> &Cn, const double
   }
   o.nviol = nviol;
   o.J_fin = mpc_cost<NP, NC>(Cn.Hs, e, Ru, DU);
+}
+
+// ---------------------------------------------------------------------------
+// iterMPC.m:53-60 stability diagnostics: Kmpc = first row of E\(GsocT*Phisoc),
+// CL = Abar - Bbar*Kmpc, mpcData.poles = eig(CL), mpcData.sv = svd(CL)
+// ---------------------------------------------------------------------------
+// E is mpc_core's (the bits iterMPC solved with); GsocT*Phisoc sums from +0 in
+// ascending prediction row; E\ is MATLAB's SPD rule (Cholesky, else LU).
+template <int NP, int NC>
+__device__ __forceinline__ void mpc_kmpc(const KCfg &cf, const Lin &L, double uk_1, double (&Km)[NA]) {
+  MpcSetupT<NP, NC> P;
+  double dx[NA], Phis[NP][NA], Hs[NP], GtG[NC][NC];
+  mpc_core<NP, NC>(cf, L, uk_1, dx, Phis, Hs, P, GtG, nullptr);
+  double R[NC][NC];
+  const bool ok = chol_n<NC>(P.E, R);
+  for (int c = 0; c < NA; ++c) {
+    double b[NC], y[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) acc = acc + (j <= i ? Hs[i - j] : 0.0) * Phis[i][c];
+      b[j] = acc;
+    }
+    mldiv_spd<NC>(P.E, R, ok, b, y);
+    Km[c] = y[0];
+  }
+}
+
+// CL of predMat.m's augmentation with A = diag(a), B = ones: rows 0-5 [diag(a) 1],
+// row 6 [-Kmpc(1:6), 1 - Kmpc(7)]
+__host__ __device__ inline void closed_loop(const double a[6], const double Km[NA], double CL[NA * NA]) {
+  for (int i = 0; i < NA * NA; ++i) CL[i] = 0.0;
+  for (int i = 0; i < 6; ++i) {
+    CL[i * NA + i] = a[i];
+    CL[i * NA + 6] = 1.0;
+  }
+  for (int j = 0; j < 6; ++j) CL[6 * NA + j] = 0.0 - Km[j];
+  CL[6 * NA + 6] = 1.0 - Km[6];
+}
+
+// per cell: lin [n][35] (this step's EKFmatsHandler record), uk1 [n] (uk_1 before the
+// step's iterMPC); poles [n][7][2] (re, im), sv [n][7] (either may be null)
+template <int NP, int NC>
+__global__ void __launch_bounds__(64) k_cl_diag(const KCfg cf, int64_t n, const double *lin, const double *uk1,
+                                                double *poles, double *sv) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  Lin L;
+  lin_load(lin + c * 35, L);
+  double Km[NA], CL[NA * NA];
+  mpc_kmpc<NP, NC>(cf, L, uk1[c], Km);
+  closed_loop(L.a, Km, CL);
+  if (poles) {
+    double re[NA], im[NA];
+    eig::eigvals(NA, CL, re, im);
+    for (int i = 0; i < NA; ++i) {
+      poles[(c * NA + i) * 2] = re[i];
+      poles[(c * NA + i) * 2 + 1] = im[i];
+    }
+  }
+  if (sv) {
+    double s[NA];
+    eig::singvals(NA, CL, s);
+    for (int i = 0; i < NA; ++i) sv[c * NA + i] = s[i];
+  }
 }
 
 }  // namespace mk

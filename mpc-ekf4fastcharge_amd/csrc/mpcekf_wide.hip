@@ -516,6 +516,22 @@ __device__ __forceinline__ double unit_t(int i, double v, double K) {
   const double vj = row_bcast(v, (i - 2 * NC) % NC);
   return i < 3 * NC ? K + vj : K - vj;
 }
+// Rows whose nonzero terms sit in lanes 0 .. 2^L - 1 only (the first Cu / -Cu rows and
+// the first rows of each Toeplitz block, M(i, k) = 0 for k > r): after L levels lane 0
+// holds the block's sum and the remaining levels would add exact zeros, so it is
+// broadcast to the row instead (the sign of a zero t aside, as for unit_t).
+template <int NP, int NC>
+__device__ __forceinline__ constexpr int row_levels(int i) {
+  const int nz = i < NC ? i + 1 : i < 2 * NC ? i - NC + 1 : i < 4 * NC ? NC : ((i - 4 * NC) % NP + 1 < NC ? (i - 4 * NC) % NP + 1 : NC);
+  return nz <= 1 ? 0 : nz <= 2 ? 1 : nz <= 4 ? 2 : nz <= 8 ? 3 : 4;
+}
+__device__ __forceinline__ double tree_rows(int L, double a) {  // L a constant after unrolling
+  if (L >= 4) return tree16(a);
+  if (L >= 1) a = a + dpp64<0xB1>(a);
+  if (L >= 2) a = a + dpp64<0x4E>(a);
+  if (L >= 3) a = a + dpp64<0x141>(a);
+  return row_bcast<0>(a);
+}
 // lane k's M entry of Toeplitz row i (0 for the constant rows, which row_term builds)
 template <int NP, int NC>
 __device__ __forceinline__ double row_m(int i, const double *mp) {
@@ -606,7 +622,8 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
         hn = hr[i + 1];
         mn = row_m<NP, NC>(i + 1, mp);
       }
-      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v, kz) : tree16(row_term<NP, NC>(i, k, v, kz, m));
+      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v, kz)
+                                       : tree_rows(row_levels<NP, NC>(i), row_term<NP, NC>(i, k, v, kz, m));
       // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
       // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
       // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
@@ -1004,6 +1021,14 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
                      st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
   hipLaunchKernelGGL((k_mpc_wide_finish<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, io, w);
+  return (int)hipGetLastError();
+}
+
+int launch_cl_diag_wide(const KCfg &c, int64_t n, const double *lin, const double *uk1, double *poles, double *sv,
+                        void *stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL((k_cl_diag<WIDE_NP, WIDE_NC>), dim3(grid(n, 64)), dim3(64), 0, (hipStream_t)stream, c, n, lin, uk1,
+                     poles, sv);
   return (int)hipGetLastError();
 }
 

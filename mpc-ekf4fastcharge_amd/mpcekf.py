@@ -140,13 +140,16 @@ class Context:
     TRAJ_FIELDS = dict(u=(np.float64, ()), v=(np.float64, ()), soc=(np.float64, ()), phise=(np.float64, ()),
                        nexec=(np.int32, ()), x=(np.float64, (6,)), zk=(np.float64, None),
                        zbk=(np.float64, None), J_unc=(np.float64, ()), J_fin=(np.float64, ()),
-                       norm_du=(np.float64, ()), nviol=(np.int32, ()))
+                       norm_du=(np.float64, ()), nviol=(np.int32, ()), poles=(np.float64, (7, 2)),
+                       sv=(np.float64, (7,)))
 
     def step(self, nsteps, outputs=("u", "v", "soc", "phise", "nexec"), tc=None):
         """nsteps fused closed-loop steps (runMPC.m:83-112).  ``outputs`` names the per-step
         stores to return as [nsteps, ncells(, k)] arrays: u, v, soc, phise, nexec, and the
         diagnostics x (x_store), zk / zbk (zkEst / zkBound), J_unc, J_fin, norm_du, nviol
-        (mpcData.cost).  ``tc`` [nsteps, ncells] (or broadcastable): the TC of each step
+        (mpcData.cost), poles ([.., 7, 2] re/im of eig(CL)) and sv (svd(CL)), the stability
+        diagnostics of iterMPC.m:53-60 (returned as complex [nsteps, ncells, 7] for poles).
+        ``tc`` [nsteps, ncells] (or broadcastable): the TC of each step
         in degC (runMPC.m:85-92); None keeps every cell's current temperature."""
         n = self.n
         tcs = None
@@ -164,6 +167,8 @@ class Context:
             setattr(tr, k, out[k].ctypes.data_as(C.c_void_p).value)
         check(self.L.mpcekf_step_ex(self.h, int(nsteps), tcs.ctypes.data_as(C.c_void_p) if tcs is not None else None,
                                     C.byref(tr), 0))
+        if "poles" in out:
+            out["poles"] = out["poles"][..., 0] + 1j * out["poles"][..., 1]
         return out
 
     def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
@@ -366,3 +371,17 @@ def runMPC(rom, SOC0, TC, nsteps, cfg=None, device=0, ncells=None, tc_traj=None)
         out = ctx.step(nsteps, tc=tc_traj)
         out["status"] = ctx.get_state()["status"]
         return out
+
+
+def cl_eig(a):
+    """eig / svd of one small square matrix as the fused step computes mpcData.poles and
+    mpcData.sv (iterMPC.m:57-60; mpcekf_cl_eig): (poles complex [n] sorted by descending
+    real then imaginary part, sv [n] descending).  Host code, no device needed."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    n = a.shape[0]
+    if a.shape != (n, n):
+        raise ValueError("square matrix expected")
+    re, im, sv = np.empty(n), np.empty(n), np.empty(n)
+    L = _lib.load()
+    check(L.mpcekf_cl_eig(n, dptr(a), dptr(re), dptr(im), dptr(sv)))
+    return re + 1j * im, sv

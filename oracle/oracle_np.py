@@ -963,6 +963,18 @@ def iter_mpc(xk, MPC, mpc, smin=None):
     DU = lu_solve(-E, F)
     r = e - mv(G_soc, DU)
     J_unc = dot(r, r) + dot(mv(Ru * np.eye(Nc), DU), DU)
+    # iterMPC.m:53-60 stability analysis: Kmpc = first row of E\(G_soc'*Phi_soc),
+    # CL = Abar - Bbar*Kmpc (predMat.m's augmentation, A = diag(a), B = ones),
+    # poles = eig(CL), sv = svd(CL) (LAPACK through numpy, as MATLAB's eig/svd)
+    Kmpc = mldivide_spd(E, mm(G_soc.T, Phi_soc))[0]
+    na = len(MPC["a"]) + 1
+    CL = np.zeros((na, na))
+    CL[:na - 1, :na - 1] = np.diag(MPC["a"])
+    CL[:na - 1, na - 1] = 1.0
+    CL[na - 1, na - 1] = 1.0
+    CL[na - 1, :] -= Kmpc
+    poles = np.linalg.eigvals(CL)
+    sv = np.linalg.svd(CL, compute_uv=False)
     M, gamma = constraints_mpc(dx, MPC, mpc, Phi_soc, G_soc)
     viol = mv(M, DU) - gamma
     nexec = 0
@@ -976,7 +988,7 @@ def iter_mpc(xk, MPC, mpc, smin=None):
     r = e - mv(G_soc, DU)
     J_fin = dot(r, r) + dot(mv(Ru * np.eye(Nc), DU), DU)
     return uk, dict(nexec=nexec, nviol=nviol, J_unc=J_unc, J_fin=J_fin, DU=DU, M=M, gamma=gamma,
-                    E=E, F=F)
+                    E=E, F=F, Kmpc=Kmpc, CL=CL, poles=poles, sv=sv)
 
 
 # ---------------------------------------------------------------------------
@@ -1011,6 +1023,9 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
     out["zk"] = np.full((nsteps, nz + 2), NAN)
     out["zbk"] = np.full((nsteps, nz + 2), NAN)
     out["status"] = np.zeros(nsteps, dtype=np.int64)
+    out["poles"] = np.full((nsteps, 7), NAN + 0j)
+    out["sv"] = np.full((nsteps, 7), NAN)
+    out["CL"] = np.full((nsteps, 7, 7), NAN)
     for k in range(nsteps):
         if tc_traj is not None:
             TC = float(tc_traj[k])
@@ -1032,6 +1047,9 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
         out["zk"][k] = zk
         out["zbk"][k] = zbk
         out["status"][k] = ekf["status"]
+        out["poles"][k] = info["poles"]
+        out["sv"][k] = info["sv"]
+        out["CL"][k] = info["CL"]
     if record_state:
         out["ekf"] = ekf
         out["mpc"] = mpc
