@@ -224,7 +224,9 @@ int mpcekf_predmat(int device, int64_t n, int32_t Np, int32_t Nc, const double *
 int mpcekf_constraints(int device, const mpcekf_config *cfg, double Q, int64_t n, const double *lin,
                        const double *uk_1, const double *soc_k1, double *M, double *gamma);
 /* hildreth: E [n][Nc][Nc], F [n][Nc], M [n][ncon][Nc], gamma/lambda [n][ncon]; lambda is
- * the warm start in and the multipliers out; DU [n][Nc]; nexec [n]. */
+ * the warm start in and the multipliers out; DU [n][Nc]; nexec [n].  Any M with
+ * 1 <= Nc <= 10 and 1 <= ncon <= 100 (hildreth.m:1; Nc = 2 / ncon = 23 is the compiled
+ * fused-path form, other sizes a runtime-sized kernel with the same defined arithmetic). */
 int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const double *E, const double *F,
                     const double *M, const double *gamma, double *lambda, int32_t max_iter, double tol,
                     double *DU, int32_t *nexec);

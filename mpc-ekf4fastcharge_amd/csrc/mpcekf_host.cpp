@@ -1025,15 +1025,17 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
                     int32_t *nexec) {
   if (n < 0 || (n && (!E || !F || !M || !gamma || !lambda || !DU || !nexec)))
     return fail(MPCEKF_E_ARG, "hildreth: bad argument");
-  if (Nc != 2 || ncon != NCON_BUILT)
-    return fail(MPCEKF_E_UNSUPPORTED, "hildreth: built for Nc=2, %d constraints", NCON_BUILT);
+  if (Nc < 1 || Nc > 10 || ncon < 1 || ncon > 100)
+    return fail(MPCEKF_E_UNSUPPORTED, "hildreth: Nc must be 1..10 and the constraint count 1..100");
   if (max_iter < 1) return fail(MPCEKF_E_ARG, "hildreth: max_iter < 1");
   if (n == 0) return MPCEKF_OK;
   HIPCHK(hipSetDevice(device));
   DevScope d;
   HIPCHK(hipStreamCreateWithFlags(&d.st, hipStreamNonBlocking));
   size_t per = (size_t)(Nc * Nc + Nc + ncon * Nc + ncon + ncon + Nc);
-  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * per * 8 + (size_t)n * 4 + 1024));
+  const bool any = Nc != 2 || ncon != NCON_BUILT;
+  const size_t scr = any ? hildreth_any_scratch(n, Nc, ncon) : 0;
+  HIPCHK(hipMalloc((void **)&d.buf, (size_t)n * per * 8 + (size_t)n * 4 + scr * 8 + 1024));
   double *dE = (double *)d.buf, *dF = dE + n * Nc * Nc, *dM = dF + n * Nc, *dg = dM + n * ncon * Nc,
          *dl = dg + n * ncon, *dD = dl + n * ncon;
   int *dn = (int *)(dD + n * Nc);
@@ -1042,7 +1044,8 @@ int mpcekf_hildreth(int device, int64_t n, int32_t Nc, int32_t ncon, const doubl
   HIPCHK(hipMemcpyAsync(dM, M, n * ncon * Nc * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(dg, gamma, n * ncon * 8, hipMemcpyHostToDevice, d.st));
   HIPCHK(hipMemcpyAsync(dl, lambda, n * ncon * 8, hipMemcpyHostToDevice, d.st));
-  int rc = lerr(launch_hildreth(n, Nc, ncon, dE, dF, dM, dg, dl, max_iter, tol, dD, dn, d.st), "hildreth");
+  double *dscr = any ? (double *)(((uintptr_t)(dn + n) + 255) & ~(uintptr_t)255) : nullptr;
+  int rc = lerr(launch_hildreth(n, Nc, ncon, dE, dF, dM, dg, dl, max_iter, tol, dD, dn, d.st, dscr), "hildreth");
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(lambda, dl, n * ncon * 8, hipMemcpyDeviceToHost, d.st));
   HIPCHK(hipMemcpyAsync(DU, dD, n * Nc * 8, hipMemcpyDeviceToHost, d.st));

@@ -2752,6 +2752,164 @@ __global__ void __launch_bounds__(64) k_hildreth(int64_t n, const double *Ei, co
   nexec[c] = it;
 }
 
+// hildreth.m for any Nc <= HANY_NC and nC <= HANY_NCON with a dense M (mpcekf_hildreth at
+// sizes other than the fused Np = 5 / Nc = 2): orc_hildreth's defined evaluation with
+// runtime sizes, lane per problem.  X = E\M' (Cholesky, else LU), H_ii and K live in a
+// per-problem scratch slab; the dense path re-forms H(i,j) entry by entry.  A stage entry
+// point, not the fused path: sized for correctness, not speed.
+constexpr int HANY_NC = 10, HANY_NCON = 100;
+__device__ inline bool chol_rt(int n, const double *E, double *R) {
+  bool ok = true;
+  for (int j = 0; j < n; ++j) {
+    double s = E[j * n + j];
+    for (int k = 0; k < j; ++k) s = s - R[k * n + j] * R[k * n + j];
+    if (!(s > 0)) ok = false;
+    R[j * n + j] = sqrt(s);
+    for (int i = j + 1; i < n; ++i) {
+      double t = E[j * n + i];
+      for (int k = 0; k < j; ++k) t = t - R[k * n + j] * R[k * n + i];
+      R[j * n + i] = t / R[j * n + j];
+    }
+  }
+  return ok;
+}
+__device__ inline void lu_rt(int n, const double *Ain, const double *b, double *x) {
+  double A[HANY_NC * HANY_NC], y[HANY_NC];
+  for (int i = 0; i < n * n; ++i) A[i] = Ain[i];
+  for (int i = 0; i < n; ++i) y[i] = b[i];
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    for (int i = k + 1; i < n; ++i)
+      if (fabs(A[i * n + k]) > fabs(A[p * n + k])) p = i;
+    if (p != k) {
+      for (int j = 0; j < n; ++j) { const double t = A[k * n + j]; A[k * n + j] = A[p * n + j]; A[p * n + j] = t; }
+      const double t = y[k]; y[k] = y[p]; y[p] = t;
+    }
+    for (int i = k + 1; i < n; ++i) {
+      const double l = A[i * n + k] / A[k * n + k];
+      A[i * n + k] = l;
+      for (int j = k + 1; j < n; ++j) A[i * n + j] = A[i * n + j] - l * A[k * n + j];
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    for (int k = 0; k < i; ++k) y[i] = y[i] - A[i * n + k] * y[k];
+  for (int i = n - 1; i >= 0; --i) {
+    double t = y[i];
+    for (int k = i + 1; k < n; ++k) t = t - A[i * n + k] * x[k];
+    x[i] = t / A[i * n + i];
+  }
+}
+// MATLAB E\b for symmetric E: Cholesky when every pivot is positive, else LU
+__device__ inline void mldiv_rt(int n, const double *E, const double *R, bool ok, const double *b, double *x) {
+  if (!ok) {
+    lu_rt(n, E, b, x);
+    return;
+  }
+  double y[HANY_NC];
+  for (int i = 0; i < n; ++i) {
+    double t = b[i];
+    for (int k = 0; k < i; ++k) t = t - R[k * n + i] * y[k];
+    y[i] = t / R[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double t = y[i];
+    for (int k = i + 1; k < n; ++k) t = t - R[i * n + k] * x[k];
+    x[i] = t / R[i * n + i];
+  }
+}
+// t_i = K_i + M(i,:)*v (orc hild_row_t): Nc <= 2 fma in ascending k; else the pairwise
+// tree over 16 slots, a_0 = fma(M_i0, v_0, K_i), a_k = M_ik v_k, +0 past Nc
+__device__ inline double row_t_rt(int Nc, const double *Mi, const double *v, double Ki) {
+  if (Nc <= 2) {
+    double t = Ki;
+    for (int k = 0; k < Nc; ++k) t = __builtin_fma(Mi[k], v[k], t);
+    return t;
+  }
+  double a[16];
+  a[0] = __builtin_fma(Mi[0], v[0], Ki);
+  for (int k = 1; k < 16; ++k) a[k] = k < Nc ? Mi[k] * v[k] : 0.0;
+  for (int w = 1; w < 16; w *= 2)
+    for (int k = 0; k < 16; k += 2 * w) a[k] = a[k] + a[k + w];
+  return a[0];
+}
+__global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, const double *Ei, const double *Fi,
+                                                     const double *Mi, const double *gi, double *lami, int maxIter,
+                                                     double tol, double *DUo, int *nexec, double *scr) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const double *E = Ei + (size_t)c * Nc * Nc, *F = Fi + (size_t)c * Nc, *M = Mi + (size_t)c * nC * Nc,
+               *gam = gi + (size_t)c * nC;
+  double *lam = lami + (size_t)c * nC;
+  double *X = scr + (size_t)c * (nC * Nc + 2 * nC), *Hd = X + nC * Nc, *K = Hd + nC;
+  double R[HANY_NC * HANY_NC], y[HANY_NC], v[HANY_NC];
+  const bool ok = chol_rt(Nc, E, R);
+  for (int i = 0; i < nC; ++i) mldiv_rt(Nc, E, R, ok, M + i * Nc, X + i * Nc);  // X(:,i) = E\M(i,:)'
+  mldiv_rt(Nc, E, R, ok, F, y);
+  bool fin = true;
+  for (int i = 0; i < nC; ++i) {
+    double s = 0.0, h = 0.0;
+    for (int k = 0; k < Nc; ++k) {
+      s = s + M[i * Nc + k] * y[k];
+      h = h + M[i * Nc + k] * X[i * Nc + k];
+      fin = fin && isfinite(X[i * Nc + k]) && isfinite(M[i * Nc + k]);
+    }
+    K[i] = s + gam[i];
+    Hd[i] = h;
+  }
+  auto xv = [&]() {
+    for (int k = 0; k < Nc; ++k) {
+      double a = 0.0;
+      for (int j = 0; j < nC; ++j) a = __builtin_fma(X[j * Nc + k], lam[j], a);
+      v[k] = a;
+    }
+  };
+  int it;
+  for (it = 1; it <= maxIter; ++it) {
+    bool conv = true;
+    if (fin) xv();
+    for (int i = 0; i < nC; ++i) {
+      const double hii = Hd[i];
+      double w;
+      if (fin) {
+        const double t = row_t_rt(Nc, M + i * Nc, v, K[i]);
+        w = __builtin_fma(hii, lam[i], -t) / hii;
+      } else {
+        double p4[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j = 0; j < nC; ++j) {
+          double h = 0.0;
+          for (int k = 0; k < Nc; ++k) h = h + M[i * Nc + k] * X[j * Nc + k];
+          p4[j & 3] = p4[j & 3] + h * lam[j];
+        }
+        const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+        w = -((K[i] + s) - hii * lam[i]) / hii;
+      }
+      const double nl = w > 0 ? w : 0.0;
+      const double d = nl - lam[i];
+      if (!(fabs(d) < tol)) conv = false;
+      lam[i] = nl;
+      if (fin) {
+        if (isfinite(d)) {
+          for (int k = 0; k < Nc; ++k) v[k] = __builtin_fma(X[i * Nc + k], d, v[k]);
+        } else {
+          xv();
+        }
+      }
+    }
+    if (conv) break;
+  }
+  if (it > maxIter) it = maxIter;
+  double rhs[HANY_NC], mE[HANY_NC * HANY_NC], DU[HANY_NC];
+  for (int k = 0; k < Nc; ++k) {
+    double s = 0.0;
+    for (int i = 0; i < nC; ++i) s = s + M[i * Nc + k] * lam[i];
+    rhs[k] = F[k] + s;
+  }
+  for (int i = 0; i < Nc * Nc; ++i) mE[i] = -E[i];
+  lu_rt(Nc, mE, rhs, DU);
+  for (int k = 0; k < Nc; ++k) DUo[(size_t)c * Nc + k] = DU[k];
+  nexec[c] = it;
+}
+
 // The fused solver (hild_fast + hild_slow, as k_hild + k_hild_slow) on constraintsMPC.m-structured
 // problems given by their Toeplitz rows: M = [Cu; -Cu; I; -I; G_v; -G_e; G_soc].
 template <bool SLOW>
@@ -2989,6 +3147,8 @@ static int hild_lds_bytes() {  // 4 waves per block; one block per CU (147 KiB o
   return 4 * HILD_LDS_PER_WAVE;
 }
 
+size_t hildreth_any_scratch(int64_t n, int Nc, int ncon) { return (size_t)n * (size_t)(ncon * Nc + 2 * ncon); }
+
 int launch_cl_diag(const KCfg &c, int64_t n, const double *lin, const double *uk1, double *poles, double *sv,
                    void *stream) {
   if (n == 0) return 0;
@@ -3028,9 +3188,14 @@ int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double
 
 int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *F, const double *M,
                     const double *gam, double *lam, int max_iter, double tol, double *DU, int *nexec,
-                    void *stream) {
-  if (Nc != NC || ncon != NCON) return -1;
+                    void *stream, double *scratch) {
   if (n == 0) return 0;
+  if (Nc != NC || ncon != NCON) {  // any other size: the runtime-sized form (scratch: hildreth_any_scratch)
+    if (Nc < 1 || Nc > HANY_NC || ncon < 1 || ncon > HANY_NCON || !scratch) return -1;
+    hipLaunchKernelGGL(k_hildreth_any, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, Nc, ncon, E, F, M,
+                       gam, lam, max_iter, tol, DU, nexec, scratch);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(k_hildreth, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, n, E, F, M, gam, lam,
                      max_iter, tol, DU, nexec);
   return (int)hipGetLastError();

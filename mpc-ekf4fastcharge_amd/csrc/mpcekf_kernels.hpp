@@ -147,9 +147,12 @@ int launch_predmat(int64_t n, int Np, int Nc, const double *a, const double *C, 
                    double *G, void *stream);
 int launch_constraints(const KCfg &c, int64_t n, const double *lin, const double *uk_1, const double *soc_k1,
                        double *M, double *gam, void *stream);
+// (Nc, ncon) = (2, 23): the compiled form; any other Nc <= 10, ncon <= 100: the runtime-sized
+// form, which needs hildreth_any_scratch(n, Nc, ncon) doubles of device scratch
 int launch_hildreth(int64_t n, int Nc, int ncon, const double *E, const double *F, const double *M,
                     const double *gam, double *lam, int max_iter, double tol, double *DU, int *nexec,
-                    void *stream);
+                    void *stream, double *scratch);
+size_t hildreth_any_scratch(int64_t n, int Nc, int ncon);
 int launch_hildreth_structured(int64_t n, const double *E, const double *F, const double *Hv, const double *He,
                                const double *Hs, const double *gam, double *lam, int max_iter, double tol,
                                double *DU, int *nexec, void *stream);

@@ -436,3 +436,38 @@ def test_lane_quad_ekf_kernel_is_exact(rom, M):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     for k in ("ekf", "bigX", "scal", "lam"):
         np.testing.assert_array_equal(a["state"][k], b["state"][k], err_msg=k)
+
+
+@pytest.mark.parametrize("Nc,ncon,n", [(10, 100, 96), (3, 17, 64), (1, 9, 64), (2, 40, 64), (7, 61, 48)])
+def test_generic_hildreth_any_size_matches_oracle(oc, M, Nc, ncon, n):
+    """mpcekf_hildreth (any M) at sizes other than the fused 2 x 23 form, bitwise against
+    orc_hildreth: random SPD and non-SPD (LU) E, warm starts, a non-finite M row (the
+    dense path) and, at 10 x 100, the constraintsMPC.m shape of configs[4]."""
+    rng = np.random.default_rng(100 + Nc * 7 + ncon)
+    E = np.empty((n, Nc, Nc))
+    for i in range(n):
+        A = rng.normal(0, 1, (Nc, Nc))
+        E[i] = A @ A.T + 0.3 * np.eye(Nc)
+        if i % 11 == 5:  # symmetric, not positive definite: MATLAB's \\ falls back to LU
+            E[i] -= (np.linalg.eigvalsh(E[i]).max() * 0.6) * np.eye(Nc)
+        E[i] = (E[i] + E[i].T) / 2
+    F = rng.normal(0, 1, (n, Nc))
+    Mm = rng.normal(0, 1, (n, ncon, Nc))
+    if (Nc, ncon) == (10, 100):
+        for i in range(0, n, 2):  # [Cu; -Cu; I; -I; G_v; -G_e; G_soc] with Toeplitz blocks
+            cu = np.tril(np.ones((Nc, Nc)))
+            blocks = []
+            for sgn in (1, -1, 1):
+                h = rng.normal(0, 1e-2, 20)
+                blocks.append(sgn * np.array([[h[r - k] if k <= r else 0.0 for k in range(Nc)] for r in range(20)]))
+            Mm[i] = np.vstack([cu, -cu, np.eye(Nc), -np.eye(Nc)] + blocks)
+    Mm[3, 1, 0] = np.inf  # the dense path (non-finite M)
+    g = rng.normal(0.2, 1, (n, ncon))
+    lam0 = np.abs(rng.normal(0, 0.05, (n, ncon)))
+    DU, lam, ne = M.hildreth(E, F, Mm, g, lam0, 100)
+    for i in range(n):
+        d2, l2, k2 = oc.hildreth(E[i], F[i], Mm[i], g[i], lam0[i], 100)
+        assert ne[i] == k2, i
+        _bitwise(DU[i], d2, f"DU[{i}]")
+        _bitwise(lam[i], l2, f"lambda[{i}]")
+    assert (ne == 100).any() and (ne < 100).any()
