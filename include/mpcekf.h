@@ -215,6 +215,12 @@ int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_mode
 /* iterMPC (uses and updates the context's uk_1 and lambda warm start):
  * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec. */
 int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
+/* iterMPC.m:53-60 stability analysis of the iterMPC that mpcekf_mpc_step would run on lin:
+ * Kmpc = first row of E\(G_soc'*Phi_soc), CL = Abar - Bbar*Kmpc; poles [ncells][7][2]
+ * (eig(CL): re, im, sorted as in mpcekf_traj), sv [ncells][7] (svd(CL)).  uk_1 [ncells]
+ * (mpcData.uk_1) or NULL for the context's current one (call before mpcekf_mpc_step).
+ * Reads nothing else of the context's state and changes none of it. */
+int mpcekf_mpc_diag(mpcekf_ctx *ctx, const double *lin, const double *uk_1, double *poles, double *sv);
 
 /* Context-free batched kernels (device chosen by `device`).
  * predMat with A = diag(a), B = ones: a,C [n][6], D [n] -> Phi [n][Np][7], G [n][Np][Nc]. */

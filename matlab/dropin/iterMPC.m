@@ -6,6 +6,8 @@ function [uk, mpcData] = iterMPC(xk, cellState, mpcData)
   S = mpcekf_session('get');
   lin = cellState.MPC.lin;
   n = size(lin, 2);
+  % iterMPC.m:53-60 stability analysis (before the solve: it uses this step's uk_1)
+  [mpcData.poles, mpcData.sv] = mpcekf_mex('mpcdiag', S.h, lin, []);
   [uk, nexec] = mpcekf_mex('mpc', S.h, lin, reshape(mpcData.SOCk_1 .* ones(1, n), 1, n));
   mpcData.uk_1 = uk;
   if isfield(mpcData, 'cost') && isfield(mpcData, 'k')

@@ -17,6 +17,8 @@
  *   [zk,zbk,xm,xg]    = mpcekf_mex('ekf', h, vk, ik, tk)               mpcekf_ekf_step     (iterEKF.m:30)
  *   lin               = mpcekf_mex('linearize', h, zk, xm, xg, tk)     mpcekf_linearize    (EKFmatsHandler.m:1)
  *   [uk,nexec]        = mpcekf_mex('mpc', h, lin, soc_k1)              mpcekf_mpc_step     (iterMPC.m:1)
+ *   [poles,sv]        = mpcekf_mex('mpcdiag', h, lin, uk_1)            mpcekf_mpc_diag     (iterMPC.m:53-60)
+ *                       uk_1: [] for the context's; poles complex 7 x ncells, sv 7 x ncells
  *   [DU,lambda,nexec] = mpcekf_mex('hildreth', E, F, M, gamma, lambda0, maxIter)   (hildreth.m:1)
  *   [Phi,G]           = mpcekf_mex('predmat', a, C, D, Np, Nc)         (predMat.m:1, A = diag(a), B = 1)
  *   st                = mpcekf_mex('get_state', h)    /  mpcekf_mex('set_state', h, st)
@@ -242,10 +244,16 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     plhs[1] = imat(1, nc);
     chk(mpcekf_mpc_step(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
                         mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1])));
+  } else if (!strcmp(cmd, "mpcdiag")) {
+    plhs[0] = mxCreateDoubleMatrix(7, (mwSize)nc, mxCOMPLEX);  /* interleaved (re, im): [ncells][7][2] */
+    plhs[1] = dmat(7, nc);
+    chk(mpcekf_mpc_diag(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), nrhs > 3 ? opt_vec(prhs[3], nc, "uk_1") : NULL,
+                        (double *)mxGetComplexDoubles(plhs[0]), mxGetDoubles(plhs[1])));
   } else if (!strcmp(cmd, "get_state") || !strcmp(cmd, "set_state")) {
     const char *f[] = {"bigX", "ekf", "scal", "lambda", "warn", "status"};
     const size_t rows[] = {(size_t)NM * 6, (size_t)NM * 20, MPCEKF_NSCAL, (size_t)ncon, 1, 1};
     mpcekf_state st;
+    memset(&st, 0, sizeof st); /* mb (the MB EKF state) is not exchanged here: NULL */
     if (cmd[0] == 'g') {
       plhs[0] = mxCreateStructMatrix(1, 1, 6, f);
       mxArray *a[6];

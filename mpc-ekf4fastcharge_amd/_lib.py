@@ -74,7 +74,7 @@ EXPORTS = [
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
-    "mpcekf_build_id", "mpcekf_cl_eig",
+    "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag",
 ]
 
 _lib = None
@@ -117,6 +117,7 @@ def load():
     L.mpcekf_get_hild_problems.argtypes = [vp, _dp, _ip]
     L.mpcekf_get_stamps.argtypes = [vp, C.POINTER(C.c_int64), _ip]
     L.mpcekf_cl_eig.argtypes = [C.c_int32, _dp, _dp, _dp, _dp]
+    L.mpcekf_mpc_diag.argtypes = [vp, _dp, _dp, _dp, _dp]
     L.mpcekf_hildreth_structured.argtypes = [C.c_int, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int32,
                                              C.c_double, _dp, _ip]
     for nm in EXPORTS:

@@ -953,6 +953,28 @@ int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, doub
   return MPCEKF_OK;
 }
 
+int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!lin) return fail(MPCEKF_E_ARG, "mpc_diag: null lin");
+  if (!poles && !sv) return MPCEKF_OK;
+  size_t n = (size_t)X->n;
+  if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + n + n * 3 * NA) * 8 + 2048))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *du = sl.take<double>(n), *dp = sl.take<double>(n * 2 * NA),
+         *ds = sl.take<double>(n * NA);
+  HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  if (uk_1) HIPCHK(hipMemcpyAsync(du, uk_1, n * 8, hipMemcpyHostToDevice, X->stream));
+  else HIPCHK(hipMemcpyAsync(du, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
+  rc = X->wide ? launch_cl_diag_wide(X->k, X->n, dl, du, poles ? dp : nullptr, sv ? ds : nullptr, X->stream)
+               : launch_cl_diag(X->k, X->n, dl, du, poles ? dp : nullptr, sv ? ds : nullptr, X->stream);
+  if ((rc = lerr(rc, "cl_diag"))) return rc;
+  if (poles) HIPCHK(hipMemcpyAsync(poles, dp, n * 2 * NA * 8, hipMemcpyDeviceToHost, X->stream));
+  if (sv) HIPCHK(hipMemcpyAsync(sv, ds, n * NA * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  return MPCEKF_OK;
+}
+
 // ---- context-free kernels ----------------------------------------------------
 }  // extern "C"
 namespace {

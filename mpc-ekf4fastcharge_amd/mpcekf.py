@@ -260,6 +260,16 @@ class Context:
         check(self.L.mpcekf_mpc_step(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne)))
         return uk, ne
 
+    def mpc_diag(self, lin, uk_1=None):
+        """mpcData.poles / mpcData.sv of the iterMPC that iterMPC(lin, ..) would run
+        (iterMPC.m:53-60): (poles complex [n, 7], sv [n, 7]).  uk_1 None: the context's."""
+        lin = np.ascontiguousarray(lin, dtype=np.float64)
+        u = None if uk_1 is None else self._vec(uk_1)
+        p = np.empty((self.n, 7, 2))
+        sv = np.empty((self.n, 7))
+        check(self.L.mpcekf_mpc_diag(self.h, dptr(lin), dptr(u), dptr(p), dptr(sv)))
+        return p[..., 0] + 1j * p[..., 1], sv
+
     # -- state -----------------------------------------------------------
     def get_state(self):
         n, NM = self.n, self.NM

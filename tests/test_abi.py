@@ -94,7 +94,7 @@ def test_mex_gateway_calls_only_declared_entry_points():
     assert called <= set(declared_symbols()), called - set(declared_symbols())
     for sym in ("mpcekf_ctx_create", "mpcekf_init_cells", "mpcekf_step", "mpcekf_plant_step", "mpcekf_ekf_step",
                 "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_hildreth", "mpcekf_predmat", "mpcekf_get_state",
-                "mpcekf_set_state", "mpcekf_ctx_destroy"):
+                "mpcekf_set_state", "mpcekf_ctx_destroy", "mpcekf_mpc_diag"):
         assert sym in called, sym
     drop = " ".join(open(os.path.join(ROOT, "matlab", "dropin", f)).read()
                     for f in os.listdir(os.path.join(ROOT, "matlab", "dropin")))

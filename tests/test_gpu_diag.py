@@ -68,3 +68,24 @@ def test_poles_sv_match_numpy_oracle(rom, M, onp, Np, Nc, n, steps):
     for c in range(min(n, 3)):
         ref = onp.run_cell(rom, soc0[c], tc[c], steps, cfg=dict(Np=Np, Nc=Nc))
         _compare(out, ref, c, steps)
+
+
+def test_mpc_diag_stage_entry_matches_fused(rom, M):
+    """mpcekf_mpc_diag on the stage path (linearize -> mpc_diag -> mpc_step) gives the
+    fused step's poles/sv bit for bit (same lin, same pre-step uk_1)."""
+    n, steps = 8, 6
+    soc0, tc = batch_inputs(n, seed=9)
+    with M.Context(rom, n) as a:
+        a.init_cells(soc0, tc)
+        ref = a.step(steps, outputs=("u", "poles", "sv"))
+    with M.Context(rom, n) as b:
+        b.init_cells(soc0, tc)
+        uk = np.zeros(n)
+        for k in range(steps):
+            v = b.OB_step(uk)
+            zk, zb, xind = b.iterEKF(v, uk)
+            lin = b.EKFmatsHandler(zk, xind)
+            p, sv = b.mpc_diag(lin)
+            assert np.array_equal(p, ref["poles"][k]) and np.array_equal(sv, ref["sv"][k]), k
+            uk, _ = b.iterMPC(lin, zk[:, -1])
+            assert np.array_equal(uk, ref["u"][k]), k
