@@ -262,6 +262,13 @@ int mpcekf_hildreth_structured(int device, int64_t n, const double *E, const dou
 #define MPCEKF_K_BOUNDS 4
 #define MPCEKF_NKERNELS 5
 int mpcekf_set_timing(mpcekf_ctx *ctx, int32_t enable);
+/* Graph replay of the fused call (runMPC.m:83-112's loop as a device graph, SURVEY.md
+ * §8(f) row 2): with enable != 0, mpcekf_step / mpcekf_step_ex capture each new call
+ * shape (nsteps, output and temperature buffers, diagnostics) into a hipGraph once and
+ * replay it on later calls of the same shape -- the per-step launches of a control loop
+ * that calls mpcekf_step(ctx, 1, ...) every period become one graph launch.  Results are
+ * identical; ignored while mpcekf_set_timing is on.  Also MPCEKF_GRAPH=1 at create. */
+int mpcekf_set_graph(mpcekf_ctx *ctx, int32_t enable);
 int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
 /* The Hildreth problem records of the last fused step, as k_cell left them for
  * k_hild (field-major [MPCEKF_PROB_DOUBLES][ncells]: E(2x2) F(2) Hv(5) He(5) Hs(5)

@@ -74,7 +74,7 @@ EXPORTS = [
     "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
-    "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag",
+    "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag", "mpcekf_set_graph",
 ]
 
 _lib = None
@@ -113,6 +113,7 @@ def load():
     L.mpcekf_get_state.argtypes = [vp, C.POINTER(State)]
     L.mpcekf_set_state.argtypes = [vp, C.POINTER(State)]
     L.mpcekf_set_timing.argtypes = [vp, C.c_int32]
+    L.mpcekf_set_graph.argtypes = [vp, C.c_int32]
     L.mpcekf_get_timing.argtypes = [vp, _dp, C.POINTER(C.c_int64)]
     L.mpcekf_get_hild_problems.argtypes = [vp, _dp, _ip]
     L.mpcekf_get_stamps.argtypes = [vp, C.POINTER(C.c_int64), _ip]

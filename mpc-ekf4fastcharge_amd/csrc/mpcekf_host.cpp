@@ -101,6 +101,41 @@ struct mpcekf_ctx {
   // soc(z,T) ends and the table temperatures, for SOC0n/p at init (OB_step.m:63-65)
   std::vector<double> tabT, soc_end[2][2];
 
+  // mpcekf_set_graph: fused calls captured into hipGraphs, keyed by the call shape
+  bool graph = false;
+  struct GraphEntry {
+    std::vector<uintptr_t> key;
+    hipGraphExec_t exec;
+  };
+  std::vector<GraphEntry> graphs;
+  template <class Fn>
+  int graph_launch(const std::vector<uintptr_t> &key, Fn &&launch) {
+    for (const GraphEntry &g : graphs)
+      if (g.key == key) {
+        HIPCHK(hipGraphLaunch(g.exec, stream));
+        return MPCEKF_OK;
+      }
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    const int rc = launch();
+    hipGraph_t gr = nullptr;
+    hipError_t e = hipStreamEndCapture(stream, &gr);
+    if (rc) {
+      if (gr) (void)hipGraphDestroy(gr);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(MPCEKF_E_HIP, "graph capture: %s", hipGetErrorString(e));
+    hipGraphExec_t ex = nullptr;
+    e = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (e != hipSuccess) return fail(MPCEKF_E_HIP, "graph instantiate: %s", hipGetErrorString(e));
+    if (graphs.size() >= 16) {  // a small cache: oldest shape out
+      (void)hipGraphExecDestroy(graphs.front().exec);
+      graphs.erase(graphs.begin());
+    }
+    graphs.push_back({key, ex});
+    HIPCHK(hipGraphLaunch(ex, stream));
+    return MPCEKF_OK;
+  }
   int diag_bufs() {  // the linearisation records and uk_1 copy of the poles / sv diagnostics
     if (!d_lin) HIPCHK(hipMalloc((void **)&d_lin, (size_t)n * MPCEKF_LIN_SIZE * sizeof(double)));
     if (!d_uk1p) HIPCHK(hipMalloc((void **)&d_uk1p, (size_t)n * sizeof(double)));
@@ -442,6 +477,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   X->quad = false;
   if (const char *e = std::getenv("MPCEKF_QUAD")) X->quad = quad_ok && std::atoi(e) != 0;
   if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) X->ekf4_block = std::atoi(e) == 1024 ? 1024 : 512;
+  if (const char *e = std::getenv("MPCEKF_GRAPH")) X->graph = std::atoi(e) != 0;  // as mpcekf_set_graph
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
   if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
   const size_t n = (size_t)ncells, NM = (size_t)X->NM;
@@ -509,6 +545,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
                   X->w.q, X->w.list, X->w.hist};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
+  for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);
   if (X->stream) (void)hipStreamDestroy(X->stream);
   delete X;
   return MPCEKF_OK;
@@ -662,94 +699,107 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   // current each LAZY_H steps and at the end of the call, so between calls (stage entry
   // points, get/set_state) every model is current, exactly as after eager updates.
   std::vector<char> flushed((size_t)nsteps, 0);
-  for (int k = 0; k < nsteps; ++k) {
-    const int t = k + 1;
-    // sampled steps: every timing_every-th (k = every-1, 2 every-1, ...: with every dividing
-    // the flush period these include the flush steps) and the last
-    const bool sample = X->timing && ((k + 1) % X->timing_every == 0 || k == nsteps - 1);
-    hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
-    if (E) HIPCHK(hipEventRecord(E[0], X->stream));
-    if (diag) HIPCHK(hipMemcpyAsync(X->d_uk1p, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
-    if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
-                   "plant")))
-      return rc;
-    if (E) HIPCHK(hipEventRecord(E[1], X->stream));
-    KIO io{};
-    io.mode = MODE_FUSED;
-    io.lazy_t = t;
-    io.stamps = X->d_stamps;
-    io.u = (double *)row(0, k);
-    io.v = (double *)row(1, k);
-    io.soc = (double *)row(2, k);
-    io.phise = (double *)row(3, k);
-    io.nexec = (int *)row(4, k);
-    io.x_out = (double *)row(5, k);
-    io.zk = f[6].dev ? (double *)row(6, k) : X->d_zk;
-    double *zbk_k = f[7].dev ? (double *)row(7, k) : X->d_zbk;
-    io.zbk = bounds ? zbk_k : nullptr;
-    io.bnd = bounds ? X->d_bnd : nullptr;
-    io.junc_out = (double *)row(8, k);
-    io.jfin_out = (double *)row(9, k);
-    io.normdu_out = (double *)row(10, k);
-    io.nviol_out = (int *)row(11, k);
-    if (diag) io.lin_out = X->d_lin;
-    KIO iow{};  // wide horizons: iterMPC in mpcekf_wide.hip from the linearisation record
-    if (X->wide) {
-      io.lin_out = X->d_lin;
-      io.zsoc_out = X->d_zsoc;
-      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF | P_LIN), "cell"))) return rc;
-      iow.mode = MODE_FUSED;
-      iow.lin_in = X->d_lin;
-      iow.soc_k1_in = X->d_zsoc;
-      iow.u = io.u;
-      iow.nexec = io.nexec;
-      iow.junc_out = io.junc_out;
-      iow.jfin_out = io.jfin_out;
-      iow.normdu_out = io.normdu_out;
-      iow.nviol_out = io.nviol_out;
-      if ((rc = lerr(launch_mpc_wide(X->k, X->s, iow, X->w, X->stream), "mpc_wide"))) return rc;
-    } else if (X->split_cell || X->quad) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
-      io.xm_out = X->d_xm;
-      io.xg_out = X->d_xg;
-      if (X->quad) {
-        if ((rc = lerr(launch_ekf4(X->r, X->k, X->s, io, X->stream, X->ekf4_block), "ekf4"))) return rc;
-      } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) {
+  auto run_steps = [&]() -> int {
+    for (int k = 0; k < nsteps; ++k) {
+      const int t = k + 1;
+      // sampled steps: every timing_every-th (k = every-1, 2 every-1, ...: with every dividing
+      // the flush period these include the flush steps) and the last
+      const bool sample = X->timing && ((k + 1) % X->timing_every == 0 || k == nsteps - 1);
+      hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
+      if (E) HIPCHK(hipEventRecord(E[0], X->stream));
+      if (diag) HIPCHK(hipMemcpyAsync(X->d_uk1p, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
+      if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
+                     "plant")))
+        return rc;
+      if (E) HIPCHK(hipEventRecord(E[1], X->stream));
+      KIO io{};
+      io.mode = MODE_FUSED;
+      io.lazy_t = t;
+      io.stamps = X->d_stamps;
+      io.u = (double *)row(0, k);
+      io.v = (double *)row(1, k);
+      io.soc = (double *)row(2, k);
+      io.phise = (double *)row(3, k);
+      io.nexec = (int *)row(4, k);
+      io.x_out = (double *)row(5, k);
+      io.zk = f[6].dev ? (double *)row(6, k) : X->d_zk;
+      double *zbk_k = f[7].dev ? (double *)row(7, k) : X->d_zbk;
+      io.zbk = bounds ? zbk_k : nullptr;
+      io.bnd = bounds ? X->d_bnd : nullptr;
+      io.junc_out = (double *)row(8, k);
+      io.jfin_out = (double *)row(9, k);
+      io.normdu_out = (double *)row(10, k);
+      io.nviol_out = (int *)row(11, k);
+      if (diag) io.lin_out = X->d_lin;
+      KIO iow{};  // wide horizons: iterMPC in mpcekf_wide.hip from the linearisation record
+      if (X->wide) {
+        io.lin_out = X->d_lin;
+        io.zsoc_out = X->d_zsoc;
+        if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF | P_LIN), "cell"))) return rc;
+        iow.mode = MODE_FUSED;
+        iow.lin_in = X->d_lin;
+        iow.soc_k1_in = X->d_zsoc;
+        iow.u = io.u;
+        iow.nexec = io.nexec;
+        iow.junc_out = io.junc_out;
+        iow.jfin_out = io.jfin_out;
+        iow.normdu_out = io.normdu_out;
+        iow.nviol_out = io.nviol_out;
+        if ((rc = lerr(launch_mpc_wide(X->k, X->s, iow, X->w, X->stream), "mpc_wide"))) return rc;
+      } else if (X->split_cell || X->quad) {  // iterEKF, then EKFmatsHandler + iterMPC from zk and Xind in HBM
+        io.xm_out = X->d_xm;
+        io.xg_out = X->d_xg;
+        if (X->quad) {
+          if ((rc = lerr(launch_ekf4(X->r, X->k, X->s, io, X->stream, X->ekf4_block), "ekf4"))) return rc;
+        } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream, P_EKF), "cell"))) {
+          return rc;
+        }
+        KIO io2 = io;
+        io2.zk = nullptr;
+        io2.zbk = nullptr;
+        io2.bnd = nullptr;
+        io2.xm_out = nullptr;
+        io2.xg_out = nullptr;
+        io2.zk_in = io.zk;
+        io2.xm_in = X->d_xm;
+        io2.xg_in = X->d_xg;
+        if ((rc = lerr(launch_cell(X->r, X->k, X->s, io2, X->stream, P_MPC), "cell"))) return rc;
+      } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) {
         return rc;
       }
-      KIO io2 = io;
-      io2.zk = nullptr;
-      io2.zbk = nullptr;
-      io2.bnd = nullptr;
-      io2.xm_out = nullptr;
-      io2.xg_out = nullptr;
-      io2.zk_in = io.zk;
-      io2.xm_in = X->d_xm;
-      io2.xg_in = X->d_xg;
-      if ((rc = lerr(launch_cell(X->r, X->k, X->s, io2, X->stream, P_MPC), "cell"))) return rc;
-    } else if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) {
-      return rc;
+      if (E) HIPCHK(hipEventRecord(E[2], X->stream));
+      // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
+      if (bounds && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
+      if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+      if (X->wide) {
+        if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
+      } else if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
+        return rc;
+      }
+      if (diag) {
+        double *pk = (double *)row(12, k), *sk = (double *)row(13, k);
+        rc = X->wide ? launch_cl_diag_wide(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream)
+                     : launch_cl_diag(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream);
+        if ((rc = lerr(rc, "cl_diag"))) return rc;
+      }
+      if (E) HIPCHK(hipEventRecord(E[4], X->stream));
+      if (t % X->flush_period == 0 || t == nsteps) {
+        if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
+        flushed[k] = 1;
+      }
+      if (E) HIPCHK(hipEventRecord(E[5], X->stream));
     }
-    if (E) HIPCHK(hipEventRecord(E[2], X->stream));
-    // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
-    if (bounds && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
-    if (E) HIPCHK(hipEventRecord(E[3], X->stream));
-    if (X->wide) {
-      if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
-    } else if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
-      return rc;
-    }
-    if (diag) {
-      double *pk = (double *)row(12, k), *sk = (double *)row(13, k);
-      rc = X->wide ? launch_cl_diag_wide(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream)
-                   : launch_cl_diag(X->k, X->n, X->d_lin, X->d_uk1p, pk, sk, X->stream);
-      if ((rc = lerr(rc, "cl_diag"))) return rc;
-    }
-    if (E) HIPCHK(hipEventRecord(E[4], X->stream));
-    if (t % X->flush_period == 0 || t == nsteps) {
-      if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
-      flushed[k] = 1;
-    }
-    if (E) HIPCHK(hipEventRecord(E[5], X->stream));
+    return MPCEKF_OK;
+  };
+  if (X->graph && !X->timing && nsteps > 0) {
+    // the call's launches depend only on these (kernel arguments are call-relative:
+    // lazy_t = 1..nsteps, the flush schedule, the output rows), so a repeated call shape
+    // replays one instantiated graph instead of 5-7 launches per step
+    std::vector<uintptr_t> key = {(uintptr_t)nsteps, (uintptr_t)dtc, (uintptr_t)diag, (uintptr_t)bounds};
+    for (const F &e : f) key.push_back((uintptr_t)e.dev);
+    if ((rc = X->graph_launch(key, run_steps))) return rc;
+  } else if ((rc = run_steps())) {
+    return rc;
   }
   if (!outputs_on_device)
     for (int i = 0; i < NF; ++i)
@@ -798,6 +848,12 @@ int mpcekf_step(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, double *tr
   tr.phise = traj_phise;
   tr.nexec = traj_nexec;
   return mpcekf_step_ex(X, nsteps, tc_degC, &tr, outputs_on_device);
+}
+
+int mpcekf_set_graph(mpcekf_ctx *X, int32_t enable) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  X->graph = enable != 0;
+  return MPCEKF_OK;
 }
 
 int mpcekf_set_timing(mpcekf_ctx *X, int32_t enable) {

@@ -176,6 +176,10 @@ class Context:
         p = [C.c_void_p(x) if x else None for x in (u, v, soc, phise, nexec)]
         check(self.L.mpcekf_step(self.h, int(nsteps), None, *p, 1))
 
+    def set_graph(self, enable=True):
+        """Replay repeated fused-call shapes from captured hipGraphs (mpcekf_set_graph)."""
+        check(self.L.mpcekf_set_graph(self.h, int(bool(enable))))
+
     def set_timing(self, enable=True):
         """enable: True/1 = every step; N > 1 = sample every N-th step (less perturbation)."""
         check(self.L.mpcekf_set_timing(self.h, int(enable)))

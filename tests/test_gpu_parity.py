@@ -471,3 +471,28 @@ def test_generic_hildreth_any_size_matches_oracle(oc, M, Nc, ncon, n):
         _bitwise(DU[i], d2, f"DU[{i}]")
         _bitwise(lam[i], l2, f"lambda[{i}]")
     assert (ne == 100).any() and (ne < 100).any()
+
+
+def test_graph_replay_is_exact(rom, M):
+    """mpcekf_set_graph: repeated call shapes replayed from captured hipGraphs give the
+    bits of direct launches (calls of 1 and 5 steps, shapes alternating, host outputs)."""
+    n = 192
+    soc0, tc = batch_inputs(n, seed=21)
+    runs = []
+    for graph in (False, True):
+        with M.Context(rom, n) as ctx:
+            ctx.init_cells(soc0, tc)
+            ctx.set_graph(graph)
+            got = []
+            for call in range(30):
+                ns = 1 if call % 3 else 5
+                out = ctx.step(ns, outputs=("u", "v", "soc", "phise", "nexec"))
+                got.append(out)
+            st = ctx.get_state()
+            runs.append((got, st))
+    (a, sa), (b, sb) = runs
+    for x, y in zip(a, b):
+        for k in x:
+            _bitwise(x[k], y[k], k)
+    for k in ("bigX", "ekf", "scal", "lam", "status"):
+        _bitwise(sa[k], sb[k], k)
