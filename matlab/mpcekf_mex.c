@@ -22,6 +22,7 @@
  *   [DU,lambda,nexec] = mpcekf_mex('hildreth', E, F, M, gamma, lambda0, maxIter)   (hildreth.m:1)
  *   [Phi,G]           = mpcekf_mex('predmat', a, C, D, Np, Nc)         (predMat.m:1, A = diag(a), B = 1)
  *   st                = mpcekf_mex('get_state', h)    /  mpcekf_mex('set_state', h, st)
+ *                       mpcekf_mex('graph', h, enable)                 mpcekf_set_graph (replay repeated step calls)
  * Per-cell vectors are 1 x ncells or ncells x 1; zk / zbk are (nz+2) x ncells, xm / xg
  * 4 x ncells (xm: 0-based model index t*nZ+z), lin 35 x ncells -- MATLAB's column-major
  * k x ncells is the library's cell-major [ncells][k], so no copy is made for them.
@@ -244,6 +245,9 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     plhs[1] = imat(1, nc);
     chk(mpcekf_mpc_step(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
                         mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1])));
+  } else if (!strcmp(cmd, "graph")) {
+    if (nrhs < 3) mexErrMsgIdAndTxt("mpcekf:arg", "graph: enable flag");
+    chk(mpcekf_set_graph(h, (int32_t)(mxGetScalar(prhs[2]) != 0.0)));
   } else if (!strcmp(cmd, "mpcdiag")) {
     plhs[0] = mxCreateDoubleMatrix(7, (mwSize)nc, mxCOMPLEX);  /* interleaved (re, im): [ncells][7][2] */
     plhs[1] = dmat(7, nc);
