@@ -160,3 +160,17 @@ def test_wide_checkpoint_and_schedule(rom, M):
     for k in ("u", "v", "soc", "phise", "nexec"):
         np.testing.assert_array_equal(ra[k], np.concatenate([r[k] for r in rb]), err_msg=k)
         np.testing.assert_array_equal(x[k], y[k], err_msg=k)
+
+
+def test_wide_temperature_profile_matches_oracle(rom, oc, M):
+    """Np = 20 / Nc = 10 with a temperature per step (a 10-degree ramp and a sine, per
+    cell): bitwise against the C oracle over 400 closed-loop steps."""
+    n, steps = 24, 400
+    soc0, tc = batch_inputs(n, seed=77)
+    k = np.arange(steps)[:, None]
+    tc_traj = tc[None, :] + 10.0 * k / steps + 2.0 * np.sin(k / 37.0 + np.arange(n)[None, :])
+    ref = oc.run(rom, soc0, tc, steps, nthreads=8, Np=NP, Nc=NC, tc_traj=tc_traj)
+    out = M.runMPC(rom, soc0, tc, steps, cfg=_cfg(M), tc_traj=tc_traj)
+    np.testing.assert_array_equal(out["status"], ref["status"])
+    for key in ("u", "v", "soc", "phise", "nexec"):
+        assert np.array_equal(out[key], ref[key], equal_nan=key != "nexec"), key
