@@ -81,6 +81,17 @@ def batch_inputs(n, seed=0x5EED):
     return rng.uniform(5, 30, n), rng.uniform(20, 30, n)
 
 
+def rom_grid(args):
+    """make_synth_rom set-point grid: NM = temps x socs (default 3 x 21 = 63); T in
+    [15, 35] degC and SOC in [0, 100] % evenly."""
+    kw = {}
+    if args.rom_temps:
+        kw["T_degC"] = tuple(np.linspace(15.0, 35.0, args.rom_temps)) if args.rom_temps > 1 else (25.0,)
+    if args.rom_socs:
+        kw["SOC_pct"] = tuple(np.linspace(0.0, 100.0, args.rom_socs))
+    return kw
+
+
 def shard_range(total, world, rank):
     """Contiguous cell range [start, stop) of one rank (runMPC.m:83-112 has no cross-cell
     term, so any split gives the same bits per cell)."""
@@ -150,6 +161,9 @@ def main():
     ap.add_argument("--bounds", type=int, default=1, help="compute boundzk every step (iterEKF.m:186-205)")
     ap.add_argument("--np", type=int, default=5, help="prediction horizon (configs[4]: 20)")
     ap.add_argument("--nc", type=int, default=2, help="control horizon (configs[4]: 10)")
+    ap.add_argument("--rom-temps", type=int, default=0,
+                    help="SURVEY.md 8(d) sensitivity: temperature set-points of the synthetic ROM (default 3)")
+    ap.add_argument("--rom-socs", type=int, default=0, help="SOC set-points of the synthetic ROM (default 21)")
     ap.add_argument("--cpu-cells", type=int, default=32768)
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: the cores this process may use")
@@ -206,7 +220,7 @@ def main():
     else:
         P = importlib.import_module("mpc-ekf4fastcharge_amd")
         M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
-        rom = P.make_synth_rom()
+        rom = P.make_synth_rom(**rom_grid(args))
         soc0_all, tc_all = batch_inputs(total)
         cfg = M.make_config(bounds=bool(args.bounds), Np=args.np, Nc=args.nc)
         ctx = M.Context(rom, ncell, cfg, device=device)
