@@ -361,6 +361,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     for (int i = 0; i < NPK; ++i)  // Sigma time update coefficients (iterEKF.m:78)
       b[nzp * NX + nzp + NX + i] = R->A[(size_t)m * n1 + pr[i]] * R->A[(size_t)m * n1 + pc[i]];
   }
+  if (cb.size() & 1) cb.push_back(0.0);  // tables at an even offset: 16-byte staging in rom_global mode
   r.cell_tab = (int)cb.size();
   r.cell_tablen = (int)cell_tablen;
   cb.insert(cb.end(), tabs.begin(), tabs.begin() + cell_tablen);
@@ -377,6 +378,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     }
     for (int e = 0; e < 6; ++e) b[NPLANT * NX + 2 * NPLANT + e] = R->A[(size_t)m * n1 + e];  // bigA column
   }
+  if (pb.size() & 1) pb.push_back(0.0);
   r.plant_tab = (int)pb.size();
   r.plant_tablen = (int)tabs.size();
   pb.insert(pb.end(), tabs.begin(), tabs.end());
@@ -392,9 +394,15 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     for (int i = 0; i < NPK; ++i) cC[m * REC + NX + i] = a[pr[i]] * a[pc[i]];
     for (int e = 0; e < 6; ++e) cP[m * 6 + e] = a[e];
   }
-  const int lds_need = std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r)), plant_lds_bytes(r));
-  if (lds_need > 160 * 1024)
-    return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of ROM tables exceed the 160 KiB LDS", lds_need);
+  // Model rows and tables staged in LDS when they fit; otherwise (NM above ~75 at the
+  // default grid, or MPCEKF_ROM_GLOBAL=1) only the tables are, and the model rows are read
+  // from the global blob (L2-resident).  Same arithmetic either way.
+  auto lds_need = [&]() { return std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r)), plant_lds_bytes(r)); };
+  const char *gev = getenv("MPCEKF_ROM_GLOBAL");
+  r.rom_global = gev && atoi(gev) == 1;
+  if (lds_need() > 160 * 1024) r.rom_global = 1;
+  if (lds_need() > 160 * 1024)
+    return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of electrode tables exceed the 160 KiB LDS", lds_need());
   int rc;
   if ((rc = dalloc(&X->d_cell_blob, cb.size()))) return rc;
   if ((rc = dalloc(&X->d_plant_blob, pb.size()))) return rc;

@@ -1232,12 +1232,17 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
 // ---------------------------------------------------------------------------
 // k_plant: OB_step simStep outputs for every cell (lane per cell)
 // ---------------------------------------------------------------------------
+template <bool GR>
 __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout,
                                                const int lazy_t, const double *tc_in) {
   extern __shared__ double lds[];
-  stage_lds(lds, r.plant_blob, r.plant_len);
+  // GR: tables only in LDS (tb + plant_tab is lds), model rows from the global blob
+  const int lo = GR ? r.plant_tab : 0;
+  stage_lds(lds, r.plant_blob + lo, r.plant_len - lo);
   __syncthreads();
-  const double *Tp = lds + r.plant_tab + r.plant_tablen;
+  const double *tb = lds - lo;
+  const double *L = GR ? r.plant_blob : lds;
+  const double *Tp = tb + r.plant_tab + r.plant_tablen;
   const double *Zp = Tp + MAXT;
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
@@ -1254,7 +1259,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   }
   double Iapp = iapp[c];
   double T = (tc_in ? tc_in[c] : s.Tc[c]) + 273.15;  // OB_step.m:75
-  const ETab et = etab(r, lds + r.plant_tab, T);
+  const ETab et = etab(r, tb + r.plant_tab, T);
   double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
   const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
   double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
@@ -1297,7 +1302,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       tsj[j] = s.ts_plant[c * r.NM + mm[j]];
-      const double *a = lds + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
+      const double *a = L + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
       for (int k = tsj[j] + 1; k < lazy_t; ++k) {  // OB_step.m:198-200 for the skipped steps
         const double u = s.hist_u[(size_t)(k % LAZY_H) * s.n + c];
 #pragma unroll
@@ -1310,7 +1315,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
     double x[6];
 #pragma unroll
     for (int e = 0; e < 6; ++e) x[e] = xs[j][e];
-    const double *B = lds + mm[j] * PREC;
+    const double *B = L + mm[j] * PREC;
 #pragma unroll
     for (int q = 0; q < NPLANT; ++q) {
       double acc = 0.0;
@@ -1348,7 +1353,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (tsj[j] >= lazy_t) continue;
-      const double *a = lds + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
+      const double *a = L + mm[j] * PREC + NPLANT * NX + 2 * NPLANT;
       double2 *p = reinterpret_cast<double2 *>(bx + (size_t)mm[j] * 6);
       double x[6];
 #pragma unroll
@@ -1723,26 +1728,28 @@ __device__ __forceinline__ void meas_cov_mb(double S[NA6 * NA6], const double L[
 // ---------------------------------------------------------------------------
 // k_cell: iterEKF measurement update + EKFmatsHandler + iterMPC (lane per cell)
 // ---------------------------------------------------------------------------
-template <int NZ, int PARTS, bool MB = false>
+template <int NZ, int PARTS, bool MB = false, bool GR = false>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
-  stage_lds(lds, r.cell_blob, r.cell_len);
+  const int lo = GR ? r.cell_tab : 0;  // GR: model rows from the global blob (k_plant)
+  stage_lds(lds, r.cell_blob + lo, r.cell_len - lo);
   __syncthreads();
-  const double *Tp = lds + r.cell_tab + r.cell_tablen;
+  const double *tb = lds - lo;
+  const double *Tp = tb + r.cell_tab + r.cell_tablen;
   const double *Zp = Tp + MAXT;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= s.n) return;
   const int nz = r.nz;
   const double NaN = __builtin_nan("");
   CellCtx cc;
-  cc.L = lds;
+  cc.L = GR ? r.cell_blob : lds;
   cc.Tp = Tp;
   cc.Zp = Zp;
   cc.erec = s.ekf + (size_t)c * r.NM * REC;
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.et = etab(r, lds + r.cell_tab, cc.T);
+  cc.et = etab(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
   const bool fused = io.mode & MODE_FUSED;
   if (io.mode & (MODE_MPC | MODE_FUSED)) s.hflag[c] = 0;  // set again only if hildreth.m must run
@@ -2196,12 +2203,14 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 // 1024-thread blocks (256 cells): the ~130 KB ROM blob is staged once per CU and the
 // CU runs 4 waves per SIMD.
 // ---------------------------------------------------------------------------
-template <int NZ, int BLOCK>
+template <int NZ, int BLOCK, bool GR>
 __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
-  stage_lds(lds, r.cell_blob, r.cell_len);
+  const int lo = GR ? r.cell_tab : 0;  // GR: model rows from the global blob (k_plant)
+  stage_lds(lds, r.cell_blob + lo, r.cell_len - lo);
   __syncthreads();
-  const double *Tp = lds + r.cell_tab + r.cell_tablen;
+  const double *tb = lds - lo;
+  const double *Tp = tb + r.cell_tab + r.cell_tablen;
   const double *Zp = Tp + MAXT;
   const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
@@ -2212,14 +2221,14 @@ __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, con
   const int nz = r.nz;
   const double NaN = __builtin_nan("");
   CellCtx cc;
-  cc.L = lds;
+  cc.L = GR ? r.cell_blob : lds;
   cc.Tp = Tp;
   cc.Zp = Zp;
   cc.erec = s.ekf + (size_t)c * r.NM * REC;
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.et = etab(r, lds + r.cell_tab, cc.T);
+  cc.et = etab(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
   const int t = io.lazy_t;
   if (live && j == 0) s.hflag[c] = 0;
@@ -2399,7 +2408,7 @@ __device__ __forceinline__ double quad_sum_seq(double v) {  // (((0 + v0) + v1) 
 // block is the CU's whole occupancy (4 waves per SIMD) and stages the blob once.
 constexpr int BOUNDS_BLOCK = 1024;
 // k_bounds stages only the models of the cell blob (its getChatV scalars come from k_cell)
-__host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.cell_tab + 1; }
+__host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.rom_global ? 0 : r.cell_tab + 1; }
 // row' * Sigma * row in symmetric form: T = Sigma with doubled off-diagonals,
 // u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, explicit fma at every step
 // (orc qform: 20 operations instead of the 60 of Sigma*row then row'*(.)).
@@ -2415,11 +2424,12 @@ __device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]
   return q;
 }
 
-template <int NZ>
+template <int NZ, bool GR>
 __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KState s, const double *bd, double *zbk) {
   extern __shared__ double lds[];
-  stage_lds(lds, r.cell_blob, r.cell_tab);
+  if (!GR) stage_lds(lds, r.cell_blob, r.cell_tab);  // GR: model rows from the global blob
   __syncthreads();
+  const double *L = GR ? r.cell_blob : lds;
   const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = s.n;
   const int j = (int)(gt & 3);
@@ -2429,7 +2439,7 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   const bool valid = cq < n && bd[BD_M * n + c] >= 0.0;
   const double g = bd[(BD_G + j) * n + c];
   const int m = valid ? (int)bd[(BD_M + j) * n + c] : 0;
-  const double *Cm = lds + m * r.cell_stride;
+  const double *Cm = L + m * r.cell_stride;
   const double S0 = bd[BD_S0 * n + c];
   // SigmaX of the first corner for all four (iterEKF.m:191)
   double S1b[NPK];
@@ -2462,7 +2472,7 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   // The constant-column terms (c0 * S0) * c0 of the 7 kinds (C0_*) in an LDS row per
   // cell, lane j filling kinds j and j + 4: each form then adds its term by a uniform
   // offset instead of a select chain.
-  double *c0t = lds + bounds_c0_base(r) + (threadIdx.x >> 2) * 8;
+  double *c0t = lds + (GR ? 0 : r.cell_tab + 1) + (threadIdx.x >> 2) * 8;
   {
     const double cv[8] = {0.0, ChV0, res0n, res0p, dUn * res0n, dUp * res0p, -dUn * res0n, 0.0};
     double lo = cv[0], hi = cv[4];
@@ -3020,17 +3030,25 @@ int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double
 }
 static int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
-int cell_lds_bytes(const KRom &r) { return (int)((r.cell_len + 1) * sizeof(double)); }
+int cell_lds_bytes(const KRom &r) {
+  return (int)((r.cell_len - (r.rom_global ? r.cell_tab : 0) + 1) * sizeof(double));
+}
 int bounds_lds_bytes(const KRom &r) { return (bounds_c0_base(r) + BOUNDS_BLOCK / 4 * 8) * (int)sizeof(double); }
-int plant_lds_bytes(const KRom &r) { return (int)((r.plant_len + 1) * sizeof(double)); }
+int plant_lds_bytes(const KRom &r) {
+  return (int)((r.plant_len - (r.rom_global ? r.plant_tab : 0) + 1) * sizeof(double));
+}
 
 bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
 
 int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
                  void *stream) {
   if (s.n == 0) return 0;
-  hipLaunchKernelGGL(k_plant, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r, s,
-                     iapp, vout, lazy_t, tc_in);
+  if (r.rom_global)
+    hipLaunchKernelGGL(k_plant<true>, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r,
+                       s, iapp, vout, lazy_t, tc_in);
+  else
+    hipLaunchKernelGGL(k_plant<false>, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r,
+                       s, iapp, vout, lazy_t, tc_in);
   return (int)hipGetLastError();
 }
 
@@ -3052,16 +3070,24 @@ int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iap
   return (int)hipGetLastError();
 }
 
-template <int NZ, int PARTS, bool MB>
-static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+template <int NZ, int PARTS, bool MB, bool GR>
+static void launch_cell_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   int lds = cell_lds_bytes(r);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB, GR>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+}
+
+template <int NZ, int PARTS, bool MB>
+static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  if (r.rom_global)
+    launch_cell_g<NZ, PARTS, MB, true>(r, c, s, io, st);
+  else
+    launch_cell_g<NZ, PARTS, MB, false>(r, c, s, io, st);
 }
 
 template <int NZ>
@@ -3095,16 +3121,24 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
   return (int)hipGetLastError();
 }
 
-template <int NZ, int BLOCK>
-static void launch_ekf4_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+template <int NZ, int BLOCK, bool GR>
+static void launch_ekf4_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_ekf4<NZ, BLOCK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_ekf4<NZ, BLOCK, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_ekf4<NZ, BLOCK>), dim3(grid_for(s.n * 4, BLOCK)), dim3(BLOCK), cell_lds_bytes(r), st, r, c,
-                     s, io);
+  hipLaunchKernelGGL((k_ekf4<NZ, BLOCK, GR>), dim3(grid_for(s.n * 4, BLOCK)), dim3(BLOCK), cell_lds_bytes(r), st, r,
+                     c, s, io);
+}
+
+template <int NZ, int BLOCK>
+static void launch_ekf4_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  if (r.rom_global)
+    launch_ekf4_g<NZ, BLOCK, true>(r, c, s, io, st);
+  else
+    launch_ekf4_g<NZ, BLOCK, false>(r, c, s, io, st);
 }
 
 // block = 512 (128 cells, 256 VGPRs, 2 waves per SIMD) or 1024 (256 cells, 128 VGPRs, 4 waves per SIMD)
@@ -3120,15 +3154,24 @@ int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
   return (int)hipGetLastError();
 }
 
-template <int NZ>
-static void launch_bounds_t(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
+template <int NZ, bool GR>
+static void launch_bounds_g(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
   static bool attr = false;
   int lds = bounds_lds_bytes(r);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_bounds<NZ>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void *)k_bounds<NZ, GR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(k_bounds<NZ>, dim3(grid_for(4 * s.n, BOUNDS_BLOCK)), dim3(BOUNDS_BLOCK), lds, st, r, s, bnd, zbk);
+  hipLaunchKernelGGL((k_bounds<NZ, GR>), dim3(grid_for(4 * s.n, BOUNDS_BLOCK)), dim3(BOUNDS_BLOCK), lds, st, r, s, bnd,
+                     zbk);
+}
+
+template <int NZ>
+static void launch_bounds_t(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
+  if (r.rom_global)
+    launch_bounds_g<NZ, true>(r, s, bnd, zbk, st);
+  else
+    launch_bounds_g<NZ, false>(r, s, bnd, zbk, st);
 }
 
 int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk, void *stream) {

@@ -44,6 +44,9 @@ struct KRom {
   const double *plant_blob;       // per model [C 9*5][res0 9][D 9] ... then tables
   int plant_tab, plant_tablen, plant_len;
   const double *bulk_tab;         // cA[NM*20], cB[NM*20], cP[NM*6]
+  // 1: the model rows of both blobs do not fit the 160 KiB LDS (large NM); the kernels
+  // stage only the tables (from *_tab, even offsets) and read the model rows from HBM/L2
+  int rom_global;
 };
 
 struct KCfg {
