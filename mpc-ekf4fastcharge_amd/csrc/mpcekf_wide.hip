@@ -27,6 +27,9 @@
 #ifndef MPCEKF_WIDE_JUNK
 #define MPCEKF_WIDE_JUNK 1
 #endif
+#ifndef PREP_UNROLL
+#define PREP_UNROLL 1  // k_hild_prep's row loops (rows in flight per wave)
+#endif
 #ifndef MPCEKF_WIDE_SORT
 #define MPCEKF_WIDE_SORT 1
 #endif
@@ -231,7 +234,9 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
   if (io.junc_out) io.junc_out[c] = J_unc;
   // constraintsMPC.m rows: gamma to the record, M*DU - gamma tested as each row is formed
   int nv = 0, nviol = 0;
-#pragma unroll
+  // the row loops stay rolled (instruction fetch, see k_hild_prep); the G_v / -G_e rows'
+  // M(k, :) is a shift register of the H column with mrow_vec's values
+#pragma unroll 1
   for (int i = 0; i < 4 * NC; ++i) {
     const double g = i < NC ? (cf.u_max - uk_1) * 1.0 : i < 2 * NC ? -(cf.u_min - uk_1) * 1.0
                    : i < 3 * NC ? cf.du_max * 1.0 : -cf.du_min * 1.0;
@@ -243,37 +248,49 @@ __global__ void __launch_bounds__(64) k_mpc_wide(const KCfg cf, const KState s, 
     if (acc - g > 1e-9) nviol++;
   }
   {  // G_v rows: predMat(Cv, Dv), gamma = v_max - (Phi_v*dx + bv)
-    double S[6], P[6], Cb[7], row[7], Hv[NP];
+    double S[6], P[6], Cb[7], row[7], b[NC];
 #pragma unroll
     for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; Cb[j] = L.Cv[j]; }
     Cb[6] = L.Dv;
 #pragma unroll
+    for (int j = 0; j < NC; ++j) b[j] = 0.0;
+#pragma unroll 1
     for (int k = 0; k < NP; ++k) {
-      pred_step(L.a, Cb, S, P, Hv[k], row);
+      double Hvk;
+      pred_step(L.a, Cb, S, P, Hvk, row);
       const double g = cf.v_max - (rowdot(row, dx) + L.bv * 1.0);
       pb[(T::GAM + 4 * NC + k) * n + c] = g;
-      pb[(T::HV + k) * n + c] = Hv[k];
+      pb[(T::HV + k) * n + c] = Hvk;
+#pragma unroll
+      for (int j = NC - 1; j > 0; --j) b[j] = b[j - 1];
+      b[0] = Hvk;
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < NC; ++j) acc = acc + (j <= k ? Hv[k - j] : 0.0) * DU[j];
+      for (int j = 0; j < NC; ++j) acc = acc + b[j] * DU[j];
       if (acc - g > 0) nv++;
       if (acc - g > 1e-9) nviol++;
     }
   }
   {  // -G_e rows: predMat(Cphi, Dphi), gamma = -phise_min + (Phi_e*dx + bphi)
-    double S[6], P[6], Cb[7], row[7], He[NP];
+    double S[6], P[6], Cb[7], row[7], b[NC];
 #pragma unroll
     for (int j = 0; j < 6; ++j) { S[j] = 0.0; P[j] = 1.0; Cb[j] = L.Cphi[j]; }
     Cb[6] = L.Dphi;
 #pragma unroll
+    for (int j = 0; j < NC; ++j) b[j] = -0.0;
+#pragma unroll 1
     for (int k = 0; k < NP; ++k) {
-      pred_step(L.a, Cb, S, P, He[k], row);
+      double Hek;
+      pred_step(L.a, Cb, S, P, Hek, row);
       const double g = -cf.phise_min + (rowdot(row, dx) + L.bphi * 1.0);
       pb[(T::GAM + 4 * NC + NP + k) * n + c] = g;
-      pb[(T::HE + k) * n + c] = He[k];
+      pb[(T::HE + k) * n + c] = Hek;
+#pragma unroll
+      for (int j = NC - 1; j > 0; --j) b[j] = b[j - 1];
+      b[0] = -Hek;
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < NC; ++j) acc = acc + (-(j <= k ? He[k - j] : 0.0)) * DU[j];
+      for (int j = 0; j < NC; ++j) acc = acc + b[j] * DU[j];
       if (acc - g > 0) nv++;
       if (acc - g > 1e-9) nviol++;
     }
@@ -323,6 +340,50 @@ __device__ __forceinline__ void mrow_vec(int i, const double *Hb, double b[NC]) 
   }
 }
 
+// One row of k_hild_prep: K_i = M(i,:)*(E\F) + gamma_i, and for a distinct row X(:,u) =
+// E\M(i,:)' and H_ii (also stored for the negated copy at i + NC when dup)
+template <int NP, int NC>
+__device__ __forceinline__ void prep_row(const KWide &w, const double *pb, int64_t n, int64_t c, int i, bool neg,
+                                         int u, bool dup, const double R[NC][NC], const double y[NC],
+                                         const double b[NC], double gam, bool &fin, double *xt, bool act) {
+  using T = W<NP, NC>;
+  constexpr int NCON = T::NCON;
+  double kk = 0.0;
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    kk = kk + b[k] * y[k];
+    fin = fin && isfinite(b[k]);
+  }
+  if (act) w.K[(size_t)c * NCON + i] = kk + gam;
+  if (neg) return;  // H_ii of -b equals that of b (stored with the b row)
+  double x[NC];
+  chol_apply<NC>(R, b, x);
+  double h = 0.0;
+  const int l = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    h = h + b[k] * x[k];
+    fin = fin && isfinite(x[k]);
+    xt[l * (NC + 1) + k] = x[k];  // odd stride: fewer bank conflicts
+  }
+  if (act) {
+    w.hii[(size_t)c * NCON + i] = h;
+    if (dup) w.hii[(size_t)c * NCON + i + NC] = h;
+  }
+  // X(:, u) of the wave's 64 cells is one contiguous [64][NC] span of w.X: written back
+  // from the LDS tile as 64 consecutive doubles per store (lane-per-cell stores of x[k]
+  // hit 64 lines per instruction), only the active cells' entries
+  __syncthreads();  // one wave per block
+  const int64_t c0 = (int64_t)blockIdx.x * blockDim.x;
+  const uint64_t am = __ballot(act);
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int e = j * 64 + l, cl = e / NC;
+    if ((am >> cl) & 1) w.X[((size_t)u * n + c0) * NC + e] = xt[cl * (NC + 1) + e % NC];
+  }
+  __syncthreads();
+}
+
 // ---------------------------------------------------------------------------
 // k_hild_prep: hildreth.m:28-29 for the cells that run it (hflag == 1)
 // ---------------------------------------------------------------------------
@@ -332,52 +393,62 @@ template <int NP, int NC>
 __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w) {
   using T = W<NP, NC>;
   constexpr int NCON = T::NCON;
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ double xt[64 * (NC + 1)];  // the wave's X(:, u) tile (one wave per block)
   const int64_t n = s.n;
-  if (c >= n || s.hflag[c] != 1) return;
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = c < n && s.hflag[c] == 1;
+  if (!__ballot(act)) return;  // uniform: every lane of the wave takes part in the tile stores
+  const int64_t cr = act ? c : (int64_t)blockIdx.x * blockDim.x;  // inactive lanes read a valid cell
   const double *pb = w.prob;
   double E[NC][NC], R[NC][NC], F[NC], y[NC];
-  load_E<NP, NC>(pb, n, c, E);
-  if (!chol_n<NC>(E, R)) {
+  load_E<NP, NC>(pb, n, cr, E);
+  if (!chol_n<NC>(E, R) && act) {
     s.hflag[c] = 3;
-    return;
+    act = false;
   }
 #pragma unroll
-  for (int a = 0; a < NC; ++a) F[a] = pb[(T::F + a) * n + c];
+  for (int a = 0; a < NC; ++a) F[a] = pb[(T::F + a) * n + cr];
   chol_apply<NC>(R, F, y);
+  // The row loops stay rolled (fully unrolled the kernel was ~45k straight-line
+  // instructions; rolled or unrolled by 2 or 4 it measured the same, ~0.40 ms per step
+  // at configs[4]).  Row i's M(i, :) is built at run time (mconst / the Toeplitz shift
+  // register), with mrow_vec's values and the same arithmetic per row.
   bool fin = true;
-  double Hb[NP];
-#pragma unroll
-  for (int i = 0; i < NCON; ++i) {
-    if (i >= 4 * NC && (i - 4 * NC) % NP == 0) {  // next Toeplitz block
-      const int blk = (i - 4 * NC) / NP;
-#pragma unroll
-      for (int r = 0; r < NP; ++r) Hb[r] = pb[(T::HV + blk * NP + r) * n + c];
-    }
+  // gamma_i (and the next Toeplitz entry) are loaded one row ahead: vmcnt counts stores
+  // too, so a load issued after a row's stores would wait for their completion
+  double gam = pb[T::GAM * n + cr];
+#pragma unroll PREP_UNROLL
+  for (int i = 0; i < 4 * NC; ++i) {  // [Cu; -Cu; I; -I]
+    const double gi = gam;
+    gam = pb[(T::GAM + i + 1) * n + cr];
     double b[NC];
-    mrow_vec<NP, NC>(i, Hb, b);
-    double kk = 0.0;
 #pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      kk = kk + b[k] * y[k];
-      fin = fin && isfinite(b[k]);
-    }
-    w.K[(size_t)c * NCON + i] = kk + pb[(T::GAM + i) * n + c];
-    if (xneg<NC>(i)) continue;  // H_ii of -b equals that of b (stored with the b row)
-    double x[NC];
-    chol_apply<NC>(R, b, x);
-    double h = 0.0;
-    const int u = xslot<NP, NC>(i);
-#pragma unroll
-    for (int k = 0; k < NC; ++k) {
-      h = h + b[k] * x[k];
-      fin = fin && isfinite(x[k]);
-      w.X[((size_t)u * n + c) * NC + k] = x[k];
-    }
-    w.hii[(size_t)c * NCON + i] = h;
-    if (i < NC || (i >= 2 * NC && i < 3 * NC)) w.hii[(size_t)c * NCON + i + NC] = h;
+    for (int k = 0; k < NC; ++k) b[k] = mconst<NC>(i, k);
+    prep_row<NP, NC>(w, pb, n, cr, i, xneg<NC>(i), xslot<NP, NC>(i), i < NC || (i >= 2 * NC && i < 3 * NC), R, y, b,
+                     gi, fin, xt, act);
   }
-  if (!fin) s.hflag[c] = 2;
+  double hn = pb[T::HV * n + cr];
+#pragma unroll 1
+  for (int blk = 0; blk < 3; ++blk) {  // [G_v; -G_e; G_soc] (constraintsMPC.m:44-80)
+    // row r of a block: M(r, k) = +-H(r - k) for k <= r, +-0 beyond (mrow_vec's -h of
+    // h = 0.0 in the negated block); row r + 1 shifts row r right by one
+    double b[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) b[k] = blk == 1 ? -0.0 : 0.0;
+#pragma unroll PREP_UNROLL
+    for (int r = 0; r < NP; ++r) {
+#pragma unroll
+      for (int k = NC - 1; k > 0; --k) b[k] = b[k - 1];
+      const double h = hn;
+      b[0] = blk == 1 ? -h : h;
+      const int i = 4 * NC + blk * NP + r;
+      const double gi = gam;
+      hn = pb[(T::HV + blk * NP + r + 1) * n + cr];  // HV + 3 NP is GAM: in the record
+      gam = pb[(T::GAM + i + 1) * n + cr];          // GAM + NCON is ERR: in the record
+      prep_row<NP, NC>(w, pb, n, cr, i, false, i - 2 * NC, false, R, y, b, gi, fin, xt, act);
+    }
+  }
+  if (act && !fin) s.hflag[c] = 2;
 }
 
 // ---------------------------------------------------------------------------
