@@ -27,6 +27,9 @@
 #ifndef MPCEKF_WIDE_JUNK
 #define MPCEKF_WIDE_JUNK 1
 #endif
+#ifndef MPCEKF_BCAST_OLD_V
+#define MPCEKF_BCAST_OLD_V 1
+#endif
 #ifndef PREP_UNROLL
 #define PREP_UNROLL 1  // k_hild_prep's row loops (rows in flight per wave)
 #endif
@@ -559,7 +562,10 @@ __device__ __forceinline__ constexpr bool unit_row(int i) {
 }
 template <int J>
 __device__ __forceinline__ double row_bcast(double v) {
-  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xF, 0xF, false);  // row_newbcast:J
+  // every lane of every row is written (row/bank masks full, the source lane valid), so
+  // the "old" operand is dead: passing v lets the move run in place of a dead v instead
+  // of first materialising a zero
+  return __builtin_amdgcn_update_dpp(MPCEKF_BCAST_OLD_V ? v : 0.0, v, 0x150 + J, 0xF, 0xF, false);  // row_newbcast:J
 }
 __device__ __forceinline__ double row_bcast(double v, int j) {  // j a constant after unrolling
   switch (j) {
