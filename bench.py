@@ -170,12 +170,16 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-every", type=int, default=8,
                     help="per-kernel HIP-event timing on every N-th step of the timed region (N | 32)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--pmc", default="",
+                    help="PMC traffic JSON (tools/pmc_traffic.py); default profiles/pmc_traffic.json, "
+                         "profiles/pmc_traffic_np20.json at Np = 20")
     ap.add_argument("--share-device", action="store_true",
                     help="all ranks on device 0 with gloo timing collectives (1-GPU multi-rank test)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: rank/shard/timing orchestration only (CPU tests)")
     args = ap.parse_args()
+    if not args.pmc:
+        args.pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.np == 5 else f"pmc_traffic_np{args.np}.json")
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         launch_ranks(args)

@@ -153,6 +153,8 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
                       mpcekf_ctx **out);
 int mpcekf_ctx_destroy(mpcekf_ctx *ctx);
 int mpcekf_ctx_info(const mpcekf_ctx *ctx, int64_t *ncells, int32_t *nmodels, int32_t *nz, int32_t *ncon);
+/* The configuration the context was created with (e.g. its method, for a checkpoint). */
+int mpcekf_ctx_config(const mpcekf_ctx *ctx, mpcekf_config *cfg);
 
 /* initKF + initMPC + OB_step first call for every cell: SOC0 in percent, Tc in degC
  * (the cell temperature until a call passes another one). */
@@ -215,6 +217,10 @@ int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_mode
 /* iterMPC (uses and updates the context's uk_1 and lambda warm start):
  * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec. */
 int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
+/* The same, also returning this call's iterMPC.m:89-95 cost log (mpcData.cost.J_uncon,
+ * J_final, norm_DU, viol) per cell; any of the four may be NULL. */
+int mpcekf_mpc_step_ex(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol);
 /* iterMPC.m:53-60 stability analysis of the iterMPC that mpcekf_mpc_step would run on lin:
  * Kmpc = first row of E\(G_soc'*Phi_soc), CL = Abar - Bbar*Kmpc; poles [ncells][7][2]
  * (eig(CL): re, im, sorted as in mpcekf_traj), sv [ncells][7] (svd(CL)).  uk_1 [ncells]

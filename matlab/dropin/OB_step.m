@@ -2,8 +2,9 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
 % Drop-in for OB_step.m:1 over the MI355X library: the first call (empty cellState)
 % creates the context from ROM and the recorded initKF / initMPC settings and runs
 % mpcekf_init_cells; every call then runs the plant step (mpcekf_plant_step) at Tc for
-% all cells.  cellState carries the handle; obs holds Vcell only (the library returns
-% the voltage; the other observables stay on the device).
+% all cells.  cellState carries the handle.  obs holds Vcell and the pre-step
+% electrode averages of OB_step.m:226-228 (negSOC, posSOC, cellSOC); the other
+% observables of OB_step.m:289-356 stay on the device (runMPC.m reads none of them).
   if nargin < 3 || isempty(cellState) || ~isfield(cellState, 'initialized') || ~cellState.initialized
     if nargin < 5 || ~isfield(initCfg, 'SOC0')
       error('First call requires initCfg.SOC0 (in %).');
@@ -13,14 +14,19 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
     n = numel(initCfg.SOC0);
     cfg = S.mpc.mpcekf_cfg;
     cfg.SigmaV = S.kf.SigmaV;  cfg.SigmaW = S.kf.SigmaW;  cfg.SigmaX0 = S.kf.SigmaX0;
-    cfg.flags = int32(1);                                  % MPCEKF_CF_BOUNDS: boundzk too
+    cfg.flags = 1;                                         % MPCEKF_CF_BOUNDS: boundzk too
     if strcmp(S.kf.method, 'MB'), cfg.method = 1; end
     h = mpcekf_mex('create', mpcekf_rom_struct(ROM), cfg, S.device, n);
     mpcekf_session('set', 'h', h);
     mpcekf_mex('init', h, reshape(initCfg.SOC0, 1, n), Tc .* ones(1, n));
-    cellState = struct('initialized', true, 'h', h, 'n', n, 'Ts', ROM.xraData.Tsamp);
+    fn = ROM.cellData.function.neg;
+    cellState = struct('initialized', true, 'h', h, 'n', n, 'Ts', ROM.xraData.Tsamp, ...
+                       'theta0n', fn.theta0(), 'theta100n', fn.theta100());
   end
   n = cellState.n;
+  st = mpcekf_mex('get_state', cellState.h);                 % pre-update averages (OB_step.m:226-228)
+  obs = struct('negSOC', st.scal(1, :), 'posSOC', st.scal(2, :));
+  obs.cellSOC = (obs.negSOC - cellState.theta0n) / (cellState.theta100n - cellState.theta0n);
   Vcell = mpcekf_mex('plant', cellState.h, reshape(Iapp .* ones(1, n), 1, n), reshape(Tc .* ones(1, n), 1, n));
-  obs = struct('Vcell', Vcell);
+  obs.Vcell = Vcell;
 end

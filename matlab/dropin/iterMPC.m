@@ -1,17 +1,29 @@
 function [uk, mpcData] = iterMPC(xk, cellState, mpcData)
-% Drop-in for iterMPC.m:1 over the MI355X library (mpcekf_mpc_step): the state is the
-% xhat of cellState.MPC.lin (EKFmatsHandler's, which runMPC.m:101 passes as xk), uk_1
-% and the Hildreth warm start live in the context.  mpcData.cost.nexec(k) is filled
-% when runMPC.m has set mpcData.k.
+% Drop-in for iterMPC.m:1 over the MI355X library (mpcekf_mpc_step_ex): the linearisation
+% is cellState.MPC.lin (EKFmatsHandler's records), with its xhat rows replaced by the
+% caller's xk (6 x ncells, the state iterMPC.m:29 augments); uk_1 and the Hildreth warm
+% start live in the context.  When runMPC.m has set mpcData.k, row k of mpcData.cost
+% (iterMPC.m:89-95: t, J_uncon, J_final, norm_DU, viol, nexec) is filled, one column
+% per cell.
   S = mpcekf_session('get');
   lin = cellState.MPC.lin;
   n = size(lin, 2);
+  if ~isempty(xk)
+    lin(30:35, :) = reshape(xk, 6, []) .* ones(1, n);        % MPCEKF_LIN_XHAT
+  end
   % iterMPC.m:53-60 stability analysis (before the solve: it uses this step's uk_1)
   [mpcData.poles, mpcData.sv] = mpcekf_mex('mpcdiag', S.h, lin, []);
-  [uk, nexec] = mpcekf_mex('mpc', S.h, lin, reshape(mpcData.SOCk_1 .* ones(1, n), 1, n));
+  [uk, nexec, J_unc, J_fin, ndu, nviol] = mpcekf_mex('mpc', S.h, lin, reshape(mpcData.SOCk_1 .* ones(1, n), 1, n));
   mpcData.uk_1 = uk;
+  mpcData.nexec = double(nexec);
   if isfield(mpcData, 'cost') && isfield(mpcData, 'k')
-    mpcData.cost.nexec(mpcData.k) = double(nexec(1));
+    k = mpcData.k;
+    if isfield(mpcData, 'Ts'), Ts = mpcData.Ts; else, Ts = cellState.Ts; end
+    mpcData.cost.t(k, 1) = (k - 1) * Ts;
+    mpcData.cost.J_uncon(k, 1:n) = J_unc;
+    mpcData.cost.J_final(k, 1:n) = J_fin;
+    mpcData.cost.norm_DU(k, 1:n) = ndu;
+    mpcData.cost.viol(k, 1:n) = double(nviol);
+    mpcData.cost.nexec(k, 1:n) = double(nexec);
   end
-  xk = []; %#ok<NASGU> (the library uses the linearisation record's xhat)
 end

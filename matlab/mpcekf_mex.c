@@ -16,18 +16,23 @@
  *   v                 = mpcekf_mex('plant', h, iapp, tc)               mpcekf_plant_step   (OB_step.m:1)
  *   [zk,zbk,xm,xg]    = mpcekf_mex('ekf', h, vk, ik, tk)               mpcekf_ekf_step     (iterEKF.m:30)
  *   lin               = mpcekf_mex('linearize', h, zk, xm, xg, tk)     mpcekf_linearize    (EKFmatsHandler.m:1)
- *   [uk,nexec]        = mpcekf_mex('mpc', h, lin, soc_k1)              mpcekf_mpc_step     (iterMPC.m:1)
+ *   [uk,nexec,J_uncon,J_final,norm_DU,viol] = mpcekf_mex('mpc', h, lin, soc_k1)
+ *                                                                      mpcekf_mpc_step_ex  (iterMPC.m:1,89-95)
  *   [poles,sv]        = mpcekf_mex('mpcdiag', h, lin, uk_1)            mpcekf_mpc_diag     (iterMPC.m:53-60)
  *                       uk_1: [] for the context's; poles complex 7 x ncells, sv 7 x ncells
  *   [DU,lambda,nexec] = mpcekf_mex('hildreth', E, F, M, gamma, lambda0, maxIter)   (hildreth.m:1)
  *   [Phi,G]           = mpcekf_mex('predmat', a, C, D, Np, Nc)         (predMat.m:1, A = diag(a), B = 1)
  *   st                = mpcekf_mex('get_state', h)    /  mpcekf_mex('set_state', h, st)
+ *                       st.bigX, ekf, scal, lambda (double), warn, status (int32 1 x ncells),
+ *                       and st.mb (42 x ncells) on a model-blend ('MB') context
  *                       mpcekf_mex('graph', h, enable)                 mpcekf_set_graph (replay repeated step calls)
  * Per-cell vectors are 1 x ncells or ncells x 1; zk / zbk are (nz+2) x ncells, xm / xg
  * 4 x ncells (xm: 0-based model index t*nZ+z), lin 35 x ncells -- MATLAB's column-major
  * k x ncells is the library's cell-major [ncells][k], so no copy is made for them.
  * Arrays the library reads row-major (the ROM's A/C/D, the electrode tables, hildreth's
  * E and M) are transposed here from MATLAB's column-major order.
+ * Scalars (device, ncells, nsteps, cfg fields ...) may be of any real numeric class.
+ * Only the first max(nargout, 1) outputs are returned.
  * Library failures raise a MATLAB error with mpcekf_last_error(); per-cell soft
  * failures stay in the status word (get_state), as in the C-ABI.
  */
@@ -42,14 +47,40 @@ static void chk(int rc) {
   if (rc != MPCEKF_OK) mexErrMsgIdAndTxt("mpcekf:lib", "mpcekf error %d: %s", rc, mpcekf_last_error());
 }
 
-static mpcekf_ctx *handle(const mxArray *a) {
-  if (!mxIsUint64(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("mpcekf:arg", "expected a uint64 handle");
-  return (mpcekf_ctx *)(uintptr_t)(*(uint64_t *)mxGetData(a));
+/* Live contexts of this MEX session: a handle is checked against them before use, so a
+ * stale or made-up uint64 raises a MATLAB error instead of crashing MATLAB. */
+#define MAXCTX 64
+static mpcekf_ctx *g_live[MAXCTX];
+
+static void track(mpcekf_ctx *h, int add) {
+  for (int i = 0; i < MAXCTX; ++i)
+    if (add ? g_live[i] == NULL : g_live[i] == h) {
+      g_live[i] = add ? h : NULL;
+      return;
+    }
 }
 
+static mpcekf_ctx *handle(const mxArray *a) {
+  if (!mxIsUint64(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("mpcekf:arg", "expected a uint64 handle");
+  mpcekf_ctx *h = (mpcekf_ctx *)(uintptr_t)(*(uint64_t *)mxGetData(a));
+  for (int i = 0; i < MAXCTX; ++i)
+    if (h && g_live[i] == h) return h;
+  mexErrMsgIdAndTxt("mpcekf:arg", "not a live mpcekf context handle (destroyed, or not from 'create')");
+  return NULL;
+}
+
+/* a real scalar of any numeric class (double, int32, ...), as MATLAB code passes them */
 static double scalar(const mxArray *a, const char *what) {
-  if (!a || !mxIsDouble(a) || mxGetNumberOfElements(a) != 1) mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected a double scalar", what);
+  if (!a || !mxIsNumeric(a) || mxIsComplex(a) || mxGetNumberOfElements(a) != 1)
+    mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected a real numeric scalar", what);
   return mxGetScalar(a);
+}
+
+/* an int32 array of exactly n elements (warn / status / xm) */
+static int32_t *ivec(const mxArray *a, size_t n, const char *what) {
+  if (!a || !mxIsInt32(a) || mxIsComplex(a) || mxGetNumberOfElements(a) != n)
+    mexErrMsgIdAndTxt("mpcekf:arg", "%s: expected %zu int32 values", what, n);
+  return (int32_t *)mxGetData(a);
 }
 
 static const double *dvec(const mxArray *a, size_t n, const char *what) {
@@ -85,7 +116,7 @@ static double *rowmajor(const mxArray *a, const char *what) {
 
 static const mxArray *field(const mxArray *s, const char *name) {
   const mxArray *f = mxGetField(s, 0, name);
-  if (!f) mexErrMsgIdAndTxt("mpcekf:arg", "ROM struct: missing field %s", name);
+  if (!f) mexErrMsgIdAndTxt("mpcekf:arg", "struct: missing field %s", name);
   return f;
 }
 
@@ -145,9 +176,11 @@ static void cfg_from_struct(const mxArray *s, mpcekf_config *c) {
 #define GETD(f) if (mxGetField(s, 0, #f)) c->f = scalar(mxGetField(s, 0, #f), #f)
   GETI(Np); GETI(Nc); GETD(target_soc); GETD(Crate); GETD(u_max); GETD(du_min); GETD(du_max); GETD(v_min);
   GETD(v_max); GETD(phise_min); GETD(z_max); GETD(z_tol); GETI(use_current); GETI(use_voltage); GETI(use_eta);
-  GETI(max_hild); GETD(hild_tol); GETD(SigmaV); GETD(SigmaW); GETI(max_warn); GETI(flags);
+  GETI(max_hild); GETD(hild_tol); GETD(SigmaV); GETD(SigmaW); GETI(max_warn); GETI(flags); GETI(method);
 #undef GETI
 #undef GETD
+  if (c->method != MPCEKF_METHOD_OB && c->method != MPCEKF_METHOD_MB)
+    mexErrMsgIdAndTxt("mpcekf:arg", "cfg.method: %d (expected 0 = 'OB' or 1 = 'MB', initKF.m:44-49)", (int)c->method);
   const mxArray *sx = mxGetField(s, 0, "SigmaX0");
   if (sx) {
     const double *v = dvec(sx, 6, "SigmaX0 (diagonal, 6)");
@@ -162,7 +195,14 @@ static const double *opt_vec(const mxArray *a, size_t n, const char *what) {
   return (!a || mxIsEmpty(a)) ? NULL : dvec(a, n, what);
 }
 
-void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
+/* Every command builds its outputs in plhs[0..MAXOUT); mexFunction hands MATLAB the
+ * first max(nlhs, 1) of them (MATLAB's plhs has room for no more) and frees the rest. */
+#define MAXOUT 8
+static void need(int nrhs, int k, const char *usage) {
+  if (nrhs < k) mexErrMsgIdAndTxt("mpcekf:arg", "usage: mpcekf_mex(%s)", usage);
+}
+
+static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   char cmd[32];
   if (nrhs < 1 || mxGetString(prhs[0], cmd, sizeof cmd)) mexErrMsgIdAndTxt("mpcekf:arg", "first argument: command");
   if (!strcmp(cmd, "create")) {
@@ -171,8 +211,12 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     mpcekf_config c;
     rom_from_struct(prhs[1], &r);
     cfg_from_struct(prhs[2], &c);
+    int free_slot = 0;
+    for (int i = 0; i < MAXCTX; ++i) free_slot = free_slot || g_live[i] == NULL;
+    if (!free_slot) mexErrMsgIdAndTxt("mpcekf:arg", "create: %d contexts are live; destroy one first", MAXCTX);
     mpcekf_ctx *h = NULL;
     chk(mpcekf_ctx_create(&r, &c, (int)scalar(prhs[3], "device"), (int64_t)scalar(prhs[4], "ncells"), &h));
+    track(h, 1);
     plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
     *(uint64_t *)mxGetData(plhs[0]) = (uint64_t)(uintptr_t)h;
     return; /* the row-major copies are mxMalloc'd: MATLAB frees them (the context copied the ROM) */
@@ -180,6 +224,10 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   if (!strcmp(cmd, "hildreth")) {
     if (nrhs != 7) mexErrMsgIdAndTxt("mpcekf:arg", "hildreth(E, F, M, gamma, lambda0, maxIter)");
     const size_t Nc = mxGetM(prhs[1]), nC = mxGetM(prhs[3]);
+    if (mxGetNumberOfDimensions(prhs[1]) != 2 || mxGetN(prhs[1]) != Nc)
+      mexErrMsgIdAndTxt("mpcekf:arg", "hildreth: E must be Nc x Nc");
+    if (mxGetNumberOfDimensions(prhs[3]) != 2 || mxGetN(prhs[3]) != Nc)
+      mexErrMsgIdAndTxt("mpcekf:arg", "hildreth: M must be nC x Nc (Nc = %zu)", Nc);
     double *E = rowmajor(prhs[1], "E"), *M = rowmajor(prhs[3], "M");
     const double *F = dvec(prhs[2], Nc, "F"), *g = dvec(prhs[4], nC, "gamma");
     plhs[1] = dmat(nC, 1);
@@ -205,6 +253,11 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     }
     return;
   }
+  static const char *const with_handle[] = {"destroy", "init", "step", "plant", "ekf", "linearize", "mpc",
+                                            "graph", "mpcdiag", "get_state", "set_state"};
+  int known = 0;
+  for (size_t i = 0; i < sizeof with_handle / sizeof *with_handle; ++i) known = known || !strcmp(cmd, with_handle[i]);
+  if (!known) mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
   if (nrhs < 2) mexErrMsgIdAndTxt("mpcekf:arg", "%s: missing handle", cmd);
   mpcekf_ctx *h = handle(prhs[1]);
   int64_t n = 0;
@@ -212,21 +265,29 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   chk(mpcekf_ctx_info(h, &n, &NM, &nz, &ncon));
   const size_t nc = (size_t)n, nzz = (size_t)nz + 2;
   if (!strcmp(cmd, "destroy")) {
+    track(h, 0);
     chk(mpcekf_ctx_destroy(h));
   } else if (!strcmp(cmd, "init")) {
+    need(nrhs, 4, "'init', h, soc0_pct, tc_degC");
     chk(mpcekf_init_cells(h, dvec(prhs[2], nc, "soc0"), dvec(prhs[3], nc, "tc")));
   } else if (!strcmp(cmd, "step")) {
-    const int32_t ns = (int32_t)scalar(prhs[2], "nsteps");
+    need(nrhs, 3, "'step', h, nsteps[, tc]");
+    const double nsd = scalar(prhs[2], "nsteps");
+    if (!(nsd >= 0 && nsd <= 2147483647.0) || nsd != (double)(int32_t)nsd)
+      mexErrMsgIdAndTxt("mpcekf:arg", "nsteps: expected a non-negative integer");
+    const int32_t ns = (int32_t)nsd;
     const double *tc = nrhs > 3 ? opt_vec(prhs[3], nc * (size_t)ns, "tc (ncells x nsteps)") : NULL;
     for (int i = 0; i < 4; ++i) plhs[i] = dmat(nc, (size_t)ns);
     plhs[4] = imat(nc, (size_t)ns);
     chk(mpcekf_step(h, ns, tc, mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]), mxGetDoubles(plhs[2]),
                     mxGetDoubles(plhs[3]), (int32_t *)mxGetData(plhs[4]), 0));
   } else if (!strcmp(cmd, "plant")) {
+    need(nrhs, 3, "'plant', h, iapp[, tc]");
     plhs[0] = dmat(1, nc);
     chk(mpcekf_plant_step(h, dvec(prhs[2], nc, "iapp"), nrhs > 3 ? opt_vec(prhs[3], nc, "tc") : NULL,
                           mxGetDoubles(plhs[0])));
   } else if (!strcmp(cmd, "ekf")) {
+    need(nrhs, 4, "'ekf', h, vk, ik[, tk]");
     plhs[0] = dmat(nzz, nc);
     plhs[1] = dmat(nzz, nc);
     plhs[2] = imat(4, nc);
@@ -235,51 +296,76 @@ void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
                         nrhs > 4 ? opt_vec(prhs[4], nc, "tk") : NULL, mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]),
                         (int32_t *)mxGetData(plhs[2]), mxGetDoubles(plhs[3])));
   } else if (!strcmp(cmd, "linearize")) {
-    if (!mxIsInt32(prhs[3]) || mxGetNumberOfElements(prhs[3]) != 4 * nc) mexErrMsgIdAndTxt("mpcekf:arg", "xm: int32 4 x ncells");
+    need(nrhs, 5, "'linearize', h, zk, xm, xg[, tk]");
     plhs[0] = dmat(MPCEKF_LIN_SIZE, nc);
-    chk(mpcekf_linearize(h, dvec(prhs[2], nzz * nc, "zk"), (const int32_t *)mxGetData(prhs[3]),
+    chk(mpcekf_linearize(h, dvec(prhs[2], nzz * nc, "zk"), ivec(prhs[3], 4 * nc, "xm (4 x ncells)"),
                          dvec(prhs[4], 4 * nc, "xg"), nrhs > 5 ? opt_vec(prhs[5], nc, "tk") : NULL,
                          mxGetDoubles(plhs[0])));
   } else if (!strcmp(cmd, "mpc")) {
-    plhs[0] = dmat(1, nc);
-    plhs[1] = imat(1, nc);
-    chk(mpcekf_mpc_step(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
-                        mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1])));
+    need(nrhs, 4, "'mpc', h, lin, soc_k1");
+    /* [uk, nexec, J_uncon, J_final, norm_DU, viol]: iterMPC.m's command and its
+       mpcData.cost row (iterMPC.m:89-95), 1 x ncells each */
+    for (int i = 0; i < 6; ++i) plhs[i] = (i == 1 || i == 5) ? imat(1, nc) : dmat(1, nc);
+    chk(mpcekf_mpc_step_ex(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
+                           mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1]), mxGetDoubles(plhs[2]),
+                           mxGetDoubles(plhs[3]), mxGetDoubles(plhs[4]), (int32_t *)mxGetData(plhs[5])));
   } else if (!strcmp(cmd, "graph")) {
     if (nrhs < 3) mexErrMsgIdAndTxt("mpcekf:arg", "graph: enable flag");
     chk(mpcekf_set_graph(h, (int32_t)(mxGetScalar(prhs[2]) != 0.0)));
   } else if (!strcmp(cmd, "mpcdiag")) {
+    need(nrhs, 3, "'mpcdiag', h, lin[, uk_1]");
     plhs[0] = mxCreateDoubleMatrix(7, (mwSize)nc, mxCOMPLEX);  /* interleaved (re, im): [ncells][7][2] */
     plhs[1] = dmat(7, nc);
     chk(mpcekf_mpc_diag(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), nrhs > 3 ? opt_vec(prhs[3], nc, "uk_1") : NULL,
                         (double *)mxGetComplexDoubles(plhs[0]), mxGetDoubles(plhs[1])));
   } else if (!strcmp(cmd, "get_state") || !strcmp(cmd, "set_state")) {
-    const char *f[] = {"bigX", "ekf", "scal", "lambda", "warn", "status"};
-    const size_t rows[] = {(size_t)NM * 6, (size_t)NM * 20, MPCEKF_NSCAL, (size_t)ncon, 1, 1};
+    /* the model-blend EKF state (xhat, SigmaX 6 x 6) is part of an MB context's checkpoint */
+    mpcekf_config cc;
+    chk(mpcekf_ctx_config(h, &cc));
+    const int nf = cc.method == MPCEKF_METHOD_MB ? 7 : 6;
+    const char *f[] = {"bigX", "ekf", "scal", "lambda", "warn", "status", "mb"};
+    const size_t rows[] = {(size_t)NM * 6, (size_t)NM * 20, MPCEKF_NSCAL, (size_t)ncon, 1, 1, MPCEKF_MB_SIZE};
     mpcekf_state st;
-    memset(&st, 0, sizeof st); /* mb (the MB EKF state) is not exchanged here: NULL */
+    memset(&st, 0, sizeof st);
     if (cmd[0] == 'g') {
-      plhs[0] = mxCreateStructMatrix(1, 1, 6, f);
-      mxArray *a[6];
-      for (int i = 0; i < 6; ++i) {
-        a[i] = i < 4 ? dmat(rows[i], nc) : imat(1, nc);
+      plhs[0] = mxCreateStructMatrix(1, 1, nf, f);
+      mxArray *a[7];
+      for (int i = 0; i < nf; ++i) {
+        a[i] = (i == 4 || i == 5) ? imat(1, nc) : dmat(rows[i], nc);
         mxSetField(plhs[0], 0, f[i], a[i]);
       }
       st.bigX = mxGetDoubles(a[0]); st.ekf = mxGetDoubles(a[1]); st.scal = mxGetDoubles(a[2]);
       st.lambda = mxGetDoubles(a[3]); st.warn = (int32_t *)mxGetData(a[4]); st.status = (int32_t *)mxGetData(a[5]);
+      if (nf == 7) st.mb = mxGetDoubles(a[6]);
       chk(mpcekf_get_state(h, &st));
     } else {
+      if (nrhs < 3 || !mxIsStruct(prhs[2])) mexErrMsgIdAndTxt("mpcekf:arg", "set_state(h, st): st must be a struct");
       const mxArray *s = prhs[2];
       st.bigX = (double *)dvec(field(s, "bigX"), rows[0] * nc, "bigX");
       st.ekf = (double *)dvec(field(s, "ekf"), rows[1] * nc, "ekf");
       st.scal = (double *)dvec(field(s, "scal"), rows[2] * nc, "scal");
       st.lambda = (double *)dvec(field(s, "lambda"), rows[3] * nc, "lambda");
-      st.warn = (int32_t *)mxGetData(field(s, "warn"));
-      st.status = (int32_t *)mxGetData(field(s, "status"));
+      st.warn = ivec(field(s, "warn"), nc, "warn");
+      st.status = ivec(field(s, "status"), nc, "status");
+      if (nf == 7) st.mb = (double *)dvec(field(s, "mb"), rows[6] * nc, "mb (MB context)");
       chk(mpcekf_set_state(h, &st));
     }
   } else {
     mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
   }
-  (void)nlhs;
+}
+
+void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
+  mxArray *out[MAXOUT] = {0};
+  gateway(out, nrhs, prhs);
+  const int keep = nlhs < 1 ? 1 : nlhs;
+  if (keep > MAXOUT) mexErrMsgIdAndTxt("mpcekf:arg", "too many outputs");
+  for (int i = 0; i < MAXOUT; ++i) {
+    if (i < keep) {
+      if (i > 0 && !out[i]) mexErrMsgIdAndTxt("mpcekf:arg", "output %d is not defined for this command", i + 1);
+      plhs[i] = out[i];
+    } else if (out[i]) {
+      mxDestroyArray(out[i]);
+    }
+  }
 }

@@ -70,8 +70,8 @@ class MpcekfError(RuntimeError):
 
 EXPORTS = [
     "mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_ctx_create",
-    "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_init_cells", "mpcekf_step", "mpcekf_step_ex", "mpcekf_get_zk",
-    "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_predmat",
+    "mpcekf_ctx_destroy", "mpcekf_ctx_info", "mpcekf_ctx_config", "mpcekf_init_cells", "mpcekf_step", "mpcekf_step_ex", "mpcekf_get_zk",
+    "mpcekf_plant_step", "mpcekf_ekf_step", "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_mpc_step_ex", "mpcekf_predmat",
     "mpcekf_constraints", "mpcekf_hildreth", "mpcekf_get_state", "mpcekf_set_state",
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
     "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag", "mpcekf_set_graph",
@@ -97,6 +97,7 @@ def load():
     L.mpcekf_ctx_create.argtypes = [C.POINTER(Rom), C.POINTER(Config), C.c_int, C.c_int64, C.POINTER(vp)]
     L.mpcekf_ctx_destroy.argtypes = [vp]
     L.mpcekf_ctx_info.argtypes = [vp, C.POINTER(C.c_int64), _ip, _ip, _ip]
+    L.mpcekf_ctx_config.argtypes = [vp, C.POINTER(Config)]
     L.mpcekf_init_cells.argtypes = [vp, _dp, _dp]
     L.mpcekf_step.argtypes = [vp, C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int32]
     L.mpcekf_step_ex.argtypes = [vp, C.c_int32, vp, C.POINTER(Traj), C.c_int32]
@@ -105,6 +106,7 @@ def load():
     L.mpcekf_ekf_step.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _ip, _dp]
     L.mpcekf_linearize.argtypes = [vp, _dp, _ip, _dp, _dp, _dp]
     L.mpcekf_mpc_step.argtypes = [vp, _dp, _dp, _dp, _ip]
+    L.mpcekf_mpc_step_ex.argtypes = [vp, _dp, _dp, _dp, _ip, _dp, _dp, _dp, _ip]
     L.mpcekf_predmat.argtypes = [C.c_int, C.c_int64, C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp]
     L.mpcekf_constraints.argtypes = [C.c_int, C.POINTER(Config), C.c_double, C.c_int64, _dp, _dp, _dp,
                                      _dp, _dp]

@@ -559,6 +559,12 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   return MPCEKF_OK;
 }
 
+int mpcekf_ctx_config(const mpcekf_ctx *X, mpcekf_config *cfg) {
+  if (!X || !cfg) return fail(MPCEKF_E_ARG, "ctx_config: null argument");
+  *cfg = X->cfg;
+  return MPCEKF_OK;
+}
+
 int mpcekf_ctx_info(const mpcekf_ctx *X, int64_t *ncells, int32_t *nmodels, int32_t *nz, int32_t *ncon) {
   if (!X) return fail(MPCEKF_E_ARG, "null ctx");
   if (ncells) *ncells = X->n;
@@ -988,14 +994,20 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
 }
 
 int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec) {
+  return mpcekf_mpc_step_ex(X, lin, soc_k1, uk, nexec, nullptr, nullptr, nullptr, nullptr);
+}
+
+int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!lin || !soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
   size_t n = (size_t)X->n;
-  if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + 2 * n) * 8 + n * 4 + 2048))) return rc;
+  if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + 5 * n) * 8 + 2 * n * 4 + 4096))) return rc;
   Slab sl{(char *)X->d_tmp};
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *ds = sl.take<double>(n), *du = sl.take<double>(n);
-  int *dn = sl.take<int>(n);
+  double *dju = sl.take<double>(n), *djf = sl.take<double>(n), *dnd = sl.take<double>(n);
+  int *dn = sl.take<int>(n), *dv = sl.take<int>(n);
   HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, X->stream));
   KIO io{};
@@ -1004,6 +1016,11 @@ int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, doub
   io.soc_k1_in = ds;
   io.uk_out = du;
   io.nexec = dn;
+  // iterMPC.m:89-95's cost log (mpcData.cost) of this call
+  io.junc_out = J_unc ? dju : nullptr;
+  io.jfin_out = J_fin ? djf : nullptr;
+  io.normdu_out = norm_du ? dnd : nullptr;
+  io.nviol_out = nviol ? dv : nullptr;
   if (X->wide) {
     if ((rc = lerr(launch_mpc_wide(X->k, X->s, io, X->w, X->stream), "mpc_wide"))) return rc;
     if ((rc = lerr(launch_hild_wide(X->k, X->s, io, X->w, X->stream), "hild_wide"))) return rc;
@@ -1013,6 +1030,10 @@ int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, doub
   }
   HIPCHK(hipMemcpyAsync(uk, du, n * 8, hipMemcpyDeviceToHost, X->stream));
   if (nexec) HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, X->stream));
+  if (J_unc) HIPCHK(hipMemcpyAsync(J_unc, dju, n * 8, hipMemcpyDeviceToHost, X->stream));
+  if (J_fin) HIPCHK(hipMemcpyAsync(J_fin, djf, n * 8, hipMemcpyDeviceToHost, X->stream));
+  if (norm_du) HIPCHK(hipMemcpyAsync(norm_du, dnd, n * 8, hipMemcpyDeviceToHost, X->stream));
+  if (nviol) HIPCHK(hipMemcpyAsync(nviol, dv, n * 4, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   return MPCEKF_OK;
 }

@@ -149,13 +149,13 @@ class Context:
         diagnostics x (x_store), zk / zbk (zkEst / zkBound), J_unc, J_fin, norm_du, nviol
         (mpcData.cost), poles ([.., 7, 2] re/im of eig(CL)) and sv (svd(CL)), the stability
         diagnostics of iterMPC.m:53-60 (returned as complex [nsteps, ncells, 7] for poles).
-        ``tc`` [nsteps, ncells] (or broadcastable): the TC of each step
-        in degC (runMPC.m:85-92); None keeps every cell's current temperature."""
+        ``tc``: the TC of each step in degC (runMPC.m:85-92), anything numpy broadcasts to
+        [nsteps, ncells]: a scalar, a per-cell vector [ncells], a per-step column [nsteps, 1]
+        or the full array; None keeps every cell's current temperature."""
         n = self.n
         tcs = None
         if tc is not None:
-            tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc, dtype=np.float64).reshape(
-                (nsteps, -1) if np.ndim(tc) else (1, 1)), (nsteps, n)))
+            tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc, dtype=np.float64), (nsteps, n)))
         out = {}
         tr = _lib.Traj()
         for k in outputs:
@@ -255,14 +255,22 @@ class Context:
         check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin)))
         return lin
 
-    def iterMPC(self, lin, SOCk_1):
-        """[uk, mpcData] = iterMPC(xk, cellState, mpcData)  (iterMPC.m:1). Returns uk, nexec."""
+    def iterMPC(self, lin, SOCk_1, cost=False):
+        """[uk, mpcData] = iterMPC(xk, cellState, mpcData)  (iterMPC.m:1). Returns uk, nexec;
+        with cost=True also this call's mpcData.cost row (iterMPC.m:89-95) as a dict of
+        J_uncon, J_final, norm_DU, viol, nexec per cell."""
         lin = np.ascontiguousarray(lin, dtype=np.float64)
         s = self._vec(SOCk_1)
         uk = np.empty(self.n)
         ne = np.empty(self.n, dtype=np.int32)
-        check(self.L.mpcekf_mpc_step(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne)))
-        return uk, ne
+        if not cost:
+            check(self.L.mpcekf_mpc_step(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne)))
+            return uk, ne
+        ju, jf, nd = np.empty(self.n), np.empty(self.n), np.empty(self.n)
+        nv = np.empty(self.n, dtype=np.int32)
+        check(self.L.mpcekf_mpc_step_ex(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne), dptr(ju), dptr(jf),
+                                        dptr(nd), iptr(nv)))
+        return uk, ne, dict(J_uncon=ju, J_final=jf, norm_DU=nd, viol=nv, nexec=ne)
 
     def mpc_diag(self, lin, uk_1=None):
         """mpcData.poles / mpcData.sv of the iterMPC that iterMPC(lin, ..) would run

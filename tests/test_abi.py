@@ -84,17 +84,17 @@ def test_matlab_dropin_wrappers_keep_reference_signatures():
 
 
 def test_mex_gateway_calls_only_declared_entry_points():
-    """matlab/mpcekf_mex.c (built on a MATLAB machine, not here) binds the C-ABI: every
-    mpcekf_* it calls is declared in include/mpcekf.h, and every MATLAB-facing stage
-    entry point is reachable from it."""
+    """matlab/mpcekf_mex.c binds the C-ABI: every mpcekf_* it calls is declared in
+    include/mpcekf.h, and every MATLAB-facing stage entry point is reachable from it
+    (tests/test_mex_gateway.py drives it through the MEX API test shim)."""
     import re
     src = open(os.path.join(ROOT, "matlab", "mpcekf_mex.c")).read()
     src_code = re.sub(r"/\*.*?\*/", "", src, flags=re.S)  # comments name MATLAB helpers too
     called = set(re.findall(r"\b(mpcekf_[a-z_]+)\s*\(", src_code)) - {"mpcekf_mex"}
     assert called <= set(declared_symbols()), called - set(declared_symbols())
     for sym in ("mpcekf_ctx_create", "mpcekf_init_cells", "mpcekf_step", "mpcekf_plant_step", "mpcekf_ekf_step",
-                "mpcekf_linearize", "mpcekf_mpc_step", "mpcekf_hildreth", "mpcekf_predmat", "mpcekf_get_state",
-                "mpcekf_set_state", "mpcekf_ctx_destroy", "mpcekf_mpc_diag"):
+                "mpcekf_linearize", "mpcekf_mpc_step_ex", "mpcekf_hildreth", "mpcekf_predmat", "mpcekf_get_state",
+                "mpcekf_set_state", "mpcekf_ctx_destroy", "mpcekf_mpc_diag", "mpcekf_ctx_config"):
         assert sym in called, sym
     drop = " ".join(open(os.path.join(ROOT, "matlab", "dropin", f)).read()
                     for f in os.listdir(os.path.join(ROOT, "matlab", "dropin")))

@@ -17,20 +17,40 @@ from collections import defaultdict
 # kernel (exact name prefix) -> bench stage; a stage's per-step figure is the sum of
 # its kernels' per-dispatch averages (each launches once per step)
 KERNELS = {"k_plant(": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild_slow(": "hild",
-           "k_bounds<": "bounds", "k_bulk(": "bulk"}
+           "k_bounds<": "bounds", "k_bulk(": "bulk",
+           # wide horizons (mpcekf_wide.hip): bench.py's "cell" slot times k_cell + k_mpc_wide,
+           # its "hild" slot the whole hildreth.m pipeline (prep, binning, sweeps, exact path, finish)
+           "k_mpc_wide<": "cell", "k_hild_prep<": "hild", "k_hild_bin<": "hild", "k_hild_sort(": "hild",
+           "k_hild_wide<": "hild", "k_hild_wide_slow<": "hild", "k_mpc_wide_finish<": "hild"}
 
 
-def read_counter(d, name):
+def bench_build_id(base):
+    """The build id the profiled bench printed (its JSON line's checks.build_id): the
+    library that ran on the box, which the local tree may since have changed."""
+    for path in sorted(glob.glob(os.path.join(base, "*.log")) + glob.glob(os.path.join(base, "*.json"))):
+        try:
+            with open(path) as f:
+                for line in f:
+                    if line.startswith("{") and '"build_id"' in line:
+                        return json.loads(line)["checks"]["build_id"]
+        except (OSError, ValueError, KeyError):
+            continue
+    return None
+
+
+def read_counter(d, name, by_kernel=False):
     vals = defaultdict(list)
     for path in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         with open(path) as f:
             for row in csv.DictReader(f):
                 if row.get("Counter_Name") != name:
                     continue
-                kn = row.get("Kernel_Name", "")
+                kn = row.get("Kernel_Name", "").replace("(anonymous namespace)::", "")
                 for k in KERNELS:
                     if ("mk::" + k) in kn or (" " + k) in kn or kn.startswith(k):
                         vals[k].append(float(row["Counter_Value"]))
+    if by_kernel:
+        return {k.rstrip("(<"): sum(v) / len(v) for k, v in vals.items() if v}
     stage = defaultdict(float)
     for k, v in vals.items():
         if v:
@@ -50,15 +70,21 @@ def main():
     a = ap.parse_args()
     base = a.base
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-    L = importlib.import_module("mpc-ekf4fastcharge_amd._lib").load()
+    bid = bench_build_id(base)
+    if bid is None:
+        bid = importlib.import_module("mpc-ekf4fastcharge_amd._lib").load().mpcekf_build_id().decode()
     fetch = read_counter(os.path.join(base, "fetch"), "FETCH_SIZE")
     write = read_counter(os.path.join(base, "write"), "WRITE_SIZE")
-    out = {"unit": "bytes per launch", "build_id": L.mpcekf_build_id().decode(), "cells": a.cells, "Np": a.np,
+    out = {"unit": "bytes per launch", "build_id": bid, "cells": a.cells, "Np": a.np,
            "bounds": a.bounds, "steps": a.steps, "fetch_kib_raw": fetch, "write_kib_raw": write,
            "correction": "reads x2 (gfx950 FETCH_SIZE halves 16-B/lane streaming reads)",
            "per_launch_bytes": {}}
     for k in set(fetch) | set(write):
         out["per_launch_bytes"][k] = 2 * fetch.get(k, 0.0) * 1024 + write.get(k, 0.0) * 1024
+    # the same per kernel (a stage's figure is the sum of its kernels')
+    fk = read_counter(os.path.join(base, "fetch"), "FETCH_SIZE", by_kernel=True)
+    wk = read_counter(os.path.join(base, "write"), "WRITE_SIZE", by_kernel=True)
+    out["per_kernel_bytes"] = {k: 2 * fk.get(k, 0.0) * 1024 + wk.get(k, 0.0) * 1024 for k in set(fk) | set(wk)}
     # FP64 work per launch: the SQ_INSTS_VALU_*_F64 counters count wave instructions;
     # x64 lanes (an upper bound when EXEC is partial), FMA = 2 flops
     fd = os.path.join(base, "fp64")
