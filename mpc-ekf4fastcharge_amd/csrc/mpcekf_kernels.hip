@@ -2827,20 +2827,23 @@ __device__ inline void mldiv_rt(int n, const double *E, const double *R, bool ok
     x[i] = t / R[i * n + i];
   }
 }
-// t_i = K_i + M(i,:)*v (orc hild_row_t): Nc <= 2 fma in ascending k; else the pairwise
-// tree over 16 slots, a_0 = fma(M_i0, v_0, K_i), a_k = M_ik v_k, +0 past Nc
+// t_i = K_i + M(i,:)*v (orc hild_row_t): Nc <= 2 fma in ascending k; else the 8-lane
+// form: a_0 = fma(M_i0, v_0, K_i), a_k = M_ik v_k (+0 past Nc), b_k = fma(M_i,k+8, v_k+8, a_k)
+// while k + 8 < Nc, then the pairwise tree over the 8 slots
 __device__ inline double row_t_rt(int Nc, const double *Mi, const double *v, double Ki) {
   if (Nc <= 2) {
     double t = Ki;
     for (int k = 0; k < Nc; ++k) t = __builtin_fma(Mi[k], v[k], t);
     return t;
   }
-  double a[16];
-  a[0] = __builtin_fma(Mi[0], v[0], Ki);
-  for (int k = 1; k < 16; ++k) a[k] = k < Nc ? Mi[k] * v[k] : 0.0;
-  for (int w = 1; w < 16; w *= 2)
-    for (int k = 0; k < 16; k += 2 * w) a[k] = a[k] + a[k + w];
-  return a[0];
+  double b[8];
+  for (int k = 0; k < 8; ++k) {
+    const double a = k == 0 ? __builtin_fma(Mi[0], v[0], Ki) : (k < Nc ? Mi[k] * v[k] : 0.0);
+    b[k] = k + 8 < Nc ? __builtin_fma(Mi[k + 8], v[k + 8], a) : a;
+  }
+  for (int w = 1; w < 8; w *= 2)
+    for (int k = 0; k < 8; k += 2 * w) b[k] = b[k] + b[k + w];
+  return b[0];
 }
 __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, const double *Ei, const double *Fi,
                                                      const double *Mi, const double *gi, double *lami, int maxIter,

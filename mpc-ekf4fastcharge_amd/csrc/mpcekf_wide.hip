@@ -9,7 +9,7 @@
 //                                     gamma arrays live); finishes cells that need no QP
 //   k_hild_prep       lane per cell   hildreth.m:17-29: R = chol(E), X(:,i) = E\M(i,:)'
 //                                     for the 80 distinct rows, K = M*(E\F) + gamma, H_ii
-//   k_hild_wide       16-lane group   hildreth.m:32-42 sweeps: lane k holds v_k and
+//   k_hild_wide       8-lane group    hildreth.m:32-42 sweeps: lane k holds v_k (and v_k+8) and
 //                     per cell        column k of X in registers; row values are summed
 //                                     by a DPP butterfly (oracle hild_row_t)
 //   k_hild_wide_slow  lane per cell   the exact rules (inf/NaN rows, non-finite X or M,
@@ -24,12 +24,6 @@
 
 #include <algorithm>
 
-#ifndef MPCEKF_WIDE_JUNK
-#define MPCEKF_WIDE_JUNK 1
-#endif
-#ifndef MPCEKF_BCAST_OLD_V
-#define MPCEKF_BCAST_OLD_V 1
-#endif
 #ifndef PREP_UNROLL
 #define PREP_UNROLL 1  // k_hild_prep's row loops (rows in flight per wave)
 #endif
@@ -58,15 +52,18 @@ struct W {
   // never reaches a result: every sum they enter starts from +0).
   static constexpr int NX_ROWS = 2 * NC + 3 * NP;
   static constexpr int HPW = NC - 1 + NP;             // one Toeplitz block, NC - 1 leading zeros
-  // k_hild_wide doubles per cell, even: each group's (H_ii, 1/H_ii) pairs are read with
-  // ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
-  // (tools/micro/lds_micro.hip)
-  // padded to 12 (mod 32) doubles: groups 0/1 (and 2/3) of a wave, which share a ds_read_b64
-  // lane half, then put their Nc M entries in disjoint banks
-  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1 - 12 + 31) / 32 * 32 + 12;
+  // k_hild_wide: 8 lanes per cell (lane k holds columns k and k + 8 of X), 16 cells per
+  // 128-thread block.  Doubles per cell, even: each group's (H_ii, 1/H_ii) pairs are read
+  // with ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
+  // (tools/micro/lds_micro.hip); the stride is 4 (mod 32) doubles, so the 8 groups of a
+  // wave reading one offset of their own regions hit 8 disjoint bank pairs (b64) / quads (b128)
+  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1 - 4 + 31) / 32 * 32 + 4;
   static constexpr int ZERO_LDS = (NCON + 1) & ~1;    // the zero row ahead of the groups
-  static constexpr int GROUPS = 16;                   // cells per 256-thread block
+  static constexpr int LANES = 8;                     // lanes per cell
+  static constexpr int BLOCK = 128;
+  static constexpr int GROUPS = BLOCK / LANES;        // cells per block
   static constexpr int JUNK = 64 + NCON;              // per-wave sink of the lanes k != 0's lambda stores
+  static constexpr int WAVES = BLOCK / 64;
 };
 
 // k_hild_sort's bins over last step's sweep count (0 .. maxIter)
@@ -457,7 +454,7 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
 // ---------------------------------------------------------------------------
 // k_hild_bin / k_hild_sort: the fast-path cells listed by predicted sweeps
 // ---------------------------------------------------------------------------
-// k_hild_wide runs 4 cells per wave and a wave lasts as long as its slowest cell; a
+// k_hild_wide runs 8 cells per wave and a wave lasts as long as its slowest cell; a
 // cell's count changes little from one control step to the next, so listing cells by
 // last step's count (longest first) puts cells of like length in one wave.  The order
 // only decides which group runs which cell: each cell's sweeps are the same operations
@@ -507,8 +504,11 @@ __global__ void __launch_bounds__(64) k_hild_sort(const KWide w) {
 
 
 // ---------------------------------------------------------------------------
-// k_hild_wide: hildreth.m:32-42 with a 16-lane group per cell
+// k_hild_wide: hildreth.m:32-42 with an 8-lane group per cell
 // ---------------------------------------------------------------------------
+// A 16-lane DPP row holds two cells (lanes 0-7 and 8-15); every DPP pattern below stays
+// inside its 8-lane group.  64-bit DPP exists only for row_newbcast, so a double moves as
+// two v_mov_b32_dpp.
 template <int CTRL>
 __device__ __forceinline__ double dpp64(double v) {
   const long long b = __double_as_longlong(v);
@@ -516,16 +516,42 @@ __device__ __forceinline__ double dpp64(double v) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
-// Sum over the 16 lanes of a DPP row as the pairwise tree of hild_row_t: each level
-// adds the partner's partial sum (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
-// row_mirror); both partners add the same two values, so every lane ends with the
-// same bits.
-__device__ __forceinline__ double tree16(double a) {
+// the DPP move into the lanes of the banks in BANK only; the other lanes keep `old`
+template <int CTRL, int BANK>
+__device__ __forceinline__ double dpp64_into(double old, double v) {
+  const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, 0xF, BANK, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xF, BANK, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+// Sum over the 8 lanes of a group as the pairwise tree of hild_row_t: each level adds the
+// partner's partial sum (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror); both partners
+// add the same two values, so every lane ends with the same bits.
+__device__ __forceinline__ double tree8(double a) {
   a = a + dpp64<0xB1>(a);
   a = a + dpp64<0x4E>(a);
   a = a + dpp64<0x141>(a);
-  a = a + dpp64<0x140>(a);
   return a;
+}
+// lane J's value in every lane of its 8-lane group: quad_perm [J%4 x4] gives each quad its
+// lane J%4, then the quad that holds lane J is copied into the other (row_shr:4 into banks
+// 1 and 3 for J < 4, row_shl:4 into banks 0 and 2 for J >= 4)
+template <int J>
+__device__ __forceinline__ double bcast8(double v) {
+  const double q = dpp64<(J & 3) * 0x55>(v);
+  return J < 4 ? dpp64_into<0x114, 0xA>(q, q) : dpp64_into<0x104, 0x5>(q, q);
+}
+__device__ __forceinline__ double bcast8(double v, int j) {  // j a constant after unrolling
+  switch (j) {
+    case 0: return bcast8<0>(v);
+    case 1: return bcast8<1>(v);
+    case 2: return bcast8<2>(v);
+    case 3: return bcast8<3>(v);
+    case 4: return bcast8<4>(v);
+    case 5: return bcast8<5>(v);
+    case 6: return bcast8<6>(v);
+    default: return bcast8<7>(v);
+  }
 }
 
 __device__ __forceinline__ double rcp_refined_w(double y) {
@@ -536,80 +562,63 @@ __device__ __forceinline__ double rcp_refined_w(double y) {
   return __builtin_fma(r, e, r);
 }
 
-// The row term a_k of hild_row_t for lane k: a_0 = fma(M_i0, v_0, K_i), a_k = M_ik v_k,
-// as fma(M_ik, v_k, kz) with kz = K_i in lane 0 and +0 elsewhere.  fma(m, v, +0) differs
-// from m*v only in the sign of a zero product, which cannot reach t: the lanes >= Nc add
-// +0, so the butterfly never returns -0.  Constant rows (M entries +-1 / +-0) become an
-// add or a select: fma(+-0, v, kz) = kz up to the sign of a zero for finite v (a
-// non-finite v ends the sweep on the exact path).
+// The row term b_k of hild_row_t for lane k (columns k and k + 8): a_0 = fma(M_i0, v_0, K_i),
+// a_k = M_ik v_k, as fma(M_ik, v_k, kz) with kz = K_i in lane 0 and +0 elsewhere (fma(m, v, +0)
+// differs from m*v only in the sign of a zero product, which cannot reach t); then
+// b_k = fma(M_i,k+8, v_k+8, a_k).  Constant rows (M entries +-1 / +-0) become an add or a
+// select.  A lane whose column k + 8 does not exist holds a stray v1 (see x1_to_lanes01)
+// and reads a zero M entry for it, or is not selected.
 template <int NP, int NC>
-__device__ __forceinline__ double row_term(int i, int k, double v, double kz, double m) {
-  if (i < NC) return k <= i ? v + kz : kz;
-  if (i < 2 * NC) return k <= i - NC ? kz - v : kz;
-  if (i < 3 * NC) return k == i - 2 * NC ? v + kz : kz;
-  if (i < 4 * NC) return k == i - 3 * NC ? kz - v : kz;
-  const int blk = (i - 4 * NC) / NP;
-  return blk == 1 ? __builtin_fma(-m, v, kz) : __builtin_fma(m, v, kz);
+__device__ __forceinline__ double row_term8(int i, int k, double v0, double v1, double kz, double m0, double m1) {
+  if (i < NC) {  // Cu row i: ones in columns 0..i
+    double a = k <= i ? v0 + kz : kz;
+    if (i >= 8) a = (k + 8 <= i && k + 8 < NC) ? a + v1 : a;
+    return a;
+  }
+  if (i < 2 * NC) {  // -Cu
+    const int r = i - NC;
+    double a = k <= r ? kz - v0 : kz;
+    if (r >= 8) a = (k + 8 <= r && k + 8 < NC) ? a - v1 : a;
+    return a;
+  }
+  const int blk = (i - 4 * NC) / NP, r = (i - 4 * NC) % NP;
+  double a = blk == 1 ? __builtin_fma(-m0, v0, kz) : __builtin_fma(m0, v0, kz);
+  if (r >= 8 && NC > 8) a = blk == 1 ? __builtin_fma(-m1, v1, a) : __builtin_fma(m1, v1, a);
+  return a;
 }
-// The I / -I rows (one M entry, +-1 in column j): the butterfly of hild_row_t adds K_i and
-// +-v_j to zeros only, which is exact, so t = K_i +- v_j in one rounding (the sign of a
-// zero t aside, which cannot reach lambda: num = fma(H_ii, lambda_i, -t) then has the
-// same magnitude and nl = max(w, +0)).  v_j comes from lane j of the DPP row by one
-// 64-bit row_newbcast move instead of the 4-level tree; kz holds K_i in every lane.
+// The I / -I rows (one M entry, +-1 in column j): the tree of hild_row_t adds K_i and +-v_j
+// to zeros only, which is exact, so t = K_i +- v_j in one rounding (the sign of a zero t
+// aside, which cannot reach lambda: num = fma(H_ii, lambda_i, -t) then has the same
+// magnitude and nl = max(w, +0)).  v_j comes from lane j % 8 of the group (v0 for j < 8,
+// v1 above) by bcast8; K_i is read in every lane.
 template <int NC>
 __device__ __forceinline__ constexpr bool unit_row(int i) {
   return i >= 2 * NC && i < 4 * NC;
 }
-template <int J>
-__device__ __forceinline__ double row_bcast(double v) {
-  // every lane of every row is written (row/bank masks full, the source lane valid), so
-  // the "old" operand is dead: passing v lets the move run in place of a dead v instead
-  // of first materialising a zero
-  return __builtin_amdgcn_update_dpp(MPCEKF_BCAST_OLD_V ? v : 0.0, v, 0x150 + J, 0xF, 0xF, false);  // row_newbcast:J
-}
-__device__ __forceinline__ double row_bcast(double v, int j) {  // j a constant after unrolling
-  switch (j) {
-    case 0: return row_bcast<0>(v);
-    case 1: return row_bcast<1>(v);
-    case 2: return row_bcast<2>(v);
-    case 3: return row_bcast<3>(v);
-    case 4: return row_bcast<4>(v);
-    case 5: return row_bcast<5>(v);
-    case 6: return row_bcast<6>(v);
-    case 7: return row_bcast<7>(v);
-    case 8: return row_bcast<8>(v);
-    case 9: return row_bcast<9>(v);
-    case 10: return row_bcast<10>(v);
-    case 11: return row_bcast<11>(v);
-    case 12: return row_bcast<12>(v);
-    case 13: return row_bcast<13>(v);
-    case 14: return row_bcast<14>(v);
-    default: return row_bcast<15>(v);
-  }
-}
 template <int NC>
-__device__ __forceinline__ double unit_t(int i, double v, double K) {
-  static_assert(NC <= 16, "one DPP row per cell");
-  const double vj = row_bcast(v, (i - 2 * NC) % NC);
+__device__ __forceinline__ double unit_t(int i, double v0, double v1, double K) {
+  static_assert(NC <= 16, "two columns per lane of an 8-lane group");
+  const int j = (i - 2 * NC) % NC;
+  const double vj = j < 8 ? bcast8(v0, j) : bcast8(v1, j - 8);
   return i < 3 * NC ? K + vj : K - vj;
 }
-// Rows whose nonzero terms sit in lanes 0 .. 2^L - 1 only (the first Cu / -Cu rows and
-// the first rows of each Toeplitz block, M(i, k) = 0 for k > r): after L levels lane 0
-// holds the block's sum and the remaining levels would add exact zeros, so it is
-// broadcast to the row instead (the sign of a zero t aside, as for unit_t).
+// Rows whose nonzero terms sit in lanes 0 .. 2^L - 1 only (after folding column k + 8 into
+// lane k): L = 0 (one term: the first Cu / -Cu row, the first row of each Toeplitz block)
+// broadcasts lane 0, L = 1 adds one level first; otherwise the full tree, whose extra levels
+// would add exact zeros (the sign of a zero t aside, as for unit_t).
 template <int NP, int NC>
-__device__ __forceinline__ constexpr int row_levels(int i) {
-  const int nz = i < NC ? i + 1 : i < 2 * NC ? i - NC + 1 : i < 4 * NC ? NC : ((i - 4 * NC) % NP + 1 < NC ? (i - 4 * NC) % NP + 1 : NC);
-  return nz <= 1 ? 0 : nz <= 2 ? 1 : nz <= 4 ? 2 : nz <= 8 ? 3 : 4;
+__device__ __forceinline__ constexpr int row_levels8(int i) {
+  const int nz = i < NC ? i + 1 : i < 2 * NC ? i - NC + 1 : ((i - 4 * NC) % NP + 1 < NC ? (i - 4 * NC) % NP + 1 : NC);
+  const int lanes = nz < 8 ? nz : 8;
+  return lanes <= 1 ? 0 : lanes <= 2 ? 1 : 3;
 }
-__device__ __forceinline__ double tree_rows(int L, double a) {  // L a constant after unrolling
-  if (L >= 4) return tree16(a);
+__device__ __forceinline__ double tree_rows8(int L, double a) {  // L a constant after unrolling
+  if (L >= 3) return tree8(a);
   if (L >= 1) a = a + dpp64<0xB1>(a);
-  if (L >= 2) a = a + dpp64<0x4E>(a);
-  if (L >= 3) a = a + dpp64<0x141>(a);
-  return row_bcast<0>(a);
+  return bcast8<0>(a);
 }
-// lane k's M entry of Toeplitz row i (0 for the constant rows, which row_term builds)
+// lane k's M entry of Toeplitz row i for column col (0 for the constant rows, which
+// row_term8 builds); mp points at the block-0 entry of row 0 for this lane's column
 template <int NP, int NC>
 __device__ __forceinline__ double row_m(int i, const double *mp) {
   if (i < 4 * NC) return 0.0;
@@ -617,13 +626,34 @@ __device__ __forceinline__ double row_m(int i, const double *mp) {
   return mp[blk * W<NP, NC>::HPW + r];
 }
 
+// X's columns 8 .. Nc-1 (lanes 0 .. Nc-9 of a group use them) are held spread over the
+// group: row u's pair sits in lanes 2q, 2q + 1 (q = u % 4) at register slot u / 4, and is
+// moved into lanes 0, 1 by one row_shl:2q when row u runs.  80 more doubles per lane for
+// column k + 8 did not fit beside column k's 80.  The other lanes receive stray values
+// there (finite: X is finite on this path), which every use masks: their M entries for
+// columns >= 8 are read from the zero row, and the Cu rows select on the lane.
+template <int Q>
+__device__ __forceinline__ double x1_to_lanes01(double v) {
+  if constexpr (Q == 0) return v;
+  else return dpp64<0x100 + 2 * Q>(v);  // row_shl:2Q
+}
+__device__ __forceinline__ double x1_to_lanes01(double v, int q) {  // q a constant after unrolling
+  switch (q) {
+    case 0: return x1_to_lanes01<0>(v);
+    case 1: return x1_to_lanes01<1>(v);
+    case 2: return x1_to_lanes01<2>(v);
+    default: return x1_to_lanes01<3>(v);
+  }
+}
+
 template <int NP, int NC>
-__global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
+__global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KState s, const KWide w) {
   using T = W<NP, NC>;
-  constexpr int NCON = T::NCON, HPW = T::HPW;
+  constexpr int NCON = T::NCON, HPW = T::HPW, LN = T::LANES;
+  static_assert(LN == 8 && NC > LN && T::BLOCK == 128, "8-lane groups with columns >= 8 (Nc = 10); the launch bounds");
   extern __shared__ double lds[];
-  double *zero = lds;  // NCON zeros: lanes that add no K_i / no M entry read these
-  const int g = threadIdx.x >> 4, k = threadIdx.x & 15;
+  double *zero = lds;  // NCON zeros: lanes that add no K_i read these
+  const int g = threadIdx.x / LN, k = threadIdx.x % LN;
   const int64_t n = s.n, slot = (int64_t)blockIdx.x * T::GROUPS + g;
   static_assert(T::ZERO_LDS % 2 == 0 && T::CELL_LDS % 2 == 0, "16-byte aligned (H_ii, 1/H_ii) pairs");
   double *base = lds + T::ZERO_LDS + g * T::CELL_LDS;
@@ -634,7 +664,7 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
   const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_bin<true>'s order
   bool ok = true;
   if (act) {
-    for (int i = k; i < NCON; i += 16) {
+    for (int i = k; i < NCON; i += LN) {
       const double li = s.lam[(size_t)i * n + c];
       const double hii = w.hii[(size_t)c * NCON + i];
       const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
@@ -644,63 +674,86 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
       Kl[i] = w.K[(size_t)c * NCON + i];
       hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
     }
-    for (int j = k; j < 3 * HPW; j += 16) {
+    for (int j = k; j < 3 * HPW; j += LN) {
       const int b = j / HPW, q = j % HPW;
       hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
     }
   }
   __syncthreads();
   if (!act) return;
-  const int gshift = 16 * (g & 3);
-  if ((__ballot(!ok) >> gshift) & 0xFFFFull) {  // outside the fast form's domain
+  const int gshift = LN * (g % (64 / LN));
+  if ((__ballot(!ok) >> gshift) & 0xFFull) {  // outside the fast form's domain
     if (k == 0) s.hflag[c] = 2;
     return;
   }
   const double *kp = k == 0 ? Kl : zero;
-  // lanes >= Nc read lane Nc-1's entry (a broadcast, no bank of their own): their v_k
-  // is +0 for good (X there is 0 and lambda >= 0), so fma(+-m, +0, +0) = +0 as before
-  const double *mp = hp + (NC - 1) - (k < NC ? k : NC - 1);
+  // lanes whose column does not exist read column Nc-1's entry (a broadcast, no bank of
+  // their own): their v is +0 for good (X there is 0 and lambda >= 0), so the term is +-0
+  const int col0 = k < NC ? k : NC - 1;
+  const double *mp0 = hp + (NC - 1) - col0;
+  const double *mp1 = k + LN < NC ? hp + (NC - 1) - (k + LN) : zero;  // zero: the stray lanes
   // lambda_i store: lane k = 0 writes lam[i]; the other lanes write their own slot of a
-  // per-wave sink (16 lanes storing one address serialise in one LDS bank, and the next
+  // per-wave sink (8 lanes storing one address serialise in one LDS bank, and the next
   // rows' operand reads queue behind that store)
   double *lst = lam;
-  if (MPCEKF_WIDE_JUNK && k != 0)
-    lst = lds + T::ZERO_LDS + T::GROUPS * T::CELL_LDS + (threadIdx.x >> 6) * T::JUNK + (threadIdx.x & 63);
-  double X[T::NX_ROWS];
+  if (k != 0) lst = lds + T::ZERO_LDS + T::GROUPS * T::CELL_LDS + (threadIdx.x >> 6) * T::JUNK + (threadIdx.x & 63);
+  static_assert(NC <= LN + 2 && T::NX_ROWS % 4 == 0, "columns >= 8 spread as pairs over 4 lane pairs");
+  double X0[T::NX_ROWS], X1[T::NX_ROWS / 4];
 #pragma unroll
-  for (int u = 0; u < T::NX_ROWS; ++u) X[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
+  for (int u = 0; u < T::NX_ROWS; ++u) X0[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
+#pragma unroll
+  for (int sl = 0; sl < T::NX_ROWS / 4; ++sl) {
+    const int u = 4 * sl + (k >> 1), col = LN + (k & 1);
+    X1[sl] = col < NC ? w.X[((size_t)u * n + c) * NC + col] : 0.0;
+  }
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
+  // v = X*lambda at the start of a sweep (orc hild_v: fma from +0 in ascending j).  The
+  // first one is summed here from the warm start; each sweep then accumulates the next
+  // sweep's (u0, u1) row by row from lambda_j's final value of this sweep, which is the same
+  // sequence of fmas on the same operands as summing after the sweep, without a second
+  // pass over X and lambda.
+  double v0 = 0.0, v1 = 0.0;
+#pragma unroll
+  for (int j = 0; j < NCON; ++j) {
+    if (j % 4 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
+    const int u = xslot<NP, NC>(j);
+    const double x0 = X0[u], x1 = x1_to_lanes01(X1[u / 4], u % 4);
+    const double lj = lam[j];
+    v0 = __builtin_fma(xneg<NC>(j) ? -x0 : x0, lj, v0);
+    v1 = __builtin_fma(xneg<NC>(j) ? -x1 : x1, lj, v1);
+  }
   int it;
   bool slow = false;
   for (it = 1; it <= maxIter; ++it) {
-    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep: hoisted out
-    // of the loop they would need ~400 more registers
+    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep
     asm volatile("" ::: "memory");
-    double v = 0.0;  // v = X*lambda (orc hild_v: fma from +0 in ascending j)
-#pragma unroll
-    for (int j = 0; j < NCON; ++j) {
-      if (j % 8 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
-      const double x = X[xslot<NP, NC>(j)];
-      v = __builtin_fma(xneg<NC>(j) ? -x : x, lam[j], v);
-    }
-    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+    double u0 = 0.0, u1 = 0.0;  // the next sweep's v
+    // hildreth.m:39's stop test as a wave mask (|d| < tol on every row; a NaN d is "not
+    // converged", as in orc_hildreth; the 8 lanes of a group compute the same d), and the
+    // fast division's domain as the range of the dividends' high words (sign cleared):
+    // |num| in [2^-400, 2^400) exactly when hi(2^-400) <= hi(|num|) < hi(2^400).  Integer,
+    // so no canonicalising max/min.
+    uint64_t convm = ~0ull;
+    unsigned xhi = 0u, xlo = 0x7fffffffu;
     // row i's LDS operands are read one row ahead (ds_read latency off the chain)
-    double kz = unit_row<NC>(0) ? Kl[0] : kp[0], li = lam[0], m = row_m<NP, NC>(0, mp);
+    double kz = unit_row<NC>(0) ? Kl[0] : kp[0], li = lam[0], m0 = row_m<NP, NC>(0, mp0), m1 = row_m<NP, NC>(0, mp1);
     double2 h = hr[0];
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
       asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
-      double kzn = kz, lin = li, mn = m;
+      double kzn = kz, lin = li, m0n = m0, m1n = m1;
       double2 hn = h;
       if (i + 1 < NCON) {
         kzn = unit_row<NC>(i + 1) ? Kl[i + 1] : kp[i + 1];
         lin = lam[i + 1];
         hn = hr[i + 1];
-        mn = row_m<NP, NC>(i + 1, mp);
+        m0n = row_m<NP, NC>(i + 1, mp0);
+        const int r1 = (i + 1 - 4 * NC) % NP;
+        m1n = (i + 1 >= 4 * NC && r1 >= 8 && NC > 8) ? row_m<NP, NC>(i + 1, mp1) : 0.0;
       }
-      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v, kz)
-                                       : tree_rows(row_levels<NP, NC>(i), row_term<NP, NC>(i, k, v, kz, m));
+      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v0, v1, kz)
+                                       : tree_rows8(row_levels8<NP, NC>(i), row_term8<NP, NC>(i, k, v0, v1, kz, m0, m1));
       // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
       // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
       // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
@@ -710,35 +763,48 @@ __global__ void __launch_bounds__(256, 2) k_hild_wide(const KCfg cf, const KStat
       const double wf = __builtin_fma(e2, h.y, q0);
       const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
       const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
-      xmax = fmax(xmax, fabs(num));
-      xmin = fmin(xmin, fabs(num));
+      const unsigned hb = (unsigned)__double2hiint(num) & 0x7fffffffu;
+      xhi = hb > xhi ? hb : xhi;
+      xlo = hb < xlo ? hb : xlo;
       const double nl = wv > 0 ? wv : 0.0;
       const double d = nl - li;
-      dmax = fmax(dmax, fabs(d));
+      convm &= __ballot(fabs(d) < tol);
       lst[i] = nl;
-      const double x = X[xslot<NP, NC>(i)];
-      v = __builtin_fma(xneg<NC>(i) ? -x : x, d, v);
+      const double x0 = xneg<NC>(i) ? -X0[xslot<NP, NC>(i)] : X0[xslot<NP, NC>(i)];
+      const double x1r = x1_to_lanes01(X1[xslot<NP, NC>(i) / 4], xslot<NP, NC>(i) % 4);
+      const double x1 = xneg<NC>(i) ? -x1r : x1r;
+      v0 = __builtin_fma(x0, d, v0);
+      v1 = __builtin_fma(x1, d, v1);
+      u0 = __builtin_fma(x0, nl, u0);
+      u1 = __builtin_fma(x1, nl, u1);
+      // every accumulation finishes in its row: left alone, the compiler sank the ones not
+      // needed before the sweep end (u, the stop flag, the domain range) and held every
+      // row's dividend, lambda and step live across the sweep
+      asm volatile("" : "+v"(xhi), "+v"(xlo), "+v"(u0), "+v"(u1), "+v"(v1), "+s"(convm));
       kz = kzn;
       li = lin;
       h = hn;
-      m = mn;
+      m0 = m0n;
+      m1 = m1n;
     }
     // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
     // the fast division's domain: the exact path redoes this cell from its warm start,
     // still in s.lam (every sweep before was bit-identical to the exact form)
-    const bool bad = !(isfinite(v) && xmax <= 0x1p400 && xmin >= 0x1p-400);
-    if ((__ballot(bad) >> gshift) & 0xFFFFull) {
+    const bool bad = !(isfinite(v0) && isfinite(v1) && xhi < 0x58f00000u && xlo >= 0x26f00000u);  // hi(2^+-400)
+    if ((__ballot(bad) >> gshift) & 0xFFull) {
       slow = true;
       break;
     }
-    if (dmax < tol) break;
+    if ((convm >> gshift) & 1ull) break;
+    v0 = u0;
+    v1 = u1;
   }
   if (slow) {
     if (k == 0) s.hflag[c] = 2;
     return;
   }
   if (it > maxIter) it = maxIter;
-  for (int i = k; i < NCON; i += 16) s.lam[(size_t)i * n + c] = lam[i];
+  for (int i = k; i < NCON; i += LN) s.lam[(size_t)i * n + c] = lam[i];
   if (k == 0) w.it[c] = it;
 }
 
@@ -772,15 +838,18 @@ __device__ __forceinline__ double row_t_rt(const double *Hall, int i, const doub
     for (int k = 0; k < NC; ++k) t = __builtin_fma(mval_rt<NP, NC>(Hall, i, k), v[k], t);
     return t;
   }
-  double a[16];
-  a[0] = __builtin_fma(mval_rt<NP, NC>(Hall, i, 0), v[0], Ki);
+  double b[8];  // orc hild_row_t's 8-lane form
 #pragma unroll
-  for (int k = 1; k < 16; ++k) a[k] = k < NC ? mval_rt<NP, NC>(Hall, i, k) * v[k] : 0.0;
+  for (int k = 0; k < 8; ++k) {
+    const double a = k == 0 ? __builtin_fma(mval_rt<NP, NC>(Hall, i, 0), v[0], Ki)
+                            : (k < NC ? mval_rt<NP, NC>(Hall, i, k) * v[k] : 0.0);
+    b[k] = k + 8 < NC ? __builtin_fma(mval_rt<NP, NC>(Hall, i, k + 8 < NC ? k + 8 : 0), v[k + 8 < NC ? k + 8 : 0], a) : a;
+  }
 #pragma unroll
-  for (int wd = 1; wd < 16; wd *= 2)
+  for (int wd = 1; wd < 8; wd *= 2)
 #pragma unroll
-    for (int k = 0; k < 16; k += 2 * wd) a[k] = a[k] + a[k + wd];
-  return a[0];
+    for (int k = 0; k < 8; k += 2 * wd) b[k] = b[k] + b[k + wd];
+  return b[0];
 }
 
 template <int NP, int NC>
@@ -1049,7 +1118,7 @@ int grid(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
 template <int NP, int NC>
 int hild_lds_bytes_w() {
-  return (W<NP, NC>::ZERO_LDS + W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS + (MPCEKF_WIDE_JUNK ? 4 * W<NP, NC>::JUNK : 0)) *
+  return (W<NP, NC>::ZERO_LDS + W<NP, NC>::GROUPS * W<NP, NC>::CELL_LDS + W<NP, NC>::WAVES * W<NP, NC>::JUNK) *
          (int)sizeof(double);
 }
 
@@ -1094,8 +1163,8 @@ int launch_hild_wide(const KCfg &c, const KState &s, const KIO &io, const KWide 
   hipLaunchKernelGGL(k_hild_bin<false>, dim3(grid(s.n, LIST_CPB)), dim3(1024), 0, st, c, s, w);
   hipLaunchKernelGGL(k_hild_sort, dim3(1), dim3(64), 0, st, w);
   hipLaunchKernelGGL(k_hild_bin<true>, dim3(grid(s.n, LIST_CPB)), dim3(1024), 0, st, c, s, w);
-  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)), dim3(256), lds,
-                     st, c, s, w);
+  hipLaunchKernelGGL((k_hild_wide<WIDE_NP, WIDE_NC>), dim3(grid(s.n, W<WIDE_NP, WIDE_NC>::GROUPS)),
+                     dim3(W<WIDE_NP, WIDE_NC>::BLOCK), lds, st, c, s, w);
   hipLaunchKernelGGL((k_hild_wide_slow<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, w);
   hipLaunchKernelGGL((k_mpc_wide_finish<WIDE_NP, WIDE_NC>), dim3(grid(s.n, 64)), dim3(64), 0, st, c, s, io, w);
   return (int)hipGetLastError();

@@ -525,22 +525,24 @@ static void hild_v(int Nc, int nC, const double *X, const double *lam, double *v
 }
 
 /* t_i = K_i + M(i,:)*v of the rank form.  Nc <= 2 (the lane-per-cell kernels): fma in
- * ascending k.  Nc > 2 (the 16-lane-group kernels, lane k holding v_k): a_0 = fma(M_i0, v_0,
- * K_i), a_k = M_ik*v_k for 0 < k < Nc, a_k = +0 for Nc <= k < 16, summed as the pairwise
- * tree ((a0+a1)+(a2+a3)) + ((a4+a5)+(a6+a7)) ... over the 16 slots (the lane butterfly). */
+ * ascending k.  Nc > 2 (the 8-lane-group kernels, lane k holding v_k and v_{k+8}):
+ * a_0 = fma(M_i0, v_0, K_i), a_k = M_ik*v_k for 0 < k < min(Nc, 8), +0 for Nc <= k < 8;
+ * b_k = fma(M_i,k+8, v_k+8, a_k) when k + 8 < Nc, else a_k; summed as the pairwise tree
+ * ((b0+b1)+(b2+b3)) + ((b4+b5)+(b6+b7)) (the 3-level lane butterfly).  For Nc <= 8 this is
+ * round 2's 16-slot tree up to the sign of a zero t (its extra slots only added +0), which
+ * cannot reach lambda: num = fma(H_ii, lambda_i, -t) and max(w, 0) absorb it. */
 static double hild_row_t(int Nc, const double *Mi, const double *v, double Ki) {
   if (Nc <= 2) {
     double t = Ki;
     for (int k = 0; k < Nc; ++k) t = fma(Mi[k], v[k], t);
     return t;
   }
-  double a[16];
-  a[0] = fma(Mi[0], v[0], Ki);
-  for (int k = 1; k < 16; ++k) a[k] = 0.0;
-  for (int k = 1; k < Nc && k < 16; ++k) a[k] = Mi[k] * v[k];
-  for (int w = 1; w < 16; w *= 2)
-    for (int k = 0; k < 16; k += 2 * w) a[k] = a[k] + a[k + w];
-  return a[0];
+  double b[8];
+  for (int k = 0; k < 8; ++k) b[k] = k == 0 ? fma(Mi[0], v[0], Ki) : (k < Nc ? Mi[k] * v[k] : 0.0);
+  for (int k = 8; k < Nc; ++k) b[k - 8] = fma(Mi[k], v[k], b[k - 8]);
+  for (int w = 1; w < 8; w *= 2)
+    for (int k = 0; k < 8; k += 2 * w) b[k] = b[k] + b[k + w];
+  return b[0];
 }
 
 int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double *M /*nC x Nc*/,

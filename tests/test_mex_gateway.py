@@ -204,7 +204,7 @@ def test_hildreth_and_predmat_through_gateway(shim, M):
         DU_c, lam_c, ne_c = M.hildreth(E[None], F[None], Mm[None], g[None], lam0[None], 100)
         _same(DU_m, DU_c.T, f"DU {Nc}x{nC}")
         _same(lam_m, lam_c.T, f"lambda {Nc}x{nC}")
-        assert float(ne_m) == float(ne_c[0])
+        assert float(np.asarray(ne_m).item()) == float(ne_c[0])
     a = np.array([0.9, 0.8, 0.7, 0.95, 0.99, 1.0])
     Cr = rng.standard_normal(6)
     for Np, Nc in ((5, 2), (20, 10)):
