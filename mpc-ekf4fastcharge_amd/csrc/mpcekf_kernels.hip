@@ -2876,15 +2876,21 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
       v[k] = a;
     }
   };
+  // Nc > 2: orc_hildreth's one-row lookahead, t_i = fma(Hoff_i, d_{i-1}, T_i) with T_i of
+  // v before row i-1's update and Hoff_i = row_t_rt(M(i,:), X(:,i-1), +0)
+  const bool ahead = Nc > 2;
+  double vp[HANY_NC], dp = 0.0;
   int it;
   for (it = 1; it <= maxIter; ++it) {
-    bool conv = true;
+    bool conv = true, look = false;
     if (fin) xv();
     for (int i = 0; i < nC; ++i) {
       const double hii = Hd[i];
       double w;
       if (fin) {
-        const double t = row_t_rt(Nc, M + i * Nc, v, K[i]);
+        const double t = look ? __builtin_fma(row_t_rt(Nc, M + i * Nc, X + (i - 1) * Nc, 0.0), dp,
+                                              row_t_rt(Nc, M + i * Nc, vp, K[i]))
+                              : row_t_rt(Nc, M + i * Nc, v, K[i]);
         w = __builtin_fma(hii, lam[i], -t) / hii;
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2902,9 +2908,15 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
       lam[i] = nl;
       if (fin) {
         if (isfinite(d)) {
-          for (int k = 0; k < Nc; ++k) v[k] = __builtin_fma(X[i * Nc + k], d, v[k]);
+          for (int k = 0; k < Nc; ++k) {
+            vp[k] = v[k];
+            v[k] = __builtin_fma(X[i * Nc + k], d, v[k]);
+          }
+          dp = d;
+          look = ahead;
         } else {
           xv();
+          look = false;
         }
       }
     }

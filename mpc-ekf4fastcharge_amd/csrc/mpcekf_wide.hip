@@ -24,6 +24,12 @@
 
 #include <algorithm>
 
+#ifndef MPCEKF_WIDE_AHEAD
+#define MPCEKF_WIDE_AHEAD 1  // k_hild_wide: orc_hildreth's one-row lookahead (must match the oracle)
+#endif
+#ifndef MPCEKF_WIDE_PF
+#define MPCEKF_WIDE_PF 2     // k_hild_wide: rows of LDS operand prefetch
+#endif
 #ifndef PREP_UNROLL
 #define PREP_UNROLL 1  // k_hild_prep's row loops (rows in flight per wave)
 #endif
@@ -57,13 +63,14 @@ struct W {
   // with ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
   // (tools/micro/lds_micro.hip); the stride is 4 (mod 32) doubles, so the 8 groups of a
   // wave reading one offset of their own regions hit 8 disjoint bank pairs (b64) / quads (b128)
-  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1 - 4 + 31) / 32 * 32 + 4;
+  static constexpr int CELL_LDS = (5 * NCON + 3 * HPW + 1 - 4 + 31) / 32 * 32 + 4;
   static constexpr int ZERO_LDS = (NCON + 1) & ~1;    // the zero row ahead of the groups
   static constexpr int LANES = 8;                     // lanes per cell
   static constexpr int BLOCK = 128;
   static constexpr int GROUPS = BLOCK / LANES;        // cells per block
   static constexpr int JUNK = 64 + NCON;              // per-wave sink of the lanes k != 0's lambda stores
   static constexpr int WAVES = BLOCK / 64;
+
 };
 
 // k_hild_sort's bins over last step's sweep count (0 .. maxIter)
@@ -658,7 +665,10 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   static_assert(T::ZERO_LDS % 2 == 0 && T::CELL_LDS % 2 == 0, "16-byte aligned (H_ii, 1/H_ii) pairs");
   double *base = lds + T::ZERO_LDS + g * T::CELL_LDS;
   double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
-  double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
+  double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON, *Ho = hp + 3 * HPW;
+  static_assert(5 * NCON + 3 * HPW <= T::CELL_LDS &&
+                    2 * (T::ZERO_LDS + T::GROUPS * T::CELL_LDS + T::WAVES * T::JUNK) * 8 <= 160 * 1024,
+                "two blocks per CU");
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
   const bool act = slot < w.q[0];            // k_hild_sort's count
   const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_bin<true>'s order
@@ -693,8 +703,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   const double *mp0 = hp + (NC - 1) - col0;
   const double *mp1 = k + LN < NC ? hp + (NC - 1) - (k + LN) : zero;  // zero: the stray lanes
   // lambda_i store: lane k = 0 writes lam[i]; the other lanes write their own slot of a
-  // per-wave sink (8 lanes storing one address serialise in one LDS bank, and the next
-  // rows' operand reads queue behind that store)
+  // per-wave sink (8 lanes storing one address serialise in one LDS bank, and an
+  // exec-masked store splits the wave's control flow inside the row)
   double *lst = lam;
   if (k != 0) lst = lds + T::ZERO_LDS + T::GROUPS * T::CELL_LDS + (threadIdx.x >> 6) * T::JUNK + (threadIdx.x & 63);
   static_assert(NC <= LN + 2 && T::NX_ROWS % 4 == 0, "columns >= 8 spread as pairs over 4 lane pairs");
@@ -705,6 +715,35 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   for (int sl = 0; sl < T::NX_ROWS / 4; ++sl) {
     const int u = 4 * sl + (k >> 1), col = LN + (k & 1);
     X1[sl] = col < NC ? w.X[((size_t)u * n + c) * NC + col] : 0.0;
+  }
+  // X(:, i) of constraint row i for lane k's two columns (the -Cu / -I rows negated)
+  auto xrow = [&](int i, double &x0, double &x1) {
+    const int u = xslot<NP, NC>(i);
+    const double a = X0[u], b = x1_to_lanes01(X1[u / 4], u % 4);
+    x0 = xneg<NC>(i) ? -a : a;
+    x1 = xneg<NC>(i) ? -b : b;
+  };
+  // lane k's M entries of row i (columns k and k + 8; the constant rows build theirs)
+  auto mrow = [&](int i, double &m0, double &m1) {
+    m0 = row_m<NP, NC>(i, mp0);
+    m1 = (i >= 4 * NC && (i - 4 * NC) % NP >= 8 && NC > 8) ? row_m<NP, NC>(i, mp1) : 0.0;
+  };
+  // K_i + M(i,:)*v as hild_row_t's lane tree (kz = K_i in lane 0, +0 elsewhere; K_i in
+  // every lane of a unit row)
+  auto rowT = [&](int i, double a0, double a1, double kz, double m0, double m1) {
+    return unit_row<NC>(i) ? unit_t<NC>(i, a0, a1, kz)
+                           : tree_rows8(row_levels8<NP, NC>(i), row_term8<NP, NC>(i, k, a0, a1, kz, m0, m1));
+  };
+  // orc_hildreth's lookahead coefficient Hoff_i = M(i,:)*X(:,i-1): the same lane tree with
+  // +0 for K_i, once per call (X and M do not change between sweeps)
+#pragma unroll
+  for (int i = 1; i < (MPCEKF_WIDE_AHEAD ? NCON : 1); ++i) {
+    if (i % 4 == 0) asm volatile("" ::: "memory");
+    double x0, x1, m0, m1;
+    xrow(i - 1, x0, x1);
+    mrow(i, m0, m1);
+    const double hv = rowT(i, x0, x1, 0.0, m0, m1);
+    if (k == 0) Ho[i] = hv;  // read back only by this group's lanes (same wave: in order)
   }
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
@@ -717,16 +756,16 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
 #pragma unroll
   for (int j = 0; j < NCON; ++j) {
     if (j % 4 == 0) asm volatile("" ::: "memory");  // no hoisting of every row's loads
-    const int u = xslot<NP, NC>(j);
-    const double x0 = X0[u], x1 = x1_to_lanes01(X1[u / 4], u % 4);
+    double x0, x1;
+    xrow(j, x0, x1);
     const double lj = lam[j];
-    v0 = __builtin_fma(xneg<NC>(j) ? -x0 : x0, lj, v0);
-    v1 = __builtin_fma(xneg<NC>(j) ? -x1 : x1, lj, v1);
+    v0 = __builtin_fma(x0, lj, v0);
+    v1 = __builtin_fma(x1, lj, v1);
   }
   int it;
   bool slow = false;
   for (it = 1; it <= maxIter; ++it) {
-    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep
+    // K_i, (H_ii, 1/H_ii), Hoff_i and the M entries are re-read from LDS every sweep
     asm volatile("" ::: "memory");
     double u0 = 0.0, u1 = 0.0;  // the next sweep's v
     // hildreth.m:39's stop test as a wave mask (|d| < tol on every row; a NaN d is "not
@@ -736,24 +775,46 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     // so no canonicalising max/min.
     uint64_t convm = ~0ull;
     unsigned xhi = 0u, xlo = 0x7fffffffu;
-    // row i's LDS operands are read one row ahead (ds_read latency off the chain)
-    double kz = unit_row<NC>(0) ? Kl[0] : kp[0], li = lam[0], m0 = row_m<NP, NC>(0, mp0), m1 = row_m<NP, NC>(0, mp1);
-    double2 h = hr[0];
+    // Row i's chain is t_i = fma(Hoff_i, d_{i-1}, T_i) -> the division -> d_i; T_{i+1}, the
+    // tree of row i+1 over v before row i's update, is formed beside it (AHEAD; else t_i
+    // is row i's own tree over v).  A row's LDS operands are read PF rows ahead of the row
+    // that first uses them: the compiler pulls a row's first chain operations up into the
+    // row before, and a one-row distance then left the reads ~20 instructions to land.
+    constexpr int AHEAD = MPCEKF_WIDE_AHEAD, PF = MPCEKF_WIDE_PF, RING = PF + 1 + AHEAD;
+    struct Ops {
+      double kz, m0, m1, li, ho;
+      double2 h;
+    } q[RING];
+    auto load_ops = [&](int r) {
+      Ops &o = q[r % RING];
+      o.kz = unit_row<NC>(r) ? Kl[r] : kp[r];
+      mrow(r, o.m0, o.m1);
+      o.li = lam[r];
+      o.h = hr[r];
+      o.ho = AHEAD && r > 0 ? Ho[r] : 0.0;
+    };
+#pragma unroll
+    for (int r = 0; r < PF + AHEAD && r < NCON; ++r) load_ops(r);
+    double T = 0.0, dp = 0.0;
+    if (AHEAD) T = rowT(0, v0, v1, q[0].kz, q[0].m0, q[0].m1);  // t_0: no lookahead at a sweep's first row
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
-      asm volatile("" ::: "memory");  // loads stay one row ahead, not all at the sweep start
-      double kzn = kz, lin = li, m0n = m0, m1n = m1;
-      double2 hn = h;
-      if (i + 1 < NCON) {
-        kzn = unit_row<NC>(i + 1) ? Kl[i + 1] : kp[i + 1];
-        lin = lam[i + 1];
-        hn = hr[i + 1];
-        m0n = row_m<NP, NC>(i + 1, mp0);
-        const int r1 = (i + 1 - 4 * NC) % NP;
-        m1n = (i + 1 >= 4 * NC && r1 >= 8 && NC > 8) ? row_m<NP, NC>(i + 1, mp1) : 0.0;
+      asm volatile("" ::: "memory");  // loads stay in their rows, not all at the sweep start
+      if (i + PF + AHEAD < NCON) load_ops(i + PF + AHEAD);
+      const Ops &o = q[i % RING];
+      double t, Tn = 0.0;
+      if (AHEAD) {
+        // T_{i+1} from v before this row's update (v0, v1 now)
+        if (i + 1 < NCON) {
+          const Ops &on = q[(i + 1) % RING];
+          Tn = rowT(i + 1, v0, v1, on.kz, on.m0, on.m1);
+        }
+        t = i == 0 ? T : __builtin_fma(o.ho, dp, T);
+      } else {
+        t = rowT(i, v0, v1, o.kz, o.m0, o.m1);
       }
-      const double t = unit_row<NC>(i) ? unit_t<NC>(i, v0, v1, kz)
-                                       : tree_rows8(row_levels8<NP, NC>(i), row_term8<NP, NC>(i, k, v0, v1, kz, m0, m1));
+      const double li = o.li;
+      const double2 h = o.h;
       // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
       // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
       // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
@@ -770,9 +831,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       const double d = nl - li;
       convm &= __ballot(fabs(d) < tol);
       lst[i] = nl;
-      const double x0 = xneg<NC>(i) ? -X0[xslot<NP, NC>(i)] : X0[xslot<NP, NC>(i)];
-      const double x1r = x1_to_lanes01(X1[xslot<NP, NC>(i) / 4], xslot<NP, NC>(i) % 4);
-      const double x1 = xneg<NC>(i) ? -x1r : x1r;
+      double x0, x1;
+      xrow(i, x0, x1);
       v0 = __builtin_fma(x0, d, v0);
       v1 = __builtin_fma(x1, d, v1);
       u0 = __builtin_fma(x0, nl, u0);
@@ -781,11 +841,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       // needed before the sweep end (u, the stop flag, the domain range) and held every
       // row's dividend, lambda and step live across the sweep
       asm volatile("" : "+v"(xhi), "+v"(xlo), "+v"(u0), "+v"(u1), "+v"(v1), "+s"(convm));
-      kz = kzn;
-      li = lin;
-      h = hn;
-      m0 = m0n;
-      m1 = m1n;
+      T = Tn;
+      dp = d;
     }
     // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
     // the fast division's domain: the exact path redoes this cell from its warm start,
@@ -913,8 +970,8 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
   const int maxIter = cf.max_hild;
   int it;
   for (it = 1; it <= maxIter; ++it) {
-    bool conv = true;
-    double v[NC];
+    bool conv = true, look = false;  // orc_hildreth's one-row lookahead (NC > 2)
+    double v[NC], vp[NC], dp = 0.0;
     if (fin) hild_v_g<NP, NC>(w.X, n, c, lam, v);
 #pragma unroll 1
     for (int i = 0; i < NCON; ++i) {
@@ -922,7 +979,16 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       const double li = lam[(size_t)i * n + c];
       double wv;
       if (fin) {
-        wv = __builtin_fma(hii, li, -row_t_rt<NP, NC>(Hall, i, v, Ki)) / hii;
+        double t;
+        if (NC > 2 && look) {
+          double xq[NC];  // X(:, i-1), Hoff_i = M(i,:)*X(:,i-1) as the lane tree
+#pragma unroll
+          for (int k = 0; k < NC; ++k) xq[k] = xval_g<NP, NC>(w.X, n, c, i - 1, k);
+          t = __builtin_fma(row_t_rt<NP, NC>(Hall, i, xq, 0.0), dp, row_t_rt<NP, NC>(Hall, i, vp, Ki));
+        } else {
+          t = row_t_rt<NP, NC>(Hall, i, v, Ki);
+        }
+        wv = __builtin_fma(hii, li, -t) / hii;
       } else {  // dense H(i,:)*lambda, 4 interleaved partial sums (orc_hildreth)
         double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
@@ -942,9 +1008,15 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       if (fin) {
         if (isfinite(d)) {
 #pragma unroll
-          for (int k = 0; k < NC; ++k) v[k] = __builtin_fma(xval_g<NP, NC>(w.X, n, c, i, k), d, v[k]);
+          for (int k = 0; k < NC; ++k) {
+            vp[k] = v[k];
+            v[k] = __builtin_fma(xval_g<NP, NC>(w.X, n, c, i, k), d, v[k]);
+          }
+          dp = d;
+          look = NC > 2;
         } else {
           hild_v_g<NP, NC>(w.X, n, c, lam, v);
+          look = false;
         }
       }
     }

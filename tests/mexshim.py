@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "mex", "_build", "libmpcekf_mexshim.so")
+LIB = os.environ.get("MEXSHIM_LIB") or os.path.join(HERE, "mex", "_build", "libmpcekf_mexshim.so")
 
 DOUBLE, INT32, UINT64, STRUCT, CHAR = 6, 12, 15, 2, 4
 _NP = {DOUBLE: np.float64, INT32: np.int32, UINT64: np.uint64, 7: np.float32, 8: np.int8, 9: np.uint8,
@@ -32,7 +32,8 @@ _lib = None
 
 def build():
     import subprocess
-    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "mex")], check=True)
+    if not os.environ.get("MEXSHIM_LIB"):
+        subprocess.run(["make", "-s", "-C", os.path.join(HERE, "mex")], check=True)
 
 
 def load():

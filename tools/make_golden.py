@@ -66,8 +66,42 @@ def make_tprofile(rom, hsh):
     np.savez_compressed(os.path.join(OUT, "tprofile4_300.npz"), rom_hash=hsh, soc0=soc0, tc=tct[0], tc_traj=tct, **r)
 
 
+def _wide_cell(args):
+    soc0, tc, steps = args
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    o = O.run_cell(P.make_synth_rom(), soc0, tc, steps, {"Np": 20, "Nc": 10})
+    return o
+
+
+def make_wide(rom, hsh):
+    """configs[4]'s horizons (Np = 20 / Nc = 10) on the MATLAB-faithful restatement (dense
+    H = M*(E\\M'), hildreth.m:28-42): 8 cells of the batched workload x 400 steps, and 4
+    near-limit cells (88-95 % SOC, the voltage / eta rows active, Hildreth into maxIter)
+    x 200 steps.  The GPU and the C oracle evaluate the rank-10 defined arithmetic
+    (DESIGN.md §3); this fixture holds them to the dense form within north_star's 1e-6."""
+    from multiprocessing import Pool
+    rng = np.random.Generator(np.random.PCG64(0x5EED))
+    soc0, tc = rng.uniform(5, 30, 8), rng.uniform(20, 30, 8)
+    soc0n, tcn = np.array([88.0, 90.5, 93.0, 95.0]), np.array([25.0, 21.0, 29.0, 24.0])
+    jobs = [(s, t, 400) for s, t in zip(soc0, tc)] + [(s, t, 200) for s, t in zip(soc0n, tcn)]
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        outs = pool.map(_wide_cell, jobs)
+    for name, sl, s0, t0 in (("wide_batch8_400.npz", slice(0, 8), soc0, tc), ("wide_near4_200.npz", slice(8, 12), soc0n, tcn)):
+        o = outs[sl]
+        r = {k: np.stack([x[k] for x in o], axis=1) for k in ("u", "v", "soc", "phise", "nexec")}
+        r["status"] = np.array([x["status"][-1] for x in o])
+        np.savez_compressed(os.path.join(OUT, name), rom_hash=hsh, soc0=s0, tc=t0, Np=20, Nc=10, **r)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--wide-only" in sys.argv:
+        P = importlib.import_module("mpc-ekf4fastcharge_amd")
+        rom = P.make_synth_rom()
+        t0 = time.time()
+        make_wide(rom, rom_hash(rom))
+        print(f"wide fixtures written in {time.time() - t0:.0f} s")
+        return
     if "--tprofile-only" in sys.argv:
         P = importlib.import_module("mpc-ekf4fastcharge_amd")
         rom = P.make_synth_rom()
@@ -108,6 +142,8 @@ def main():
     #     call): warming ramps with a ripple, one profile crossing a set-point and the table
     #     grid ends (0 and 50 degC, clamped), 300 steps
     make_tprofile(rom, hsh)
+    # 5c. the wide horizons (configs[4]: Np = 20 / Nc = 10)
+    make_wide(rom, hsh)
     # 6. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
     rng = np.random.default_rng(11)
     n = 24
