@@ -1221,11 +1221,29 @@ __device__ __forceinline__ void hild_mtl(const Cons &Cn, const double L[NCON], d
 // ---------------------------------------------------------------------------
 // LDS staging
 // ---------------------------------------------------------------------------
+// The block's copy of a ROM blob (L2-resident, 30-130 KB) into LDS: 16 loads of 16 B per
+// lane in flight before their stores.  A plain copy loop waited one L2 round trip per
+// 16 B per lane (load, s_waitcnt vmcnt(0), ds_write): ~32 round trips for the cell blob.
 __device__ __forceinline__ void stage_lds(double *dst, const double *src, int len) {
-  int n2 = len / 2;
+  constexpr int B = 16;
+  const int n2 = len / 2, nt = blockDim.x;
   const double2 *s2 = reinterpret_cast<const double2 *>(src);
   double2 *d2 = reinterpret_cast<double2 *>(dst);
-  for (int i = threadIdx.x; i < n2; i += blockDim.x) d2[i] = s2[i];
+  int i = threadIdx.x;
+  for (; i + (B - 1) * nt < n2; i += B * nt) {
+    double2 v[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) v[b] = s2[i + b * nt];
+#pragma unroll
+    for (int b = 0; b < B; ++b) d2[i + b * nt] = v[b];
+  }
+  double2 v[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    if (i + b * nt < n2) v[b] = s2[i + b * nt];
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    if (i + b * nt < n2) d2[i + b * nt] = v[b];
   if ((len & 1) && threadIdx.x == 0) dst[len - 1] = src[len - 1];
 }
 
@@ -2876,21 +2894,15 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
       v[k] = a;
     }
   };
-  // Nc > 2: orc_hildreth's one-row lookahead, t_i = fma(Hoff_i, d_{i-1}, T_i) with T_i of
-  // v before row i-1's update and Hoff_i = row_t_rt(M(i,:), X(:,i-1), +0)
-  const bool ahead = Nc > 2;
-  double vp[HANY_NC], dp = 0.0;
   int it;
   for (it = 1; it <= maxIter; ++it) {
-    bool conv = true, look = false;
+    bool conv = true;
     if (fin) xv();
     for (int i = 0; i < nC; ++i) {
       const double hii = Hd[i];
       double w;
       if (fin) {
-        const double t = look ? __builtin_fma(row_t_rt(Nc, M + i * Nc, X + (i - 1) * Nc, 0.0), dp,
-                                              row_t_rt(Nc, M + i * Nc, vp, K[i]))
-                              : row_t_rt(Nc, M + i * Nc, v, K[i]);
+        const double t = row_t_rt(Nc, M + i * Nc, v, K[i]);
         w = __builtin_fma(hii, lam[i], -t) / hii;
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2908,15 +2920,9 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
       lam[i] = nl;
       if (fin) {
         if (isfinite(d)) {
-          for (int k = 0; k < Nc; ++k) {
-            vp[k] = v[k];
-            v[k] = __builtin_fma(X[i * Nc + k], d, v[k]);
-          }
-          dp = d;
-          look = ahead;
+          for (int k = 0; k < Nc; ++k) v[k] = __builtin_fma(X[i * Nc + k], d, v[k]);
         } else {
           xv();
-          look = false;
         }
       }
     }

@@ -24,9 +24,6 @@
 
 #include <algorithm>
 
-#ifndef MPCEKF_WIDE_AHEAD
-#define MPCEKF_WIDE_AHEAD 1  // k_hild_wide: orc_hildreth's one-row lookahead (must match the oracle)
-#endif
 #ifndef MPCEKF_WIDE_PF
 #define MPCEKF_WIDE_PF 2     // k_hild_wide: rows of LDS operand prefetch
 #endif
@@ -63,7 +60,7 @@ struct W {
   // with ds_read_b128, which on a 16-byte-misaligned address costs ~15x an aligned read
   // (tools/micro/lds_micro.hip); the stride is 4 (mod 32) doubles, so the 8 groups of a
   // wave reading one offset of their own regions hit 8 disjoint bank pairs (b64) / quads (b128)
-  static constexpr int CELL_LDS = (5 * NCON + 3 * HPW + 1 - 4 + 31) / 32 * 32 + 4;
+  static constexpr int CELL_LDS = (4 * NCON + 3 * HPW + 1 - 4 + 31) / 32 * 32 + 4;
   static constexpr int ZERO_LDS = (NCON + 1) & ~1;    // the zero row ahead of the groups
   static constexpr int LANES = 8;                     // lanes per cell
   static constexpr int BLOCK = 128;
@@ -665,8 +662,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   static_assert(T::ZERO_LDS % 2 == 0 && T::CELL_LDS % 2 == 0, "16-byte aligned (H_ii, 1/H_ii) pairs");
   double *base = lds + T::ZERO_LDS + g * T::CELL_LDS;
   double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
-  double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON, *Ho = hp + 3 * HPW;
-  static_assert(5 * NCON + 3 * HPW <= T::CELL_LDS &&
+  double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
+  static_assert(4 * NCON + 3 * HPW <= T::CELL_LDS &&
                     2 * (T::ZERO_LDS + T::GROUPS * T::CELL_LDS + T::WAVES * T::JUNK) * 8 <= 160 * 1024,
                 "two blocks per CU");
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
@@ -734,17 +731,6 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     return unit_row<NC>(i) ? unit_t<NC>(i, a0, a1, kz)
                            : tree_rows8(row_levels8<NP, NC>(i), row_term8<NP, NC>(i, k, a0, a1, kz, m0, m1));
   };
-  // orc_hildreth's lookahead coefficient Hoff_i = M(i,:)*X(:,i-1): the same lane tree with
-  // +0 for K_i, once per call (X and M do not change between sweeps)
-#pragma unroll
-  for (int i = 1; i < (MPCEKF_WIDE_AHEAD ? NCON : 1); ++i) {
-    if (i % 4 == 0) asm volatile("" ::: "memory");
-    double x0, x1, m0, m1;
-    xrow(i - 1, x0, x1);
-    mrow(i, m0, m1);
-    const double hv = rowT(i, x0, x1, 0.0, m0, m1);
-    if (k == 0) Ho[i] = hv;  // read back only by this group's lanes (same wave: in order)
-  }
   const double tol = cf.hild_tol;
   const int maxIter = cf.max_hild;
   // v = X*lambda at the start of a sweep (orc hild_v: fma from +0 in ascending j).  The
@@ -765,7 +751,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   int it;
   bool slow = false;
   for (it = 1; it <= maxIter; ++it) {
-    // K_i, (H_ii, 1/H_ii), Hoff_i and the M entries are re-read from LDS every sweep
+    // K_i, (H_ii, 1/H_ii) and the M entries are re-read from LDS every sweep
     asm volatile("" ::: "memory");
     double u0 = 0.0, u1 = 0.0;  // the next sweep's v
     // hildreth.m:39's stop test as a wave mask (|d| < tol on every row; a NaN d is "not
@@ -775,14 +761,12 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     // so no canonicalising max/min.
     uint64_t convm = ~0ull;
     unsigned xhi = 0u, xlo = 0x7fffffffu;
-    // Row i's chain is t_i = fma(Hoff_i, d_{i-1}, T_i) -> the division -> d_i; T_{i+1}, the
-    // tree of row i+1 over v before row i's update, is formed beside it (AHEAD; else t_i
-    // is row i's own tree over v).  A row's LDS operands are read PF rows ahead of the row
-    // that first uses them: the compiler pulls a row's first chain operations up into the
-    // row before, and a one-row distance then left the reads ~20 instructions to land.
-    constexpr int AHEAD = MPCEKF_WIDE_AHEAD, PF = MPCEKF_WIDE_PF, RING = PF + 1 + AHEAD;
+    // A row's LDS operands are read PF rows ahead: the compiler pulls a row's first
+    // operations up into the row before, and a one-row distance then left the reads ~20
+    // instructions to land (PF = 2: 3.70 -> 3.59 ms per step at configs[4]).
+    constexpr int PF = MPCEKF_WIDE_PF, RING = PF + 1;
     struct Ops {
-      double kz, m0, m1, li, ho;
+      double kz, m0, m1, li;
       double2 h;
     } q[RING];
     auto load_ops = [&](int r) {
@@ -791,28 +775,15 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       mrow(r, o.m0, o.m1);
       o.li = lam[r];
       o.h = hr[r];
-      o.ho = AHEAD && r > 0 ? Ho[r] : 0.0;
     };
 #pragma unroll
-    for (int r = 0; r < PF + AHEAD && r < NCON; ++r) load_ops(r);
-    double T = 0.0, dp = 0.0;
-    if (AHEAD) T = rowT(0, v0, v1, q[0].kz, q[0].m0, q[0].m1);  // t_0: no lookahead at a sweep's first row
+    for (int r = 0; r < PF && r < NCON; ++r) load_ops(r);
 #pragma unroll
     for (int i = 0; i < NCON; ++i) {
       asm volatile("" ::: "memory");  // loads stay in their rows, not all at the sweep start
-      if (i + PF + AHEAD < NCON) load_ops(i + PF + AHEAD);
+      if (i + PF < NCON) load_ops(i + PF);
       const Ops &o = q[i % RING];
-      double t, Tn = 0.0;
-      if (AHEAD) {
-        // T_{i+1} from v before this row's update (v0, v1 now)
-        if (i + 1 < NCON) {
-          const Ops &on = q[(i + 1) % RING];
-          Tn = rowT(i + 1, v0, v1, on.kz, on.m0, on.m1);
-        }
-        t = i == 0 ? T : __builtin_fma(o.ho, dp, T);
-      } else {
-        t = rowT(i, v0, v1, o.kz, o.m0, o.m1);
-      }
+      const double t = rowT(i, v0, v1, o.kz, o.m0, o.m1);
       const double li = o.li;
       const double2 h = o.h;
       // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
@@ -841,8 +812,6 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       // needed before the sweep end (u, the stop flag, the domain range) and held every
       // row's dividend, lambda and step live across the sweep
       asm volatile("" : "+v"(xhi), "+v"(xlo), "+v"(u0), "+v"(u1), "+v"(v1), "+s"(convm));
-      T = Tn;
-      dp = d;
     }
     // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
     // the fast division's domain: the exact path redoes this cell from its warm start,
@@ -970,8 +939,8 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
   const int maxIter = cf.max_hild;
   int it;
   for (it = 1; it <= maxIter; ++it) {
-    bool conv = true, look = false;  // orc_hildreth's one-row lookahead (NC > 2)
-    double v[NC], vp[NC], dp = 0.0;
+    bool conv = true;
+    double v[NC];
     if (fin) hild_v_g<NP, NC>(w.X, n, c, lam, v);
 #pragma unroll 1
     for (int i = 0; i < NCON; ++i) {
@@ -979,16 +948,7 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       const double li = lam[(size_t)i * n + c];
       double wv;
       if (fin) {
-        double t;
-        if (NC > 2 && look) {
-          double xq[NC];  // X(:, i-1), Hoff_i = M(i,:)*X(:,i-1) as the lane tree
-#pragma unroll
-          for (int k = 0; k < NC; ++k) xq[k] = xval_g<NP, NC>(w.X, n, c, i - 1, k);
-          t = __builtin_fma(row_t_rt<NP, NC>(Hall, i, xq, 0.0), dp, row_t_rt<NP, NC>(Hall, i, vp, Ki));
-        } else {
-          t = row_t_rt<NP, NC>(Hall, i, v, Ki);
-        }
-        wv = __builtin_fma(hii, li, -t) / hii;
+        wv = __builtin_fma(hii, li, -row_t_rt<NP, NC>(Hall, i, v, Ki)) / hii;
       } else {  // dense H(i,:)*lambda, 4 interleaved partial sums (orc_hildreth)
         double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
@@ -1008,15 +968,9 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       if (fin) {
         if (isfinite(d)) {
 #pragma unroll
-          for (int k = 0; k < NC; ++k) {
-            vp[k] = v[k];
-            v[k] = __builtin_fma(xval_g<NP, NC>(w.X, n, c, i, k), d, v[k]);
-          }
-          dp = d;
-          look = NC > 2;
+          for (int k = 0; k < NC; ++k) v[k] = __builtin_fma(xval_g<NP, NC>(w.X, n, c, i, k), d, v[k]);
         } else {
           hild_v_g<NP, NC>(w.X, n, c, lam, v);
-          look = false;
         }
       }
     }

@@ -574,30 +574,20 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
    *    after row i v += X(:,i)*(new - old lambda(i)) by fma; when that change is not
    *    finite (a zero-diagonal row going to or from +inf) v is recomputed from lambda
    *    instead, which reproduces the dense form's inf/NaN propagation in kind.
-   *    Nc > 2 (the 8-lane kernels) looks one row ahead: for a row i > 0 whose previous
-   *    row's change d_{i-1} was finite, t_i = fma(Hoff_i, d_{i-1}, T_i) with
-   *    T_i = hild_row_t of v before row i-1's update and Hoff_i = M(i,:)*X(:,i-1) =
-   *    hild_row_t(M(i,:), X(:,i-1), +0) (the same sum, H(i,i-1) of hildreth.m:28), so
-   *    the kernels form T_i's lane tree while row i-1's division runs.
    *  - otherwise the dense H(i,:)*lambda as 4 interleaved partial sums (terms j = q
    *    mod 4 from +0) combined as (p0+p1)+(p2+p3).
    * MATLAB's own BLAS order for H(i,:)*lambda is unpinned; the math is hildreth.m:35. */
-  const int ahead = Nc > 2;
-  double Hoff[NCONMAX];
-  Hoff[0] = 0.0;
-  for (int i = 1; i < nC; ++i) Hoff[i] = hild_row_t(Nc, M + i * Nc, X + (i - 1) * Nc, 0.0);
   int finite = 1;
   for (int i = 0; i < nC * Nc; ++i) finite = finite && isfinite(X[i]) && isfinite(M[i]);
   int it = 0;
   for (it = 1; it <= maxIter; ++it) {
     int conv = 1;
-    double v[NCMAX], vp[NCMAX], dp = 0.0;  /* vp: v before the previous row's update */
-    int look = 0;                            /* 1: row i may use vp + Hoff_i * dp */
+    double v[NCMAX];
     if (finite) hild_v(Nc, nC, X, lam, v);
     for (int i = 0; i < nC; ++i) {
       double w, hii = H[i * HMAX + i];
       if (finite) {
-        double t = look ? fma(Hoff[i], dp, hild_row_t(Nc, M + i * Nc, vp, K[i])) : hild_row_t(Nc, M + i * Nc, v, K[i]);
+        double t = hild_row_t(Nc, M + i * Nc, v, K[i]);
         w = fma(hii, lam[i], -t) / hii;
       } else {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
@@ -610,17 +600,10 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
       if (!(fabs(d) < tol)) conv = 0;
       lam[i] = nl;
       if (finite) {
-        if (isfinite(d)) {
-          for (int k = 0; k < Nc; ++k) {
-            vp[k] = v[k];
-            v[k] = fma(X[i * Nc + k], d, v[k]);
-          }
-          dp = d;
-          look = ahead;
-        } else {
+        if (isfinite(d))
+          for (int k = 0; k < Nc; ++k) v[k] = fma(X[i * Nc + k], d, v[k]);
+        else
           hild_v(Nc, nC, X, lam, v);
-          look = 0;
-        }
       }
     }
     if (conv) break;
