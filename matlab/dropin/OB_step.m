@@ -16,7 +16,7 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
     cfg.SigmaV = S.kf.SigmaV;  cfg.SigmaW = S.kf.SigmaW;  cfg.SigmaX0 = S.kf.SigmaX0;
     cfg.flags = 1;                                         % MPCEKF_CF_BOUNDS: boundzk too
     if strcmp(S.kf.method, 'MB'), cfg.method = 1; end
-    h = mpcekf_mex('create', mpcekf_rom_struct(ROM), cfg, S.device, n);
+    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], unique(Tc(:)')), cfg, S.device, n);  % Tc on the table grid
     mpcekf_session('set', 'h', h);
     mpcekf_mex('init', h, reshape(initCfg.SOC0, 1, n), Tc .* ones(1, n));
     fn = ROM.cellData.function.neg;

@@ -1,11 +1,26 @@
-function R = mpcekf_rom_struct(ROM, ntheta, TdegC)
+function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC)
 % MPCEKF_ROM_STRUCT  The reference ROM struct (runMPC.m:5) as the plain arrays of the
 % library's mpcekf_rom (include/mpcekf.h): what mpcekf_mex('create', R, ...) takes and
-% what mpcekf_export_rom writes to JSON.  Defaults: ntheta = 101, TdegC = 6 points from
-% 10 degC below the coldest to 10 degC above the warmest ROM set-point.
+% what mpcekf_export_rom writes to JSON.
+% The electrode functions (k0, Rf, Cdleff, Uocp, dUocp) are tabulated on TdegC and
+% interpolated linearly in T between table temperatures; at a table temperature the
+% lookup is the handle's value exactly.  Default TdegC: the ROM set-point temperatures,
+% the simulation temperatures TC (default 25 degC, runMPC.m:8) and guard points 10 degC
+% beyond the coldest / warmest (T is clamped to the table range); spare slots up to 8
+% split the widest intervals.
+% Between table points an Arrhenius k0 interpolated linearly is off by about
+% h^2/8 (Ea/(R T^2))^2 (DESIGN.md 3: ~1.4 % at h = 5 K, Ea = 50 kJ/mol).
   if nargin < 2 || isempty(ntheta), ntheta = 101; end
+  if nargin < 4 || isempty(TC), TC = 25; end
   if nargin < 3 || isempty(TdegC)
-    TdegC = linspace(min(ROM.xraData.T) - 10, max(ROM.xraData.T) + 10, 6);
+    Ts = ROM.xraData.T(:)';
+    TdegC = unique([Ts, TC(:)']);
+    guard = [min(TdegC) - 10, max(TdegC) + 10];
+    if numel(TdegC) + 2 <= 8, TdegC = unique([guard(1), TdegC, guard(2)]); end
+    while numel(TdegC) < 8                  % spare slots halve the widest intervals
+      [~, k] = max(diff(TdegC));
+      TdegC = [TdegC(1:k), (TdegC(k) + TdegC(k + 1)) / 2, TdegC(k + 1:end)];
+    end
   end
   assert(numel(TdegC) >= 1 && numel(TdegC) <= 8 && all(diff(TdegC) > 0), ...
          'mpcekf_rom_struct: 1..8 ascending table temperatures');

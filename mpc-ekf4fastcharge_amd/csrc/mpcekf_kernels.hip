@@ -28,6 +28,18 @@ constexpr int NP = 5;                  // compiled horizon (runMPC.m:28)
 constexpr int NC = 2;                  // compiled control horizon (runMPC.m:29)
 constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 
+// k_cell build options (A/B knobs; the defaults are the measured best):
+// MPCEKF_REC_ONCE: corners whose whole record (xhat and Sigma) is read with the first
+// read; the others read Sigma at their update.  1: corner 0's Sigma is what the gains
+// use first; 2..4 hold more Sigma in registers and spill (measured no faster).
+// MPCEKF_CELL_OUTLINE: the Jacobi symmetrisation as a call instead of inline.
+#ifndef MPCEKF_REC_ONCE
+#define MPCEKF_REC_ONCE 1
+#endif
+#ifndef MPCEKF_CELL_OUTLINE
+#define MPCEKF_CELL_OUTLINE false
+#endif
+
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
 #define STAMP(i)                                                                          \
@@ -320,12 +332,13 @@ __device__ __forceinline__ void jacobi5(double a[NPK], double V[NX * NX]) {
 }
 
 // Positive definiteness of a packed symmetric 5x5 by LDL' pivots (orc_is_pd, same order).
-__device__ __forceinline__ bool is_pd5(const double a[NPK]) {
+// sc: a = sc * the given array (1.0: a itself), applied where an entry is read.
+__device__ __forceinline__ bool is_pd5(const double a[NPK], double sc = 1.0) {
   double l[NX][NX], d[NX];
   bool pd = true;
 #pragma unroll
   for (int j = 0; j < NX; ++j) {
-    double s = a[pk(j, j)];
+    double s = a[pk(j, j)] * sc;
 #pragma unroll
     for (int k = 0; k < j; ++k) s = __builtin_fma(-(l[j][k] * l[j][k]), d[k], s);
     pd = pd && (s > 0);
@@ -334,7 +347,7 @@ __device__ __forceinline__ bool is_pd5(const double a[NPK]) {
       const double inv = 1.0 / s;
 #pragma unroll
       for (int i = j + 1; i < NX; ++i) {
-        double t = a[pk(j, i)];
+        double t = a[pk(j, i)] * sc;
 #pragma unroll
         for (int k = 0; k < j; ++k) t = __builtin_fma(-(l[i][k] * l[j][k]), d[k], t);
         l[i][j] = t * inv;
@@ -389,7 +402,7 @@ __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], co
   double LS[NX];
 #pragma unroll
   for (int r = 0; r < NX; ++r) LS[r] = L[r] * St;
-  double Ps[NPK], a[NPK];
+  double Ps[NPK];
 #pragma unroll
   for (int r = 0; r < NX; ++r)
 #pragma unroll
@@ -398,25 +411,27 @@ __device__ __forceinline__ void meas_update_regs(double x[NX], double S[NPK], co
       double pcr = __builtin_fma(-LS[c], L[r], S[pk(r, c)]);
       Ps[pk(r, c)] = prc + pcr;
     }
-  // a = (P + P')/2: the same operation on the same sum, formed where it is used
-#pragma unroll
-  for (int i = 0; i < NPK; ++i) a[i] = Ps[i] * 0.5;
+  // a = (P + P')/2 = Ps * 0.5: the same operation on the same sum, formed where it is
+  // used (not held: an array of 15 doubles less at the kernel's register peak)
   const bool bump = res * res > 9 * St;
   // HH = VV*SS*VV' (iterEKF.m:145-146) is the polar factor of the symmetric part a:
   // a itself when a is positive definite (the usual case), else V|Lambda|V' (Jacobi).
   // The decomposition runs only if some lane of the wave needs it.
-  const bool pd = is_pd5(a);
+  const bool pd = is_pd5(Ps, 0.5);
   if (__all(pd)) {
 #pragma unroll
     for (int i = 0; i < NPK; ++i) {
-      double v = ((Ps[i] + a[i]) + a[i]) / 4.0;
+      const double a = Ps[i] * 0.5;
+      double v = ((Ps[i] + a) + a) / 4.0;
       if (bump) v = v * 2.0;
       S[i] = v;
     }
-  } else if constexpr (OUTLINE) {
-    meas_polar_slow(Ps, a, S, pd, bump);
   } else {
-    meas_polar<true>(Ps, a, S, pd, bump);
+    double a[NPK];
+#pragma unroll
+    for (int i = 0; i < NPK; ++i) a[i] = Ps[i] * 0.5;
+    if constexpr (OUTLINE) meas_polar_slow(Ps, a, S, pd, bump);
+    else meas_polar<true>(Ps, a, S, pd, bump);
   }
 }
 
@@ -689,13 +704,22 @@ using Cons = ConsT<NP, NC>;
 using MpcSetup = MpcSetupT<NP, NC>;
 
 // EKFmatsHandler.m:26-114.  zTE1.. are the role rows of zk, Zsoc = zk(end).
-template <int NZ>
-__device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
-                                             double Zsoc, double TK, Lin &L, double xend = 0.0) {
+// EKFmatsHandler.m:26-31: the corner of largest weight, first of equals; max()
+// skips NaN weights.
+__device__ __forceinline__ int corner_max(const XI &xi) {
   int imax = 0;
 #pragma unroll
   for (int j = 1; j < 4; ++j)
     if (xi.g[j] > xi.g[imax] || (xi.g[imax] != xi.g[imax] && xi.g[j] == xi.g[j])) imax = j;
+  return imax;
+}
+
+// xm: that corner's xhat when the caller holds it (k_cell's fused step), else read
+template <int NZ>
+__device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
+                                             double Zsoc, double TK, Lin &L, double xend = 0.0,
+                                             const double *xm = nullptr) {
+  const int imax = corner_max(xi);
   int m = xi.m[0];
 #pragma unroll
   for (int j = 1; j < 4; ++j)
@@ -704,7 +728,12 @@ __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, c
   const double *Dm = Cm + NZ * NX;
   const double *am = Dm + NZ;
   double x[NX];
-  load_x(cc.erec + (size_t)m * REC, x);
+  if (xm) {
+#pragma unroll
+    for (int k = 0; k < NX; ++k) x[k] = xm[k];
+  } else {
+    load_x(cc.erec + (size_t)m * REC, x);
+  }
 #pragma unroll
   for (int k = 0; k < NX; ++k) { L.xhat[k] = x[k]; L.a[k] = am[k]; }
   L.xhat[NX] = xend;  // ekfData.xhat(end) (EKFmatsHandler.m:33): 0 in 'OB', the MB integrator
@@ -1237,10 +1266,9 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
 #pragma unroll
     for (int b = 0; b < B; ++b) d2[i + b * nt] = v[b];
   }
-  double2 v[B];
+  double2 v[B];  // the remainder: clamped (in-bounds) loads, guarded stores
 #pragma unroll
-  for (int b = 0; b < B; ++b)
-    if (i + b * nt < n2) v[b] = s2[i + b * nt];
+  for (int b = 0; b < B; ++b) v[b] = s2[min(i + b * nt, n2 - 1)];
 #pragma unroll
   for (int b = 0; b < B; ++b)
     if (i + b * nt < n2) d2[i + b * nt] = v[b];
@@ -1798,6 +1826,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   };
 
   double Z[NZ];
+  double xmax[NX];         // fused step: EKFmatsHandler's corner xhat, from the EKF's registers
+  bool have_xmax = false;
   double vhat = 0.0, Zsoc = 0.0;
   XI xi;
   double ik = 0.0, vk = 0.0;
@@ -1960,20 +1990,23 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     STAMP(1);
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
     STAMP(2);
-    // The 4 corner models stay in registers from one load to one store: xhat now,
-    // Sigma at its measurement update, each advanced over the steps its (deferred)
-    // time update skipped.  A corner repeating an earlier one (single-set-point grids)
-    // is a duplicate: the reference updates that model twice in sequence.
+    // The 4 corner records are read once, whole (one round trip), advanced over the
+    // steps their (deferred) time update skipped, used by getVariables and the gains,
+    // updated and stored once; the updated xhat feeds the second getVariables and
+    // EKFmatsHandler when the second getXind names the same corners.  A corner repeating
+    // an earlier one (single-set-point grids) is a duplicate: the reference updates that
+    // model twice in sequence, the second time from the state the first update left.
     const int t = io.lazy_t;
     bool dup[4];
     int tsj[4];
-    double xr[4][NX];
+    double xr[4][NX], Sr[4][NPK];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       dup[j] = false;
 #pragma unroll
       for (int i = 0; i < j; ++i) dup[j] = dup[j] || xi.m[i] == xi.m[j];
-      load_x(cc.erec + (size_t)xi.m[j] * REC, xr[j]);
+      if (j < MPCEKF_REC_ONCE) load_rec(cc.erec + (size_t)xi.m[j] * REC, xr[j], Sr[j]);
+      else load_x(cc.erec + (size_t)xi.m[j] * REC, xr[j]);
       tsj[j] = t ? s.ts_ekf[c * r.NM + xi.m[j]] : 0;
     }
     const double pt = t ? s.hist_p[(size_t)(t % LAZY_H) * s.n + c] : 0.0;
@@ -2002,9 +2035,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     __builtin_amdgcn_sched_barrier(0);
     double ChatV[4][NX], C0;
     get_chatv<NZ>(r, cc, xi, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
-    double S1[NPK];
-    load_S(cc.erec + (size_t)xi.m[0] * REC, S1);
-    if (t) replay_S(S1, cc.L + xi.m[0] * cc.stride + NZ * NX + NZ, tsj[0], t, cf.SigmaW);
+    if (t) replay_S(Sr[0], cc.L + xi.m[0] * cc.stride + NZ * NX + NZ, tsj[0], t, cf.SigmaW);
     double St[4], Lg[4][NX];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -2013,7 +2044,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int cI = 0; cI < NX; ++cI) {
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < NX; ++k) acc = __builtin_fma(S1[pk(k, cI)], ChatV[j][k], acc);
+        for (int k = 0; k < NX; ++k) acc = __builtin_fma(Sr[0][pk(k, cI)], ChatV[j][k], acc);
         row[cI] = acc;
       }
       double acc = 0.0;
@@ -2034,6 +2065,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
     __builtin_amdgcn_sched_barrier(0);
     STAMP(5);
+    double xu[4][NX];  // corner j's xhat after its update
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       double *rec = cc.erec + (size_t)xi.m[j] * REC;
@@ -2043,27 +2075,44 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       } else {
 #pragma unroll
         for (int k = 0; k < NX; ++k) xj[k] = xr[j][k];
-        if (j == 0) {
+        if (j < MPCEKF_REC_ONCE) {
 #pragma unroll
-          for (int k = 0; k < NPK; ++k) Sj[k] = S1[k];
+          for (int k = 0; k < NPK; ++k) Sj[k] = Sr[j][k];
         } else {
           load_S(rec, Sj);
-          if (t) replay_S(Sj, cc.L + xi.m[j] * cc.stride + NZ * NX + NZ, tsj[j], t, cf.SigmaW);
         }
+        if (t && j > 0) replay_S(Sj, cc.L + xi.m[j] * cc.stride + NZ * NX + NZ, tsj[j], t, cf.SigmaW);
       }
-      meas_update_regs(xj, Sj, Lg[j], St[j], res);
+      meas_update_regs<MPCEKF_CELL_OUTLINE>(xj, Sj, Lg[j], St[j], res);
       store_rec(rec, xj, Sj);
       if (t) s.ts_ekf[c * r.NM + xi.m[j]] = t;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) xu[j][k] = xj[k];
       __builtin_amdgcn_sched_barrier(0);
     }
     STAMP(6);
     x0 = __builtin_fma(L0, res, x0);
     S0 = S0 - L0 * St0 * L0;
     SOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
+    int m1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) m1[j] = xi.m[j];
     get_xind(r.nT, r.nZ, Tp, Zp, cc.T, SOC, xi);
-    if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
+    // same corners: their xhat is in registers and current; else catch the new corners
+    // up and read them (their records are the stored ones)
+    const bool same = m1[0] == xi.m[0] && m1[1] == xi.m[1] && m1[2] == xi.m[2] && m1[3] == xi.m[3] &&
+                      !(dup[1] || dup[2] || dup[3]);
+    if (!same) {
+      if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) load_x(cc.erec + (size_t)xi.m[j] * REC, xu[j]);
+    }
     STAMP(7);
-    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc);
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xu);
+    const int jm = corner_max(xi);
+#pragma unroll
+    for (int k = 0; k < NX; ++k) xmax[k] = jm == 0 ? xu[0][k] : jm == 1 ? xu[1][k] : jm == 2 ? xu[2][k] : xu[3][k];
+    have_xmax = true;
     __builtin_amdgcn_sched_barrier(0);
     STAMP(8);
     s.warn[c] = warn;
@@ -2126,7 +2175,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { xi.m[j] = io.xm_in[c * 4 + j]; xi.g[j] = io.xg_in[c * 4 + j]; }
     }
-    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0);
+    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0, fused && (PARTS & P_EKF) && have_xmax ? xmax : nullptr);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
     if (io.x_out)
 #pragma unroll
