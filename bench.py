@@ -177,6 +177,9 @@ def main():
                     help="all ranks on device 0 with gloo timing collectives (1-GPU multi-rank test)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: rank/shard/timing orchestration only (CPU tests)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the process group and run the timing collectives at WORLD_SIZE 1 too "
+                         "(exercises the RCCL leg on a one-GPU box)")
     args = ap.parse_args()
     if not args.pmc:
         args.pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.np == 5 else f"pmc_traffic_np{args.np}.json")
@@ -194,15 +197,17 @@ def main():
     device = 0 if args.share_device else local
     import torch
     dist = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         if args.dry_run or args.share_device:
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    backend = dist.get_backend() if dist else "none"
     print(f"bench.py rank {rank}/{world}: cells [{lo}, {hi}) ({ncell}) on "
-          f"{'no device (dry run)' if args.dry_run else f'cuda:{device}'}", file=sys.stderr, flush=True)
+          f"{'no device (dry run)' if args.dry_run else f'cuda:{device}'}, process group: {backend}",
+          file=sys.stderr, flush=True)
     K, W = args.steps, args.warmup
     coll_dev = torch.device("cpu") if (args.dry_run or args.share_device) else torch.device("cuda", device)
 
@@ -287,6 +292,7 @@ def main():
                 "Np": args.np, "Nc": args.nc, "models_per_cell": rom.NM if rom else None,
                 "rom_outputs": rom.nz if rom else None,
                 "parallelism": f"cell-shard x{world} (no data-path collective)",
+                "timing_collectives": backend,
                 "step_window": [W, W + K], "mean_nexec": round(mean_nexec, 3),
             },
         }

@@ -39,6 +39,10 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_CELL_OUTLINE
 #define MPCEKF_CELL_OUTLINE false
 #endif
+// k_hild: rows of LDS operand prefetch in the fast sweep
+#ifndef MPCEKF_HILD_PF
+#define MPCEKF_HILD_PF 3
+#endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
@@ -1042,14 +1046,22 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     v1 = __builtin_fma(x.y, L[j], v1);
   }
   asm volatile("" ::: "memory");
-  // row i's slots are read one row ahead: ds_read latency (~76 cycles) stays off the chain
-  double2 xc = hx(hl, 0), hc = hh(hl, 0);
+  // row i's slots are read MPCEKF_HILD_PF rows ahead: ds_read latency (~76 cycles idle,
+  // more under load) stays off the chain; one row ahead left ~10 instructions between a
+  // read and its use
+  constexpr int PF = MPCEKF_HILD_PF;
+  double2 xq[PF], hq[PF];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    xq[p] = hx(hl, p < NCON ? p : NCON - 1);
+    hq[p] = hh(hl, p < NCON ? p : NCON - 1);
+  }
 #pragma unroll
   for (int i = 0; i < NCON; ++i) {
-    double2 xn = xc, hn = hc;
-    if (i + 1 < NCON) {
-      xn = hx(hl, i + 1);
-      hn = hh(hl, i + 1);
+    const double2 xc = xq[i % PF], hc = hq[i % PF];
+    if (i + PF < NCON) {
+      xq[i % PF] = hx(hl, i + PF);
+      hq[i % PF] = hh(hl, i + PF);
     }
     double t = __builtin_fma(Mf(i, 0), v0, K[i]);
     t = __builtin_fma(Mf(i, 1), v1, t);
@@ -1066,8 +1078,6 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     L[i] = nl;
     v0 = __builtin_fma(xc.x, d, v0);
     v1 = __builtin_fma(xc.y, d, v1);
-    xc = xn;
-    hc = hn;
   }
   vfin = isfinite(v0) && isfinite(v1);
 }

@@ -180,7 +180,9 @@ def test_zk_and_boundzk_match_oracle(rom, oc, M):
     _bitwise(zb, ref["zbk"], "boundzk")
 
 
-def test_checkpoint_restore_is_exact(rom, M):
+def test_checkpoint_restore_is_exact(rom, oc, M):
+    """get_state / set_state mid-run: the rerun from the checkpoint gives the first run's
+    bits, and both are the C oracle's uninterrupted trajectory (steps 15-40)."""
     n = 2048
     soc0, tc = batch_inputs(n, seed=5)
     with M.Context(rom, n) as ctx:
@@ -190,8 +192,10 @@ def test_checkpoint_restore_is_exact(rom, M):
         a = ctx.step(25)
         ctx.set_state(snap)
         b = ctx.step(25)
+    ref = oc.run(rom, soc0, tc, 40, nthreads=8)
     for k in ("u", "v", "soc", "phise", "nexec"):
         np.testing.assert_array_equal(a[k], b[k])
+        _bitwise(b[k], ref[k][15:], k)
 
 
 def test_runmpc_cell_full_charge(rom, oc, M):
@@ -425,15 +429,18 @@ def test_model_blend_stage_entry_points_match_fused(rom, M):
             np.testing.assert_array_equal(ne, fused["nexec"][k])
 
 
-def test_lane_quad_ekf_kernel_is_exact(rom, M):
+def test_lane_quad_ekf_kernel_is_exact(rom, oc, M):
     """k_ekf4 (iterEKF with a lane quad per cell, MPCEKF_QUAD=1) gives the bits of the
-    lane-per-cell k_cell path over a closed loop, state included."""
+    lane-per-cell k_cell path over a closed loop, state included, and both are the C
+    oracle's trajectories."""
     n = 700
     soc0, tc = batch_inputs(n, seed=31)
     a = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=0)
     b = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=1)
+    ref = oc.run(rom, soc0, tc, 120, nthreads=8)
     for k in ("u", "v", "soc", "phise", "nexec"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        _bitwise(b[k], ref[k], k)
     for k in ("ekf", "bigX", "scal", "lam"):
         np.testing.assert_array_equal(a["state"][k], b["state"][k], err_msg=k)
 
@@ -473,9 +480,10 @@ def test_generic_hildreth_any_size_matches_oracle(oc, M, Nc, ncon, n):
     assert (ne == 100).any() and (ne < 100).any()
 
 
-def test_graph_replay_is_exact(rom, M):
+def test_graph_replay_is_exact(rom, oc, M):
     """mpcekf_set_graph: repeated call shapes replayed from captured hipGraphs give the
-    bits of direct launches (calls of 1 and 5 steps, shapes alternating, host outputs)."""
+    bits of direct launches (calls of 1 and 5 steps, shapes alternating, host outputs),
+    and the concatenated trajectory is the C oracle's."""
     n = 192
     soc0, tc = batch_inputs(n, seed=21)
     runs = []
@@ -496,3 +504,32 @@ def test_graph_replay_is_exact(rom, M):
             _bitwise(x[k], y[k], k)
     for k in ("bigX", "ekf", "scal", "lam", "status"):
         _bitwise(sa[k], sb[k], k)
+    ref = oc.run(rom, soc0, tc, sum(o["u"].shape[0] for o in b), nthreads=4)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        _bitwise(np.concatenate([o[k] for o in b]), ref[k], k)
+
+
+@pytest.mark.parametrize("Np,Nc", [(5, 2), (20, 10)])
+def test_graph_replay_temperature_profile_and_diagnostics(oc, M, P, Np, Nc):
+    """Graph replay with a temperature profile per call (the profile buffer is part of the
+    captured shape, its contents change every call), the cost log and the stability
+    diagnostics, at both horizons: replayed calls equal direct launches and the C
+    oracle's trajectory with the same profile."""
+    rom = P.make_synth_rom()
+    n, calls, ns = 64, 8, 3
+    soc0, tc = batch_inputs(n, seed=61)
+    prof = tc[None, :] + 2.5 * np.sin(np.arange(calls * ns)[:, None] / 4.0 + np.arange(n)[None, :] / 7.0)
+    names = ("u", "v", "soc", "phise", "nexec", "J_unc", "J_fin", "norm_du", "nviol", "poles", "sv")
+    runs = []
+    for graph in (False, True):
+        with M.Context(rom, n, M.make_config(Np=Np, Nc=Nc)) as ctx:
+            ctx.init_cells(soc0, tc)
+            ctx.set_graph(graph)
+            runs.append([ctx.step(ns, outputs=names, tc=prof[c * ns:(c + 1) * ns]) for c in range(calls)])
+    for x, y in zip(*runs):
+        for k in names:
+            _bitwise(x[k], y[k], k)
+    ref = oc.run(rom, soc0, tc, calls * ns, nthreads=4, traj=True, tc_traj=prof, Np=Np, Nc=Nc)
+    for k, rk in dict(u="u", v="v", soc="soc", phise="phise", nexec="nexec", J_unc="J_unc", J_fin="J_fin",
+                      norm_du="norm_du", nviol="nviol").items():
+        _bitwise(np.concatenate([o[k] for o in runs[1]]), ref[rk], k)

@@ -51,17 +51,20 @@ def test_rom_size_sensitivity_matches_oracle(P, oc, M, temps, socs, method):
     np.testing.assert_array_equal(st["status"], ref["status"])
 
 
-def test_rom_global_layout_matches_lds_layout(P, M):
+def test_rom_global_layout_matches_lds_layout(P, oc, M):
     """MPCEKF_ROM_GLOBAL=1 at NM = 63 gives the LDS layout's bits, state included, through
-    k_cell, the lane-quad k_ekf4 (MPCEKF_QUAD=1) and k_bounds."""
+    k_cell, the lane-quad k_ekf4 (MPCEKF_QUAD=1) and k_bounds; every run is the C
+    oracle's trajectory."""
     rom = P.make_synth_rom()
     n = 640
     soc0, tc = batch_inputs(n, seed=43)
+    ref = oc.run(rom, soc0, tc, 150, nthreads=8)
     for quad in (0, 1):
         a = _run_with_env(M, rom, soc0, tc, 150, MPCEKF_QUAD=quad, MPCEKF_ROM_GLOBAL=0)
         b = _run_with_env(M, rom, soc0, tc, 150, MPCEKF_QUAD=quad, MPCEKF_ROM_GLOBAL=1)
         for k in ("u", "v", "soc", "phise", "nexec"):
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"quad={quad} {k}")
+            _bitwise(b[k], ref[k], f"quad={quad} {k}")
         for k in ("ekf", "bigX", "scal", "lam"):
             np.testing.assert_array_equal(a["state"][k], b["state"][k], err_msg=f"quad={quad} {k}")
 
