@@ -39,6 +39,10 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_CELL_OUTLINE
 #define MPCEKF_CELL_OUTLINE false
 #endif
+// k_flush: the next cell's loads issued before this cell's replay
+#ifndef MPCEKF_FLUSH_PF
+#define MPCEKF_FLUSH_PF 1
+#endif
 // k_hild: rows of LDS operand prefetch in the fast sweep
 #ifndef MPCEKF_HILD_PF
 #define MPCEKF_HILD_PF 3
@@ -1491,31 +1495,48 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
     for (int e = 0; e < REC; ++e) ce[e] = cC[(size_t)mm * REC + e];
 #pragma unroll
     for (int e = 0; e < 6; ++e) cp[e] = cP[(size_t)mm * 6 + e];
-    for (int64_t c = w0; c < s.n; c += nw) {
-      const double hpl = s.hist_p[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
-      const double hul = s.hist_u[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+    // software pipelined over the wave's cells: the next cell's rings, timestamps and
+    // records are loaded while this cell replays, so every wave keeps a cell's 13.6 KB
+    // in flight (MPCEKF_FLUSH_PF = 0: load, replay, store in turn)
+    struct FCell {
+      double hpl, hul, xe[REC], xp[6];
+      int tse, tsp;
+    };
+    auto fload = [&](int64_t c, FCell &F) {
+      F.hpl = s.hist_p[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+      F.hul = s.hist_u[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
       // MB never time-updates the per-model EKF records (iterEKF.m:90-102)
-      const int tse = (act && !(cf.flags & KF_MB)) ? s.ts_ekf[c * NM + m] : t;
-      const int tsp = act ? s.ts_plant[c * NM + m] : t;
+      F.tse = (act && !(cf.flags & KF_MB)) ? s.ts_ekf[c * NM + m] : t;
+      F.tsp = act ? s.ts_plant[c * NM + m] : t;
+      const double2 *re = reinterpret_cast<const double2 *>(s.ekf + ((size_t)c * NM + mm) * REC);
+      const double2 *rp = reinterpret_cast<const double2 *>(s.bigx + ((size_t)c * NM + mm) * 6);
+#pragma unroll
+      for (int e = 0; e < REC / 2; ++e) {
+        const double2 v = re[e];
+        F.xe[2 * e] = v.x;
+        F.xe[2 * e + 1] = v.y;
+      }
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const double2 v = rp[e];
+        F.xp[2 * e] = v.x;
+        F.xp[2 * e + 1] = v.y;
+      }
+    };
+    FCell cur;
+    if (MPCEKF_FLUSH_PF && w0 < s.n) fload(w0, cur);
+    for (int64_t c = w0; c < s.n; c += nw) {
+      FCell nx;
+      if (MPCEKF_FLUSH_PF) {
+        if (c + nw < s.n) fload(c + nw, nx);
+      } else {
+        fload(c, cur);
+      }
+      const double hpl = cur.hpl, hul = cur.hul;
+      const int tse = cur.tse, tsp = cur.tsp;
       double2 *re = reinterpret_cast<double2 *>(s.ekf + ((size_t)c * NM + mm) * REC);
       double2 *rp = reinterpret_cast<double2 *>(s.bigx + ((size_t)c * NM + mm) * 6);
-      double xe[REC], xp[6];
-      if (tse < t) {
-#pragma unroll
-        for (int e = 0; e < REC / 2; ++e) {
-          const double2 v = re[e];
-          xe[2 * e] = v.x;
-          xe[2 * e + 1] = v.y;
-        }
-      }
-      if (tsp < t) {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          const double2 v = rp[e];
-          xp[2 * e] = v.x;
-          xp[2 * e + 1] = v.y;
-        }
-      }
+      double *xe = cur.xe, *xp = cur.xp;
       int kmin = min(tse, tsp);
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) kmin = min(kmin, __shfl_xor(kmin, o));
@@ -1545,6 +1566,7 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
         s.ts_ekf[c * NM + m] = new_ts;
         s.ts_plant[c * NM + m] = new_ts;
       }
+      if (MPCEKF_FLUSH_PF) cur = nx;
     }
   }
 }
@@ -3135,8 +3157,10 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
 int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream) {
   if (s.n == 0) return 0;
   static_assert((LAZY_H & (LAZY_H - 1)) == 0 && LAZY_H <= 64, "k_flush: ring slots live in lanes");
-  // persistent waves: 3 per SIMD (k_flush holds ~140 VGPRs), striding over cells
-  const int64_t waves = s.n < 3072 ? s.n : 3072;
+  // persistent waves striding over cells, as many as fit: 2 per SIMD with the pipelined
+  // loads (210 VGPRs), 3 without (150)
+  const int64_t wmax = MPCEKF_FLUSH_PF ? 2048 : 3072;
+  const int64_t waves = s.n < wmax ? s.n : wmax;
   hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts);
   return (int)hipGetLastError();
 }
