@@ -119,3 +119,18 @@ def test_bench_refuses_world_size_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, env=e, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_bench_force_dist_at_world_size_one():
+    """--force-dist creates the process group at WORLD_SIZE 1 (the RCCL leg on a one-GPU
+    box; gloo here with --dry-run) and runs the timing collectives through it; without it
+    a single rank runs no collective."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    line, err = _bench("--gpus", "1", "--dry-run", "--force-dist", "--steps", "3", env=env)
+    assert "process group: gloo" in err and line["config"]["timing_collectives"] == "gloo"
+    line, err = _bench("--gpus", "1", "--dry-run", "--steps", "3")
+    assert "process group: none" in err and line["config"]["timing_collectives"] == "none"
