@@ -312,9 +312,15 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
     """Rank 0's roofline / per-kernel / CPU-baseline objects (rank 0's shard timings)."""
     ncon = 4 * args.nc + 3 * args.np
     bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
-    # HIP-event averages over the sampled launches (--timing-every); every flush step is
-    # sampled, so a kernel's share of a step is its average x its launches per step
-    n_flush = K // 32 + (1 if K % 32 else 0)
+    # HIP-event averages over the sampled launches (--timing-every), so a kernel's share of
+    # a step is its average x its launches per step.  k_flush flushes every cell each period
+    # steps (the library default; every flush step is sampled); the rolling schedule
+    # (MPCEKF_FLUSH_ROLL=1) flushes one slice of ncell / period cells every step on a second
+    # stream beside k_bounds / Hildreth
+    period = int(os.environ.get("MPCEKF_FLUSH_PERIOD", "32"))
+    roll = os.environ.get("MPCEKF_FLUSH_ROLL", "0") != "0"
+    n_flush = K if roll else K // period + (1 if K % period else 0)
+    cells_per_launch = {k: (ncell / period if (k == "flush" and roll) else ncell) for k in tim}
     per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches_timed=tim[k][1],
                           launches=(n_flush if k == "flush" else K))
                   for k in tim if tim[k][1] > 0}
@@ -323,7 +329,7 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
     # the dominant kernel = the largest share of the timed region (k_flush runs every 32 steps)
     dom = max(per_kernel, key=lambda k: per_kernel[k]["ms_total"])
     ms = per_kernel[dom]["ms_per_launch"]
-    achieved = bpc[dom] * ncell / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    achieved = bpc[dom] * cells_per_launch[dom] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
     pmc = {}
     if os.path.exists(args.pmc):
         try:
@@ -351,7 +357,7 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
             "traffic_source": (os.path.relpath(args.pmc, ROOT) if traffic is not None else
                                f"null: {os.path.relpath(args.pmc, ROOT)} was not measured on this build "
                                f"({build_id}) and workload"),
-            "algorithmic_bytes_per_cell": bpc[dom], "cells_per_launch": ncell,
+            "algorithmic_bytes_per_cell": bpc[dom], "cells_per_launch": cells_per_launch[dom],
             "fp64": fp64,
             "step_equivalent": {
                 "bytes_per_cell_step": survey_bytes_per_cell_step(rom.NM, ncon),
@@ -363,7 +369,8 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
         "kernels": {k: dict(ms_per_launch=round(v["ms_per_launch"], 5), launches=v["launches"],
                             launches_timed=v["launches_timed"],
                             ms_per_step=round(v["ms_total"] / K, 5) if K else None,
-                            gbs_algorithmic=round(bpc[k] * ncell / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
+                            cells_per_launch=cells_per_launch[k],
+                            gbs_algorithmic=round(bpc[k] * cells_per_launch[k] / (v["ms_per_launch"] * 1e-3) / 1e9, 1)
                             if v["ms_per_launch"] > 0 else None)
                     for k, v in per_kernel.items()},
         "cpu_baseline": cpu,

@@ -89,6 +89,13 @@ struct mpcekf_ctx {
   double *d_lin = nullptr, *d_zsoc = nullptr;  // [n][35], [n]
   double *d_uk1p = nullptr;                      // [n] uk_1 before the step (poles / sv)
   int flush_period = LAZY_H;      // steps between all-model flushes (<= LAZY_H)
+  // rolling flush (MPCEKF_FLUSH_ROLL=1, off by default): step t flushes the cell slice
+  // t % flush_period on fstream, forked after k_cell and joined before the next step's k_plant.
+  // Measured slower (0.287 vs 0.257 ms per step at 65,536 cells, profiles/r03m_roll_ab.txt):
+  // every kernel of the step slows by 5-10 us once the step crosses streams.
+  bool flush_roll = false;
+  hipStream_t fstream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -486,7 +493,14 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   if (const char *e = std::getenv("MPCEKF_QUAD")) X->quad = quad_ok && std::atoi(e) != 0;
   if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) X->ekf4_block = std::atoi(e) == 1024 ? 1024 : 512;
   if (const char *e = std::getenv("MPCEKF_GRAPH")) X->graph = std::atoi(e) != 0;  // as mpcekf_set_graph
+  // MPCEKF_FLUSH_ROLL=1: the rolling flush schedule (results identical)
+  if (const char *e = std::getenv("MPCEKF_FLUSH_ROLL")) X->flush_roll = std::atoi(e) != 0;
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
+  if (e == hipSuccess && X->flush_roll) {
+    e = hipStreamCreateWithFlags(&X->fstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_join, hipEventDisableTiming);
+  }
   if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
   const size_t n = (size_t)ncells, NM = (size_t)X->NM;
   KState &s = X->s;
@@ -546,7 +560,10 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (!X) return MPCEKF_OK;
   (void)hipSetDevice(X->device);
   if (X->stream) (void)hipStreamSynchronize(X->stream);
+  if (X->fstream) (void)hipStreamSynchronize(X->fstream);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
+  if (X->ev_fork) (void)hipEventDestroy(X->ev_fork);
+  if (X->ev_join) (void)hipEventDestroy(X->ev_join);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
@@ -554,6 +571,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);
+  if (X->fstream) (void)hipStreamDestroy(X->fstream);
   if (X->stream) (void)hipStreamDestroy(X->stream);
   delete X;
   return MPCEKF_OK;
@@ -702,7 +720,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   // and the uk_1 the step's iterMPC used
   const bool diag = f[12].dev || f[13].dev;
   if (diag && (rc = X->diag_bufs())) return rc;
-  constexpr int NEV = 6;  // events per step: plant | cell | bounds | hild | flush |
+  constexpr int NEV = 7;  // events per step: plant | cell | bounds | hild (+ diag) |, then | flush |
   if (X->timing && X->ev.size() < (size_t)nsteps * NEV) {
     size_t old = X->ev.size();
     X->ev.resize((size_t)nsteps * NEV);
@@ -712,6 +730,20 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   // touches (k_plant: plant corners, k_cell: EKF corners); k_flush brings every model
   // current each LAZY_H steps and at the end of the call, so between calls (stage entry
   // points, get/set_state) every model is current, exactly as after eager updates.
+  //
+  // Rolling schedule (flush_roll, MPCEKF_FLUSH_ROLL=1): step t < nsteps flushes only the cells of
+  // slice t % P (P = flush_period; slice j = [j n / P, (j + 1) n / P)), so each cell is still
+  // flushed every P steps and no replay needs more than P <= LAZY_H ring entries.  The slice
+  // runs on fstream, forked after k_cell and joined before the next step's k_plant: k_bounds
+  // and Hildreth read no timestamp, ring or model record that k_flush writes (k_flush stores
+  // only records older than t, and k_bounds reads the corner k_cell updated at t), and
+  // k_plant(t + 1) overwrites the ring slot of step t + 1 - LAZY_H only after the join.  The
+  // last step flushes every cell on the step's stream (timestamps 0, as before).  Under graph
+  // capture the slices stay on the step's stream (same bits, no overlap).
+  const bool capturing = X->graph && !X->timing && nsteps > 0;
+  const bool roll = X->flush_roll;
+  const bool fork = roll && X->fstream && !capturing;
+  const int P = X->flush_period;
   std::vector<char> flushed((size_t)nsteps, 0);
   auto run_steps = [&]() -> int {
     for (int k = 0; k < nsteps; ++k) {
@@ -782,6 +814,22 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         return rc;
       }
       if (E) HIPCHK(hipEventRecord(E[2], X->stream));
+      const bool slice = roll && t < nsteps;
+      if (slice) {
+        const int j = t % P;
+        const int64_t lo = n * j / P, hi = n * (j + 1) / P;
+        hipStream_t fs = X->stream;
+        if (fork) {
+          HIPCHK(hipEventRecord(X->ev_fork, X->stream));
+          HIPCHK(hipStreamWaitEvent(X->fstream, X->ev_fork, 0));
+          fs = X->fstream;
+        }
+        if (E) HIPCHK(hipEventRecord(E[5], fs));
+        if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t, fs, lo, hi), "flush"))) return rc;
+        if (E) HIPCHK(hipEventRecord(E[6], fs));
+        if (fork) HIPCHK(hipEventRecord(X->ev_join, fs));
+        flushed[k] = hi > lo;
+      }
       // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
       if (bounds && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
       if (E) HIPCHK(hipEventRecord(E[3], X->stream));
@@ -797,15 +845,18 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         if ((rc = lerr(rc, "cl_diag"))) return rc;
       }
       if (E) HIPCHK(hipEventRecord(E[4], X->stream));
-      if (t % X->flush_period == 0 || t == nsteps) {
+      if (slice && fork) HIPCHK(hipStreamWaitEvent(X->stream, X->ev_join, 0));
+      if (roll ? t == nsteps : (t % P == 0 || t == nsteps)) {
+        const bool timed = E && !roll;  // the rolling schedule times its slices only
+        if (timed) HIPCHK(hipEventRecord(E[5], X->stream));
         if ((rc = lerr(launch_flush(X->r, X->k, X->s, t, t == nsteps ? 0 : t, X->stream), "flush"))) return rc;
-        flushed[k] = 1;
+        if (timed) HIPCHK(hipEventRecord(E[6], X->stream));
+        flushed[k] = timed;
       }
-      if (E) HIPCHK(hipEventRecord(E[5], X->stream));
     }
     return MPCEKF_OK;
   };
-  if (X->graph && !X->timing && nsteps > 0) {
+  if (capturing) {
     // the call's launches depend only on these (kernel arguments are call-relative:
     // lazy_t = 1..nsteps, the flush schedule, the output rows), so a repeated call shape
     // replays one instantiated graph instead of 5-7 launches per step
@@ -826,13 +877,15 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     HIPCHK(hipMemcpyAsync(X->d_zbk, row(7, nsteps - 1), n * nzz * 8, hipMemcpyDeviceToDevice, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   if (X->timing) {
-    static const int slot[NEV - 1] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_BOUNDS, MPCEKF_K_HILD, MPCEKF_K_FLUSH};
+    // (start, end) events of plant, cell, bounds, hild, flush
+    static const int slot[5] = {MPCEKF_K_PLANT, MPCEKF_K_CELL, MPCEKF_K_BOUNDS, MPCEKF_K_HILD, MPCEKF_K_FLUSH};
+    static const int e0[5] = {0, 1, 2, 3, 5};
     for (int k = 0; k < nsteps; ++k)
-      for (int j = 0; j < NEV - 1; ++j) {
+      for (int j = 0; j < 5; ++j) {
         if ((k + 1) % X->timing_every != 0 && k != nsteps - 1) continue;
         if ((j == 4 && !flushed[k]) || (j == 2 && !bounds)) continue;
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + j], X->ev[(size_t)k * NEV + j + 1]));
+        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + e0[j]], X->ev[(size_t)k * NEV + e0[j] + 1]));
         X->t_ms[slot[j]] += ms;
         X->t_n[slot[j]] += 1;
       }

@@ -1479,7 +1479,7 @@ __device__ __forceinline__ double rl64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
 }
 __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, const KState s, const int t,
-                                               const int new_ts) {
+                                               const int new_ts, const int64_t c_lo, const int64_t c_hi) {
   const int NM = r.NM;
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -1524,11 +1524,11 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
       }
     };
     FCell cur;
-    if (MPCEKF_FLUSH_PF && w0 < s.n) fload(w0, cur);
-    for (int64_t c = w0; c < s.n; c += nw) {
+    if (MPCEKF_FLUSH_PF && c_lo + w0 < c_hi) fload(c_lo + w0, cur);
+    for (int64_t c = c_lo + w0; c < c_hi; c += nw) {
       FCell nx;
       if (MPCEKF_FLUSH_PF) {
-        if (c + nw < s.n) fload(c + nw, nx);
+        if (c + nw < c_hi) fload(c + nw, nx);
       } else {
         fload(c, cur);
       }
@@ -3154,14 +3154,18 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
   return (int)hipGetLastError();
 }
 
-int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream) {
-  if (s.n == 0) return 0;
+int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream, int64_t c_lo,
+                 int64_t c_hi) {
+  if (c_hi < 0 || c_hi > s.n) c_hi = s.n;
+  if (c_lo < 0) c_lo = 0;
+  if (c_hi <= c_lo) return 0;
   static_assert((LAZY_H & (LAZY_H - 1)) == 0 && LAZY_H <= 64, "k_flush: ring slots live in lanes");
   // persistent waves striding over cells, as many as fit: 2 per SIMD with the pipelined
   // loads (210 VGPRs), 3 without (150)
   const int64_t wmax = MPCEKF_FLUSH_PF ? 2048 : 3072;
-  const int64_t waves = s.n < wmax ? s.n : wmax;
-  hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts);
+  const int64_t waves = c_hi - c_lo < wmax ? c_hi - c_lo : wmax;
+  hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts,
+                     c_lo, c_hi);
   return (int)hipGetLastError();
 }
 

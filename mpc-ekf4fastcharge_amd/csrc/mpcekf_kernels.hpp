@@ -135,7 +135,9 @@ struct KWide {
 int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
                  void *stream);
 // brings every model of every cell from its ts to step t, then sets ts = new_ts
-int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream);
+// every model of cells [c_lo, c_hi) (c_hi < 0: to the end) brought to step t, timestamps new_ts
+int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_ts, void *stream, int64_t c_lo = 0,
+                 int64_t c_hi = -1);
 int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iapp, int do_plant, int do_ekf,
                 void *stream);
 int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int parts = P_ALL);

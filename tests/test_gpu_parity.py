@@ -257,10 +257,13 @@ def _run_with_env(M, rom, soc0, tc, steps, **env):
 
 
 def test_flush_period_is_exact(rom, M):
-    """The deferred time update gives the same bits for any flush period <= the ring."""
-    n = 1024
+    """The deferred time update gives the same bits for any flush period <= the ring, with
+    every cell flushed at once on the step's stream (the default) and with the rolling
+    schedule (MPCEKF_FLUSH_ROLL=1: one cell slice per step on a second stream)."""
+    n = 1000  # slices of unequal size for P = 7 and 32
     soc0, tc = batch_inputs(n, seed=22)
-    runs = [_run_with_env(M, rom, soc0, tc, 300, MPCEKF_FLUSH_PERIOD=p) for p in (32, 1, 7)]
+    runs = [_run_with_env(M, rom, soc0, tc, 300, MPCEKF_FLUSH_PERIOD=p, MPCEKF_FLUSH_ROLL=roll)
+            for p, roll in ((32, 0), (1, 0), (7, 0), (32, 1), (7, 1))]
     for r in runs[1:]:
         for k in ("u", "v", "soc", "phise", "nexec"):
             np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)
