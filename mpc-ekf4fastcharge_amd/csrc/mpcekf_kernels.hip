@@ -1280,12 +1280,17 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
 #pragma unroll
     for (int b = 0; b < B; ++b) d2[i + b * nt] = v[b];
   }
-  double2 v[B];  // the remainder: clamped (in-bounds) loads, guarded stores
+  // The remainder: clamped loads AND clamped stores, no branch.  With guarded stores the
+  // compiler sank each load into its store's branch, so the remainder (up to 15 chunks per
+  // lane for the cell blob) waited one L2 round trip per chunk.  Lanes past the end store
+  // the last chunk's own value to the last chunk: the same bytes, whichever lane lands.
+  if (n2 > 0) {
+    double2 v[B];
 #pragma unroll
-  for (int b = 0; b < B; ++b) v[b] = s2[min(i + b * nt, n2 - 1)];
+    for (int b = 0; b < B; ++b) v[b] = s2[min(i + b * nt, n2 - 1)];
 #pragma unroll
-  for (int b = 0; b < B; ++b)
-    if (i + b * nt < n2) d2[i + b * nt] = v[b];
+    for (int b = 0; b < B; ++b) d2[min(i + b * nt, n2 - 1)] = v[b];
+  }
   if ((len & 1) && threadIdx.x == 0) dst[len - 1] = src[len - 1];
 }
 
