@@ -47,6 +47,9 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_HILD_PF
 #define MPCEKF_HILD_PF 3
 #endif
+#ifndef MPCEKF_HILD_REGROWS  // k_hild: the constant rows' X / H_ii slots in registers
+#define MPCEKF_HILD_REGROWS 1
+#endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
@@ -1038,14 +1041,31 @@ __device__ __forceinline__ void hild_unstage(const double2 *hl, XS &Xs) {
 // reference's inf-norm test, hildreth.m:39), max / min |numerator| (div_fast's
 // dividend domain) and whether v ended finite (false once any d was not finite: inf
 // and NaN stay in v).
-__device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double K[NCON], double L[NCON],
+// The constant rows 0-7 ([Cu; -Cu; I; -I]) use 3 of the 18 slots (X: +-a, +-b, +-c; their
+// (H_ii, 1/H_ii)): those 6 pairs are held in registers (xr3 / hr3, read back from the
+// lane's LDS slots once per solve), so a sweep reads LDS for the 15 Toeplitz rows only.
+// At 4 waves per CU in the maxIter window the two ds_read_b128 per row were as long as
+// the row's dependent chain.
+constexpr int HILD_REG_ROWS = MPCEKF_HILD_REGROWS ? 4 * NC : 0;
+__device__ __forceinline__ double2 hx_r(const double2 *hl, const double2 xr3[3], int i) {
+  if (i < HILD_REG_ROWS) {
+    const double2 x = xr3[hslot(i)];
+    return hneg(i) ? make_double2(-x.x, -x.y) : x;
+  }
+  return hx(hl, i);
+}
+__device__ __forceinline__ double2 hh_r(const double2 *hl, const double2 hr3[3], int i) {
+  return i < HILD_REG_ROWS ? hr3[hslot(i)] : hh(hl, i);
+}
+__device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double2 xr3[3],
+                                           const double2 hr3[3], const double K[NCON], double L[NCON],
                                            double &dmax, double &xmax, double &xmin, bool &vfin) {
   ConsM Mf{Cn};
   asm volatile("" ::: "memory");  // reload the LDS slots each sweep (no hoisting)
   double v0 = 0.0, v1 = 0.0;
 #pragma unroll
   for (int j = 0; j < NCON; ++j) {
-    const double2 x = hx(hl, j);
+    const double2 x = hx_r(hl, xr3, j);
     v0 = __builtin_fma(x.x, L[j], v0);
     v1 = __builtin_fma(x.y, L[j], v1);
   }
@@ -1057,15 +1077,15 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
   double2 xq[PF], hq[PF];
 #pragma unroll
   for (int p = 0; p < PF; ++p) {
-    xq[p] = hx(hl, p < NCON ? p : NCON - 1);
-    hq[p] = hh(hl, p < NCON ? p : NCON - 1);
+    xq[p] = hx_r(hl, xr3, p < NCON ? p : NCON - 1);
+    hq[p] = hh_r(hl, hr3, p < NCON ? p : NCON - 1);
   }
 #pragma unroll
   for (int i = 0; i < NCON; ++i) {
     const double2 xc = xq[i % PF], hc = hq[i % PF];
     if (i + PF < NCON) {
-      xq[i % PF] = hx(hl, i + PF);
-      hq[i % PF] = hh(hl, i + PF);
+      xq[i % PF] = hx_r(hl, xr3, i + PF);
+      hq[i % PF] = hh_r(hl, hr3, i + PF);
     }
     double t = __builtin_fma(Mf(i, 0), v0, K[i]);
     t = __builtin_fma(Mf(i, 1), v1, t);
@@ -1176,6 +1196,12 @@ __device__ __forceinline__ bool hild_fast(const Cons &Cn, const double E[NC][NC]
     hild_x(Cn, E, Xs, fin);
     yok = hild_stage(Cn, Xs, hl);
   }
+  double2 xr3[3], hr3[3];  // slots 0-2 (the constant rows'), the staged bits
+#pragma unroll
+  for (int sl = 0; sl < 3; ++sl) {
+    xr3[sl] = hl[sl * 64];
+    hr3[sl] = hl[(HS_X + sl) * 64];
+  }
   nexec = maxIter;
   bool lok = true;
 #pragma unroll
@@ -1187,7 +1213,7 @@ __device__ __forceinline__ bool hild_fast(const Cons &Cn, const double E[NC][NC]
     if (__all(!active)) break;
     double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
     bool vfin;
-    sweep_fast(Cn, hl, K, L, dmax, xmax, xmin, vfin);
+    sweep_fast(Cn, hl, xr3, hr3, K, L, dmax, xmax, xmin, vfin);
     const bool bad = !(vfin && xmax <= 0x1p400 && xmin >= 0x1p-400);
     const bool conv = dmax < tol;
     const bool newconv = active && !bad && conv;
