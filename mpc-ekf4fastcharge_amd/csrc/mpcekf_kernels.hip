@@ -50,6 +50,9 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_HILD_REGROWS  // k_hild: the constant rows' X / H_ii slots in registers
 #define MPCEKF_HILD_REGROWS 1
 #endif
+#ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
+#define MPCEKF_HILD_NEXTV 1
+#endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
@@ -1057,18 +1060,30 @@ __device__ __forceinline__ double2 hx_r(const double2 *hl, const double2 xr3[3],
 __device__ __forceinline__ double2 hh_r(const double2 *hl, const double2 hr3[3], int i) {
   return i < HILD_REG_ROWS ? hr3[hslot(i)] : hh(hl, i);
 }
-__device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double2 xr3[3],
-                                           const double2 hr3[3], const double K[NCON], double L[NCON],
-                                           double &dmax, double &xmax, double &xmin, bool &vfin) {
-  ConsM Mf{Cn};
-  asm volatile("" ::: "memory");  // reload the LDS slots each sweep (no hoisting)
-  double v0 = 0.0, v1 = 0.0;
+// v = X*lambda from +0 in ascending j (the sweep-start v of orc_hildreth)
+__device__ __forceinline__ void hild_v(const double2 *hl, const double2 xr3[3], const double L[NCON], double &v0,
+                                       double &v1) {
+  v0 = 0.0;
+  v1 = 0.0;
 #pragma unroll
   for (int j = 0; j < NCON; ++j) {
     const double2 x = hx_r(hl, xr3, j);
     v0 = __builtin_fma(x.x, L[j], v0);
     v1 = __builtin_fma(x.y, L[j], v1);
   }
+}
+// (v0, v1): this sweep's start v in, the next sweep's out.  The next sweep's v is summed
+// row by row from lambda_i's final value of this sweep (row i is the last to change it),
+// the same fmas on the same operands in the same order as hild_v after the sweep, with the
+// X(:,i) the row already read (MPCEKF_HILD_NEXTV; 0: hild_v at every sweep start).
+__device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double2 xr3[3],
+                                           const double2 hr3[3], const double K[NCON], double L[NCON],
+                                           double &v0, double &v1, double &dmax, double &xmax, double &xmin,
+                                           bool &vfin) {
+  ConsM Mf{Cn};
+  asm volatile("" ::: "memory");  // reload the LDS slots each sweep (no hoisting)
+  if (!MPCEKF_HILD_NEXTV) hild_v(hl, xr3, L, v0, v1);
+  double u0 = 0.0, u1 = 0.0;
   asm volatile("" ::: "memory");
   // row i's slots are read MPCEKF_HILD_PF rows ahead: ds_read latency (~76 cycles idle,
   // more under load) stays off the chain; one row ahead left ~10 instructions between a
@@ -1102,8 +1117,16 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     L[i] = nl;
     v0 = __builtin_fma(xc.x, d, v0);
     v1 = __builtin_fma(xc.y, d, v1);
+    if (MPCEKF_HILD_NEXTV) {
+      u0 = __builtin_fma(xc.x, nl, u0);
+      u1 = __builtin_fma(xc.y, nl, u1);
+    }
   }
   vfin = isfinite(v0) && isfinite(v1);
+  if (MPCEKF_HILD_NEXTV) {
+    v0 = u0;
+    v1 = u1;
+  }
 }
 
 // The exact form for lanes the fast form flagged: plain division, v recomputed from
@@ -1208,12 +1231,14 @@ __device__ __forceinline__ bool hild_fast(const Cons &Cn, const double E[NC][NC]
   for (int i = 0; i < NCON; ++i) lok = lok && isfinite(L[i]);
   bool slow = !done && !(fin && yok && lok);
   bool active = !done && !slow;  // still sweeping for itself
+  double v0, v1;
+  hild_v(hl, xr3, L, v0, v1);
 #pragma unroll 1
   for (int it = 1; it <= maxIter; ++it) {
     if (__all(!active)) break;
     double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
     bool vfin;
-    sweep_fast(Cn, hl, xr3, hr3, K, L, dmax, xmax, xmin, vfin);
+    sweep_fast(Cn, hl, xr3, hr3, K, L, v0, v1, dmax, xmax, xmin, vfin);
     const bool bad = !(vfin && xmax <= 0x1p400 && xmin >= 0x1p-400);
     const bool conv = dmax < tol;
     const bool newconv = active && !bad && conv;
