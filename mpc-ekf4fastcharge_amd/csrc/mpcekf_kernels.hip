@@ -50,6 +50,9 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_HILD_REGROWS  // k_hild: the constant rows' X / H_ii slots in registers
 #define MPCEKF_HILD_REGROWS 1
 #endif
+#ifndef MPCEKF_FLUSH_COAL  // k_flush_coal (coalesced chunks, NM <= 64): measured slower, off
+#define MPCEKF_FLUSH_COAL 0
+#endif
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
 #endif
@@ -1624,6 +1627,112 @@ __global__ void __launch_bounds__(256) k_flush(const KRom r, const KCfg cf, cons
       }
       if (MPCEKF_FLUSH_PF) cur = nx;
     }
+  }
+}
+
+// k_flush_coal: k_flush with coalesced record traffic (NM <= 64).  A cell's EKF records
+// ([NM][20] doubles) and plant states ([NM][6]) are contiguous, and every element's update
+// is its own recurrence x <- fma(coef, x, input) over the steps its model skipped, so a wave
+// takes the cell's regions as consecutive 16-byte chunks, lane l chunk l + 64 q: each load
+// and store instruction moves one contiguous KB instead of 16 B at a 160-B stride per lane.
+// A chunk is two elements of one model (REC and 6 are even); its coefficients are at the
+// same offset of bulk_tab, its timestamp is the model's.  Same fmas, same order per element.
+// Bitwise-green but slower (645 vs 455 us per flush at configs[2], profiles/r03n_ab_flush_coal.txt):
+// 13 per-chunk timestamp gathers and a compare per chunk and step replace k_flush's two per
+// lane, and the per-lane 16-B stride was not what held k_flush back.  Off by default.
+constexpr int FC_QE = 10, FC_QP = 3;  // chunks per lane: 64 * 10 >= 64 * 20 / 2, 64 * 3 >= 64 * 6 / 2
+__global__ void __launch_bounds__(256) k_flush_coal(const KRom r, const KCfg cf, const KState s, const int t,
+                                                    const int new_ts, const int64_t c_lo, const int64_t c_hi) {
+  const int NM = r.NM;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const double W = cf.SigmaW;
+  const bool mb = cf.flags & KF_MB;  // MB never time-updates the per-model EKF records
+  const int ne2 = NM * REC / 2, np2 = NM * 3;
+  const double *cC = r.bulk_tab, *cP = r.bulk_tab + (size_t)NM * REC;
+  // per-lane constants: the chunks' coefficients, models and element kinds
+  double2 ke[FC_QE], kp[FC_QP];
+  int me[FC_QE], mp[FC_QP];
+  bool xe0[FC_QE], xe1[FC_QE];  // element is an xhat entry (input priorI) or Sigma (input SigmaW)
+#pragma unroll
+  for (int q = 0; q < FC_QE; ++q) {
+    const int j = lane + 64 * q, jj = j < ne2 ? j : ne2 - 1;
+    ke[q] = reinterpret_cast<const double2 *>(cC)[jj];
+    me[q] = j < ne2 ? (2 * j) / REC : -1;
+    xe0[q] = (2 * jj) % REC < NX;
+    xe1[q] = (2 * jj + 1) % REC < NX;
+  }
+#pragma unroll
+  for (int q = 0; q < FC_QP; ++q) {
+    const int j = lane + 64 * q, jj = j < np2 ? j : np2 - 1;
+    kp[q] = reinterpret_cast<const double2 *>(cP)[jj];
+    mp[q] = j < np2 ? (2 * j) / 6 : -1;
+  }
+  struct FCell {
+    double hpl, hul;
+    double2 xe[FC_QE], xp[FC_QP];
+    int tse[FC_QE], tsp[FC_QP];
+  };
+  auto fload = [&](int64_t c, FCell &F) {
+    F.hpl = s.hist_p[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+    F.hul = s.hist_u[(size_t)(lane & (LAZY_H - 1)) * s.n + c];
+    const double2 *re = reinterpret_cast<const double2 *>(s.ekf + (size_t)c * NM * REC);
+    const double2 *rp = reinterpret_cast<const double2 *>(s.bigx + (size_t)c * NM * 6);
+#pragma unroll
+    for (int q = 0; q < FC_QE; ++q) {
+      const bool a = me[q] >= 0;
+      F.xe[q] = re[a ? lane + 64 * q : 0];
+      F.tse[q] = (a && !mb) ? s.ts_ekf[c * NM + me[q]] : t;
+    }
+#pragma unroll
+    for (int q = 0; q < FC_QP; ++q) {
+      const bool a = mp[q] >= 0;
+      F.xp[q] = rp[a ? lane + 64 * q : 0];
+      F.tsp[q] = a ? s.ts_plant[c * NM + mp[q]] : t;
+    }
+  };
+  FCell cur;
+  if (c_lo + w0 < c_hi) fload(c_lo + w0, cur);
+  for (int64_t c = c_lo + w0; c < c_hi; c += nw) {
+    FCell nx;
+    if (c + nw < c_hi) fload(c + nw, nx);
+    int kmin = t;
+#pragma unroll
+    for (int q = 0; q < FC_QE; ++q) kmin = min(kmin, cur.tse[q]);
+#pragma unroll
+    for (int q = 0; q < FC_QP; ++q) kmin = min(kmin, cur.tsp[q]);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) kmin = min(kmin, __shfl_xor(kmin, o));
+    for (int k = kmin + 1; k <= t; ++k) {  // k is wave-uniform
+      const int sl = k & (LAZY_H - 1);
+      const double p = rl64(cur.hpl, sl), u = rl64(cur.hul, sl);
+#pragma unroll
+      for (int q = 0; q < FC_QE; ++q)
+        if (k > cur.tse[q]) {
+          cur.xe[q].x = __builtin_fma(ke[q].x, cur.xe[q].x, xe0[q] ? p : W);
+          cur.xe[q].y = __builtin_fma(ke[q].y, cur.xe[q].y, xe1[q] ? p : W);
+        }
+#pragma unroll
+      for (int q = 0; q < FC_QP; ++q)
+        if (k > cur.tsp[q]) {
+          cur.xp[q].x = __builtin_fma(kp[q].x, cur.xp[q].x, u);
+          cur.xp[q].y = __builtin_fma(kp[q].y, cur.xp[q].y, u);
+        }
+    }
+    double2 *re = reinterpret_cast<double2 *>(s.ekf + (size_t)c * NM * REC);
+    double2 *rp = reinterpret_cast<double2 *>(s.bigx + (size_t)c * NM * 6);
+#pragma unroll
+    for (int q = 0; q < FC_QE; ++q)
+      if (me[q] >= 0 && cur.tse[q] < t) re[lane + 64 * q] = cur.xe[q];
+#pragma unroll
+    for (int q = 0; q < FC_QP; ++q)
+      if (mp[q] >= 0 && cur.tsp[q] < t) rp[lane + 64 * q] = cur.xp[q];
+    if (lane < NM) {
+      s.ts_ekf[c * NM + lane] = new_ts;
+      s.ts_plant[c * NM + lane] = new_ts;
+    }
+    cur = nx;
   }
 }
 
@@ -3220,8 +3329,12 @@ int launch_flush(const KRom &r, const KCfg &c, const KState &s, int t, int new_t
   // loads (210 VGPRs), 3 without (150)
   const int64_t wmax = MPCEKF_FLUSH_PF ? 2048 : 3072;
   const int64_t waves = c_hi - c_lo < wmax ? c_hi - c_lo : wmax;
-  hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts,
-                     c_lo, c_hi);
+  if (MPCEKF_FLUSH_COAL && r.NM <= 64)
+    hipLaunchKernelGGL(k_flush_coal, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t,
+                       new_ts, c_lo, c_hi);
+  else
+    hipLaunchKernelGGL(k_flush, dim3((int)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, r, c, s, t, new_ts,
+                       c_lo, c_hi);
   return (int)hipGetLastError();
 }
 
