@@ -7,7 +7,9 @@ EKFmatsHandler -> iterMPC/hildreth) over every cell of the batch.  Workload:
 synthetic NMC30-like ROM (3 x 21 set-points), Np=5 / Nc=2, SOC0 ~ U[5,30] %,
 TC ~ U[20,30] degC (seed 0x5EED).  Multi-GPU: one process per GPU, cells sharded
 contiguously with no collective on the data path (weak scaling); the only
-collectives are the timing barrier and the max-over-ranks of the elapsed time.
+collectives are the timing barrier and the max-over-ranks of the elapsed time, run
+over gloo by a coordinator child of each rank (the rank process loads one HIP
+runtime, libmpcekf's, and never imports torch).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--cells-per-gpu C | --total-cells T]
 
@@ -150,6 +152,73 @@ def launch_ranks(args):
     sys.exit(bad[0] if bad else 0)
 
 
+class Coordinator:
+    """The ranks' timing collectives (barrier, max/sum over ranks) over gloo, run by a
+    child process (``bench.py --coordinator``) that this rank starts before it touches the
+    GPU.  The rank process itself never imports torch: torch's bundled HIP runtime would
+    otherwise be mapped next to the one libmpcekf links (two runtimes in one process, a
+    round-3 finding).  The path has no data-path collective (cells are independent,
+    SURVEY.md §8(e)); these are the bench contract's barrier and max-over-ranks time."""
+
+    def __init__(self):
+        import subprocess
+        self.p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--coordinator"],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
+        self.backend = self._reply()
+
+    def _reply(self):
+        line = self.p.stdout.readline()
+        if not line:
+            code = self.p.wait()
+            sys.exit(f"bench.py: timing coordinator exited ({code})")
+        return line.strip()
+
+    def _cmd(self, *words):
+        self.p.stdin.write(" ".join(str(w) for w in words) + "\n")
+        self.p.stdin.flush()
+        return self._reply()
+
+    def barrier(self):
+        self._cmd("barrier")
+
+    def reduce(self, dt, nerr, nexec_sum):
+        """(max over ranks of dt, sum of nerr, sum of nexec_sum)"""
+        a, b, c = self._cmd("reduce", repr(float(dt)), repr(float(nerr)), repr(float(nexec_sum))).split()
+        return float(a), int(float(b)), float(c)
+
+    def close(self):
+        self._cmd("exit")
+        self.p.wait(timeout=60)
+
+
+def coordinator_main():
+    """Child of one rank: joins the gloo process group (RANK / WORLD_SIZE / MASTER_* from
+    the environment, torchrun's agent store when present) and serves the rank's timing
+    collectives over stdin/stdout on CPU tensors."""
+    # replies go to a private copy of stdout; anything torch / gloo print goes to stderr
+    reply = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    print(dist.get_backend(), file=reply, flush=True)
+    for line in sys.stdin:
+        w = line.split()
+        if not w or w[0] == "exit":
+            print("bye", file=reply, flush=True)
+            break
+        if w[0] == "barrier":
+            dist.barrier()
+            print("ok", file=reply, flush=True)
+        elif w[0] == "reduce":
+            dt = torch.tensor([float(w[1])], dtype=torch.float64)
+            rest = torch.tensor([float(w[2]), float(w[3])], dtype=torch.float64)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            dist.all_reduce(rest, op=dist.ReduceOp.SUM)
+            print(repr(float(dt[0])), repr(float(rest[0])), repr(float(rest[1])), file=reply, flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -174,13 +243,16 @@ def main():
                     help="PMC traffic JSON (tools/pmc_traffic.py); default profiles/pmc_traffic.json, "
                          "profiles/pmc_traffic_np20.json at Np = 20")
     ap.add_argument("--share-device", action="store_true",
-                    help="all ranks on device 0 with gloo timing collectives (1-GPU multi-rank test)")
+                    help="all ranks on device 0 (1-GPU multi-rank test)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: rank/shard/timing orchestration only (CPU tests)")
     ap.add_argument("--force-dist", action="store_true",
-                    help="create the process group and run the timing collectives at WORLD_SIZE 1 too "
-                         "(exercises the RCCL leg on a one-GPU box)")
+                    help="start the timing coordinator (gloo process group) at WORLD_SIZE 1 too")
+    ap.add_argument("--coordinator", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.coordinator:
+        coordinator_main()
+        return
     if not args.pmc:
         args.pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.np == 5 else f"pmc_traffic_np{args.np}.json")
 
@@ -195,35 +267,22 @@ def main():
     lo, hi = shard_range(total, world, rank)
     ncell = hi - lo
     device = 0 if args.share_device else local
-    import torch
-    dist = None
-    if world > 1 or args.force_dist:
-        import torch.distributed as dist
-        if args.dry_run or args.share_device:
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    backend = dist.get_backend() if dist else "none"
+    # timing collectives in a gloo child process, started before any GPU call
+    coord = Coordinator() if (world > 1 or args.force_dist) else None
+    backend = coord.backend if coord else "none"
     print(f"bench.py rank {rank}/{world}: cells [{lo}, {hi}) ({ncell}) on "
-          f"{'no device (dry run)' if args.dry_run else f'cuda:{device}'}, process group: {backend}",
+          f"{'no device (dry run)' if args.dry_run else f'device {device}'}, process group: {backend}",
           file=sys.stderr, flush=True)
     K, W = args.steps, args.warmup
-    coll_dev = torch.device("cpu") if (args.dry_run or args.share_device) else torch.device("cuda", device)
-
-    def sync():
-        if not args.dry_run:
-            torch.cuda.synchronize(torch.device("cuda", device))
+    runtimes = None
 
     if args.dry_run:
         rom = None
         soc0_all, tc_all = batch_inputs(total)
-        if dist:
-            dist.barrier()
+        if coord:
+            coord.barrier()
         t0 = time.perf_counter()
         _ = soc0_all[lo:hi].sum() + tc_all[lo:hi].sum()
-        if dist:
-            dist.barrier()
         dt = time.perf_counter() - t0
         tim, nerr, mean_nexec, u_last = {}, 0, 0.0, np.zeros(0)
     else:
@@ -234,39 +293,38 @@ def main():
         cfg = M.make_config(bounds=bool(args.bounds), Np=args.np, Nc=args.nc)
         ctx = M.Context(rom, ncell, cfg, device=device)
         ctx.init_cells(soc0_all[lo:hi], tc_all[lo:hi])
-        dev = torch.device("cuda", device)
-        outs = [torch.empty((max(K, W), ncell), dtype=torch.float64, device=dev) for _ in range(4)]
-        nex = torch.empty((max(K, W), ncell), dtype=torch.int32, device=dev)
-        ptrs = [t.data_ptr() for t in outs] + [nex.data_ptr()]
+        # [steps][cells] trajectories in HBM, allocated by the library's runtime
+        rows = max(K, W, 1)
+        outs = [M.DeviceBuffer((rows, ncell), np.float64, device) for _ in range(4)]
+        nex = M.DeviceBuffer((rows, ncell), np.int32, device)
         if W:
-            ctx.step_device(W, *ptrs)
+            ctx.step_device(W, *outs, nex)
         ctx.set_timing(args.timing_every)
         ctx.get_timing()
-        sync()
-        if dist:
-            dist.barrier()
-        sync()
+        ctx.sync()
+        if coord:
+            coord.barrier()
+        ctx.sync()
         t0 = time.perf_counter()
-        ctx.step_device(K, *ptrs)
-        sync()
-        if dist:
-            dist.barrier()
+        ctx.step_device(K, *outs, nex)
+        ctx.sync()
         dt = time.perf_counter() - t0
         tim = ctx.get_timing()
         status = ctx.get_state()["status"]
         nerr = int((status & 1).sum())
-        u_last = outs[0][K - 1].double().cpu().numpy() if K else np.zeros(0)
-        mean_nexec = float(nex[:K].float().mean().item()) if K else 0.0
+        u_last = outs[0].to_host(K)[K - 1] if K else np.zeros(0)
+        mean_nexec = float(nex.to_host(K).mean()) if K else 0.0
         build_id = ctx.L.mpcekf_build_id().decode()
+        runtimes = M.hip_runtimes()
+        for b in outs + [nex]:
+            b.free()
         ctx.close()
-    if dist:
-        t = torch.tensor([dt, float(nerr), mean_nexec * ncell], dtype=torch.float64, device=coll_dev)
-        dt_max = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(dt_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        dt = float(dt_max.item())
-        nerr = int(t[1].item())
-        mean_nexec = float(t[2].item()) / total
+    if coord:
+        # max over ranks of each rank's time from the common barrier to its own sync
+        coord.barrier()
+        dt, nerr, nexec_sum = coord.reduce(dt, nerr, mean_nexec * ncell)
+        mean_nexec = nexec_sum / total
+        coord.close()
 
     if rank == 0:
         cell_steps = total * K
@@ -303,9 +361,8 @@ def main():
         else:
             line.update(report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id,
                                soc0_all, tc_all, world))
+            line["checks"]["hip_runtime"] = runtimes
             print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
 
 
 def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, soc0_all, tc_all, world):

@@ -288,6 +288,24 @@ int mpcekf_get_hild_problems(mpcekf_ctx *ctx, double *prob, int32_t *hflag);
 #define MPCEKF_NSTAMPS 12
 int mpcekf_get_stamps(mpcekf_ctx *ctx, int64_t *stamps, int32_t *nstamps);
 
+/* ---- device memory (not part of the reference interface) ----
+ * Device buffers for outputs_on_device calls, allocated by the library's own HIP
+ * runtime so a host process never holds a second one (a framework's bundled
+ * runtime must not hand its pointers to these kernels).  mpcekf_dev_copy is
+ * synchronous; kind is MPCEKF_COPY_*.  mpcekf_dev_copy2d copies `height` rows of
+ * `width` bytes with the given pitches (e.g. every k-th cell of a [nsteps][ncells]
+ * trajectory: width 8, spitch 8k).  mpcekf_sync waits for every launch of the
+ * context's device. */
+#define MPCEKF_COPY_H2D 0
+#define MPCEKF_COPY_D2H 1
+#define MPCEKF_COPY_D2D 2
+int mpcekf_dev_alloc(int device, int64_t bytes, void **ptr);
+int mpcekf_dev_free(void *ptr);
+int mpcekf_dev_copy(void *dst, const void *src, int64_t bytes, int32_t kind);
+int mpcekf_dev_copy2d(void *dst, int64_t dpitch, const void *src, int64_t spitch, int64_t width, int64_t height,
+                      int32_t kind);
+int mpcekf_sync(mpcekf_ctx *ctx);
+
 /* ---- state access (open-loop parity, checkpoint/restore) ---- */
 typedef struct {
   double *bigX;    /* [ncells][NM][6]   OB_step cellState.bigX (column per model)     */
@@ -312,8 +330,17 @@ typedef struct {
 #define MPCEKF_S_VK 7      /* last plant voltage         */
 #define MPCEKF_NSCAL 8
 
+/* Every non-NULL field of st is copied; NULL fields are neither read nor written (a
+ * checkpoint without mb restores an MB context's other fields and keeps its blend state). */
 int mpcekf_get_state(mpcekf_ctx *ctx, mpcekf_state *st);
 int mpcekf_set_state(mpcekf_ctx *ctx, const mpcekf_state *st);
+/* The few per-cell scalars a stage-call host reads every step (the MATLAB drop-ins:
+ * cellState.SOCnAvg/SOCpAvg before OB_step, OB_step.m:226-228; ekfData.x0, SigmaX0,
+ * priorI, warnCount and the status after iterEKF): slots[nslots] are MPCEKF_S_* indices,
+ * scal [ncells][nslots]; warn / status [ncells] may be NULL.  Only these bytes cross
+ * PCIe: 8 * nslots (+ 4 + 4) per cell. */
+int mpcekf_get_scalars(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                       int32_t *status);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,9 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
     cfg.SigmaV = S.kf.SigmaV;  cfg.SigmaW = S.kf.SigmaW;  cfg.SigmaX0 = S.kf.SigmaX0;
     cfg.flags = 1;                                         % MPCEKF_CF_BOUNDS: boundzk too
     if strcmp(S.kf.method, 'MB'), cfg.method = 1; end
-    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], unique(Tc(:)')), cfg, S.device, n);  % Tc on the table grid
+    % the electrode tables hold the ROM set-points and the span of Tc (a per-cell Tc of
+    % thousands of distinct values must not each become a table temperature)
+    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], [min(Tc(:)), max(Tc(:))]), cfg, S.device, n);
     mpcekf_session('set', 'h', h);
     mpcekf_mex('init', h, reshape(initCfg.SOC0, 1, n), Tc .* ones(1, n));
     fn = ROM.cellData.function.neg;
@@ -24,8 +26,8 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
                        'theta0n', fn.theta0(), 'theta100n', fn.theta100());
   end
   n = cellState.n;
-  st = mpcekf_mex('get_state', cellState.h);                 % pre-update averages (OB_step.m:226-228)
-  obs = struct('negSOC', st.scal(1, :), 'posSOC', st.scal(2, :));
+  s = mpcekf_mex('scalars', cellState.h, [1 2]);             % pre-update averages (OB_step.m:226-228),
+  obs = struct('negSOC', s(1, :), 'posSOC', s(2, :));         % 16 B per cell over PCIe
   obs.cellSOC = (obs.negSOC - cellState.theta0n) / (cellState.theta100n - cellState.theta0n);
   Vcell = mpcekf_mex('plant', cellState.h, reshape(Iapp .* ones(1, n), 1, n), reshape(Tc .* ones(1, n), 1, n));
   obs.Vcell = Vcell;

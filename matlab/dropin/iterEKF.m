@@ -10,7 +10,7 @@ function [zk,boundzk,ekfData,Xind] = iterEKF(vk,ik,Tk,ekfData)
   nZ = numel(ekfData.ROM.xraData.SOC);
   Xind = struct('gamma', xg, 'theT', double(idivide(xm, int32(nZ))) + 1, 'theZ', double(mod(xm, nZ)) + 1, ...
                 'model', xm);
-  st = mpcekf_mex('get_state', S.h);
-  ekfData.x0 = st.scal(3, :);  ekfData.SigmaX0 = st.scal(4, :);  ekfData.priorI = st.scal(5, :);
-  ekfData.status = st.status;  ekfData.warnCount = st.warn;
+  [s, warn, status] = mpcekf_mex('scalars', S.h, [3 4 5]);   % x0, SigmaX0, priorI: 32 B per cell
+  ekfData.x0 = s(1, :);  ekfData.SigmaX0 = s(2, :);  ekfData.priorI = s(3, :);
+  ekfData.status = status;  ekfData.warnCount = warn;
 end

@@ -24,7 +24,12 @@
  *   [Phi,G]           = mpcekf_mex('predmat', a, C, D, Np, Nc)         (predMat.m:1, A = diag(a), B = 1)
  *   st                = mpcekf_mex('get_state', h)    /  mpcekf_mex('set_state', h, st)
  *                       st.bigX, ekf, scal, lambda (double), warn, status (int32 1 x ncells),
- *                       and st.mb (42 x ncells) on a model-blend ('MB') context
+ *                       and st.mb (42 x ncells) on a model-blend ('MB') context (optional
+ *                       in set_state: a checkpoint without it keeps the blend state)
+ *   [s,warn,status]   = mpcekf_mex('scalars', h, idx)                 mpcekf_get_scalars
+ *                       s: numel(idx) x ncells of the 1-based MPCEKF_S_* slots idx (1-2
+ *                       SOCnAvg/SOCpAvg, 3 x0, 4 SigmaX0, 5 priorI, 6 uk_1, 7 uk, 8 vk):
+ *                       what the drop-ins read every step, 8 B per slot and cell
  *                       mpcekf_mex('graph', h, enable)                 mpcekf_set_graph (replay repeated step calls)
  * Per-cell vectors are 1 x ncells or ncells x 1; zk / zbk are (nz+2) x ncells, xm / xg
  * 4 x ncells (xm: 0-based model index t*nZ+z), lin 35 x ncells -- MATLAB's column-major
@@ -35,6 +40,8 @@
  * Only the first max(nargout, 1) outputs are returned.
  * Library failures raise a MATLAB error with mpcekf_last_error(); per-cell soft
  * failures stay in the status word (get_state), as in the C-ABI.
+ * `clear mex` / MATLAB exit destroys every context still live (mexAtExit), freeing its
+ * device memory; handles saved across a clear are then rejected as not live.
  */
 #include <stdint.h>
 #include <string.h>
@@ -57,6 +64,15 @@ static void track(mpcekf_ctx *h, int add) {
     if (add ? g_live[i] == NULL : g_live[i] == h) {
       g_live[i] = add ? h : NULL;
       return;
+    }
+}
+
+/* mexAtExit: `clear mex` or MATLAB exit releases every live context's device memory */
+static void destroy_all(void) {
+  for (int i = 0; i < MAXCTX; ++i)
+    if (g_live[i]) {
+      (void)mpcekf_ctx_destroy(g_live[i]);
+      g_live[i] = NULL;
     }
 }
 
@@ -217,6 +233,7 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     mpcekf_ctx *h = NULL;
     chk(mpcekf_ctx_create(&r, &c, (int)scalar(prhs[3], "device"), (int64_t)scalar(prhs[4], "ncells"), &h));
     track(h, 1);
+    mexAtExit(destroy_all);
     plhs[0] = mxCreateNumericMatrix(1, 1, mxUINT64_CLASS, mxREAL);
     *(uint64_t *)mxGetData(plhs[0]) = (uint64_t)(uintptr_t)h;
     return; /* the row-major copies are mxMalloc'd: MATLAB frees them (the context copied the ROM) */
@@ -254,7 +271,7 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     return;
   }
   static const char *const with_handle[] = {"destroy", "init", "step", "plant", "ekf", "linearize", "mpc",
-                                            "graph", "mpcdiag", "get_state", "set_state"};
+                                            "graph", "mpcdiag", "get_state", "set_state", "scalars"};
   int known = 0;
   for (size_t i = 0; i < sizeof with_handle / sizeof *with_handle; ++i) known = known || !strcmp(cmd, with_handle[i]);
   if (!known) mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
@@ -347,9 +364,27 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
       st.lambda = (double *)dvec(field(s, "lambda"), rows[3] * nc, "lambda");
       st.warn = ivec(field(s, "warn"), nc, "warn");
       st.status = ivec(field(s, "status"), nc, "status");
-      if (nf == 7) st.mb = (double *)dvec(field(s, "mb"), rows[6] * nc, "mb (MB context)");
+      /* an MB checkpoint saved before st.mb existed restores without it (NULL keeps the
+         context's blend state, as the C-ABI allows) */
+      if (nf == 7 && mxGetField(s, 0, "mb")) st.mb = (double *)dvec(mxGetField(s, 0, "mb"), rows[6] * nc, "mb (MB context)");
       chk(mpcekf_set_state(h, &st));
     }
+  } else if (!strcmp(cmd, "scalars")) {
+    need(nrhs, 3, "'scalars', h, idx");
+    const size_t k = mxGetNumberOfElements(prhs[2]);
+    if (k < 1 || k > MPCEKF_NSCAL) mexErrMsgIdAndTxt("mpcekf:arg", "scalars: 1..%d slot indices", MPCEKF_NSCAL);
+    const double *idx = dvec(prhs[2], k, "idx");
+    int32_t slots[MPCEKF_NSCAL];
+    for (size_t j = 0; j < k; ++j) {
+      if (!(idx[j] >= 1 && idx[j] <= MPCEKF_NSCAL) || idx[j] != (double)(int)idx[j])
+        mexErrMsgIdAndTxt("mpcekf:arg", "scalars: idx(%zu) = %g is not a slot 1..%d", j + 1, idx[j], MPCEKF_NSCAL);
+      slots[j] = (int32_t)idx[j] - 1;
+    }
+    plhs[0] = dmat(k, nc); /* k x ncells column-major = the library's [ncells][k] */
+    plhs[1] = imat(1, nc);
+    plhs[2] = imat(1, nc);
+    chk(mpcekf_get_scalars(h, slots, (int32_t)k, mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1]),
+                           (int32_t *)mxGetData(plhs[2])));
   } else {
     mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
   }

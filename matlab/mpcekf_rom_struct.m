@@ -14,7 +14,14 @@ function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC)
   if nargin < 4 || isempty(TC), TC = 25; end
   if nargin < 3 || isempty(TdegC)
     Ts = ROM.xraData.T(:)';
-    TdegC = unique([Ts, TC(:)']);
+    TCu = unique(TC(:)');
+    % more distinct simulation temperatures than free table slots (e.g. a per-cell Tc):
+    % keep only their span, the interior is filled by the interval halving below
+    if numel(unique([Ts, TCu])) > 8, TCu = unique([min(TCu), max(TCu)]); end
+    TdegC = unique([Ts, TCu]);
+    if numel(TdegC) > 8                     % set-points + span still too many: the span
+      TdegC = linspace(min(TdegC), max(TdegC), 8);  % evenly (lookups off the points interpolate)
+    end
     guard = [min(TdegC) - 10, max(TdegC) + 10];
     if numel(TdegC) + 2 <= 8, TdegC = unique([guard(1), TdegC, guard(2)]); end
     while numel(TdegC) < 8                  % spare slots halve the widest intervals

@@ -941,6 +941,59 @@ int mpcekf_get_timing(mpcekf_ctx *X, double *ms_sum, int64_t *launches) {
   return MPCEKF_OK;
 }
 
+// ---- device memory owned by the library ---------------------------------------
+// Callers that keep trajectories on the device (bench.py, the GPU tests, a MEX host)
+// allocate them here, so a process holds exactly one HIP runtime: the one this
+// library links.  A second runtime (e.g. a framework's bundled copy) in the same
+// process owns its own HSA queues and address-space bookkeeping; pointers must not
+// cross between the two.
+int mpcekf_dev_alloc(int device, int64_t bytes, void **ptr) {
+  if (!ptr || bytes < 0) return fail(MPCEKF_E_ARG, "dev_alloc: bad argument");
+  *ptr = nullptr;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MPCEKF_E_ARG, "dev_alloc: device %d of %d", device, ndev);
+  if (bytes == 0) return MPCEKF_OK;
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipMalloc(ptr, (size_t)bytes));
+  return MPCEKF_OK;
+}
+
+int mpcekf_dev_free(void *ptr) {
+  if (ptr) HIPCHK(hipFree(ptr));
+  return MPCEKF_OK;
+}
+
+static hipMemcpyKind copy_kind(int32_t kind) {
+  return kind == MPCEKF_COPY_H2D ? hipMemcpyHostToDevice
+       : kind == MPCEKF_COPY_D2H ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+}
+
+int mpcekf_dev_copy(void *dst, const void *src, int64_t bytes, int32_t kind) {
+  if (bytes < 0 || kind < MPCEKF_COPY_H2D || kind > MPCEKF_COPY_D2D || (bytes && (!dst || !src)))
+    return fail(MPCEKF_E_ARG, "dev_copy: bad argument");
+  if (bytes) HIPCHK(hipMemcpy(dst, src, (size_t)bytes, copy_kind(kind)));
+  return MPCEKF_OK;
+}
+
+int mpcekf_dev_copy2d(void *dst, int64_t dpitch, const void *src, int64_t spitch, int64_t width, int64_t height,
+                      int32_t kind) {
+  if (width < 0 || height < 0 || dpitch < width || spitch < width || kind < MPCEKF_COPY_H2D ||
+      kind > MPCEKF_COPY_D2D || (width && height && (!dst || !src)))
+    return fail(MPCEKF_E_ARG, "dev_copy2d: bad argument");
+  if (width && height)
+    HIPCHK(hipMemcpy2D(dst, (size_t)dpitch, src, (size_t)spitch, (size_t)width, (size_t)height, copy_kind(kind)));
+  return MPCEKF_OK;
+}
+
+int mpcekf_sync(mpcekf_ctx *X) {
+  if (!X) return fail(MPCEKF_E_ARG, "null ctx");
+  HIPCHK(hipSetDevice(X->device));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  HIPCHK(hipDeviceSynchronize());
+  return MPCEKF_OK;
+}
+
 int mpcekf_get_zk(mpcekf_ctx *X, double *zk, double *boundzk) {
   int rc = need_init(X);
   if (rc) return rc;
@@ -1282,11 +1335,13 @@ int mpcekf_get_state(mpcekf_ctx *X, mpcekf_state *st) {
   if (st->bigX) HIPCHK(hipMemcpyAsync(st->bigX, X->s.bigx, n * NM * 6 * 8, hipMemcpyDeviceToHost, X->stream));
   if (st->ekf) HIPCHK(hipMemcpyAsync(st->ekf, X->s.ekf, n * NM * REC * 8, hipMemcpyDeviceToHost, X->stream));
   if (st->mb && X->mb) HIPCHK(hipMemcpyAsync(st->mb, X->d_mb, n * MBREC * 8, hipMemcpyDeviceToHost, X->stream));
-  std::vector<double> sc(n * 8), lam(n * nc);
-  std::vector<int> iv(n * 2);
-  HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(lam.data(), X->s.lam, n * nc * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
+  // only the requested fields cross PCIe (a MEX drop-in reading SOCnAvg/SOCpAvg each
+  // step moves the 64-B scalar block per cell, not the NM-model records)
+  std::vector<double> sc(st->scal ? n * 8 : 0), lam(st->lambda ? n * nc : 0);
+  std::vector<int> iv(st->warn || st->status ? n * 2 : 0);
+  if (st->scal) HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
+  if (st->lambda) HIPCHK(hipMemcpyAsync(lam.data(), X->s.lam, n * nc * 8, hipMemcpyDeviceToHost, X->stream));
+  if (!iv.empty()) HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   for (size_t c = 0; c < n; ++c) {
     if (st->scal)
@@ -1299,6 +1354,29 @@ int mpcekf_get_state(mpcekf_ctx *X, mpcekf_state *st) {
   return MPCEKF_OK;
 }
 
+int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                       int32_t *status) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (nslots < 0 || nslots > MPCEKF_NSCAL || (nslots && (!slots || !scal)))
+    return fail(MPCEKF_E_ARG, "get_scalars: bad slot list");
+  for (int j = 0; j < nslots; ++j)
+    if (slots[j] < 0 || slots[j] >= MPCEKF_NSCAL) return fail(MPCEKF_E_ARG, "get_scalars: slot %d", slots[j]);
+  const size_t n = (size_t)X->n;
+  // the SoA scalar block holds each slot as one contiguous [ncells] vector: exactly the
+  // requested slots cross PCIe
+  std::vector<double> sc(n * (size_t)nslots);
+  for (int j = 0; j < nslots; ++j)
+    HIPCHK(hipMemcpyAsync(sc.data() + (size_t)j * n, X->d_scal + (size_t)kScalMap[slots[j]] * n, n * 8,
+                          hipMemcpyDeviceToHost, X->stream));
+  if (warn) HIPCHK(hipMemcpyAsync(warn, X->s.warn, n * 4, hipMemcpyDeviceToHost, X->stream));
+  if (status) HIPCHK(hipMemcpyAsync(status, X->s.status, n * 4, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  for (size_t c = 0; c < n; ++c)
+    for (int j = 0; j < nslots; ++j) scal[c * nslots + j] = sc[(size_t)j * n + c];
+  return MPCEKF_OK;
+}
+
 int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
   int rc = need_init(X);
   if (rc) return rc;
@@ -1307,12 +1385,14 @@ int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
   if (st->bigX) HIPCHK(hipMemcpyAsync(X->s.bigx, st->bigX, n * NM * 6 * 8, hipMemcpyHostToDevice, X->stream));
   if (st->ekf) HIPCHK(hipMemcpyAsync(X->s.ekf, st->ekf, n * NM * REC * 8, hipMemcpyHostToDevice, X->stream));
   if (st->mb && X->mb) HIPCHK(hipMemcpyAsync(X->d_mb, st->mb, n * MBREC * 8, hipMemcpyHostToDevice, X->stream));
-  std::vector<double> sc(n * 8), lam(n * nc);
-  std::vector<int> iv(n * 2);
-  HIPCHK(hipMemcpyAsync(sc.data(), X->d_scal, n * 8 * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(lam.data(), X->s.lam, n * nc * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
+  // scal and lambda are whole blocks (every slot given); warn and status share one block,
+  // read back first when only one of them is given
+  std::vector<double> sc(st->scal ? n * 8 : 0), lam(st->lambda ? n * nc : 0);
+  std::vector<int> iv(st->warn || st->status ? n * 2 : 0);
+  if (!iv.empty() && !(st->warn && st->status)) {
+    HIPCHK(hipMemcpyAsync(iv.data(), X->d_int, n * 2 * 4, hipMemcpyDeviceToHost, X->stream));
+    HIPCHK(hipStreamSynchronize(X->stream));
+  }
   for (size_t c = 0; c < n; ++c) {
     if (st->scal)
       for (int k = 0; k < MPCEKF_NSCAL; ++k) sc[kScalMap[k] * n + c] = st->scal[c * MPCEKF_NSCAL + k];
@@ -1321,9 +1401,9 @@ int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
     if (st->warn) iv[c] = st->warn[c];
     if (st->status) iv[n + c] = st->status[c];
   }
-  HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), n * 8 * 8, hipMemcpyHostToDevice, X->stream));
-  HIPCHK(hipMemcpyAsync(X->s.lam, lam.data(), n * nc * 8, hipMemcpyHostToDevice, X->stream));
-  HIPCHK(hipMemcpyAsync(X->d_int, iv.data(), n * 2 * 4, hipMemcpyHostToDevice, X->stream));
+  if (st->scal) HIPCHK(hipMemcpyAsync(X->d_scal, sc.data(), n * 8 * 8, hipMemcpyHostToDevice, X->stream));
+  if (st->lambda) HIPCHK(hipMemcpyAsync(X->s.lam, lam.data(), n * nc * 8, hipMemcpyHostToDevice, X->stream));
+  if (!iv.empty()) HIPCHK(hipMemcpyAsync(X->d_int, iv.data(), n * 2 * 4, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
   return MPCEKF_OK;
 }

@@ -1486,6 +1486,147 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
 }
 
 // ---------------------------------------------------------------------------
+// k_plant4: k_plant with a lane quad per cell, lane j = corner j of OB_step.m:251-275.
+// Lane-per-cell k_plant runs 65,536 cells as one wave per SIMD, so every round trip
+// (the per-cell scalars, then the corner gathers they select) and every dependent FP64
+// chain is exposed (60 % of its cycles in s_waitcnt, VALU 15 %).  Here lane j gathers and
+// replays only its corner's 48-B state and forms its 9 output rows; the blend of
+// OB_step.m:281-285 takes the four corners' rows by DPP quad broadcasts in the one-lane
+// expression order, and the per-cell scalar chain (bracket, clamps, asinh, Vcell) is the
+// same instruction stream for the whole quad.  1024-thread blocks: 256 cells share one
+// staged plant blob per CU at 4 waves per SIMD.  Results: k_plant's bits.
+// ---------------------------------------------------------------------------
+#ifndef MPCEKF_PLANT_QUAD
+#define MPCEKF_PLANT_QUAD 1
+#endif
+constexpr int PLANT4_BLOCK = 1024;
+template <bool GR>
+__global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KState s, const double *iapp,
+                                                         double *vout, const int lazy_t, const double *tc_in) {
+  extern __shared__ double lds[];
+  const int lo = GR ? r.plant_tab : 0;
+  stage_lds(lds, r.plant_blob + lo, r.plant_len - lo);
+  __syncthreads();
+  const double *tb = lds - lo;
+  const double *L = GR ? r.plant_blob : lds;
+  const double *Tp = tb + r.plant_tab + r.plant_tablen;
+  const double *Zp = Tp + MAXT;
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (int)(gt & 3);
+  const int64_t c = gt >> 2;  // a quad is one cell: every exit below is quad-uniform
+  if (gt == 0 && lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
+  if (c >= s.n) return;
+  const double Iapp = iapp[c];
+  const double tcs = tc_in ? tc_in[c] : s.Tc[c];
+  const double priorI = s.priorI[c];
+  const int status = s.status[c];
+  double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
+  const double SOC0n = s.SOC0n[c], SOC0p = s.SOC0p[c];
+  if (j == 0) {
+    if (tc_in) s.Tc[c] = tcs;  // this step's TC (runMPC.m:85-92), read by every later kernel
+    if (lazy_t) {  // this step's inputs, for the deferred updates of every model (k_cell, k_flush)
+      const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
+      s.hist_u[slot] = Iapp;
+      s.hist_p[slot] = priorI;
+    }
+  }
+  if (status & ST_ERROR) {
+    if (j == 0) vout[c] = __builtin_nan("");
+    return;
+  }
+  const double T = tcs + 273.15;  // OB_step.m:75
+  const ETab et = etab(r, tb + r.plant_tab, T);
+  const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
+  double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
+  int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
+  if (r.nZ > 1) {
+    int a, b;
+    two_nearest(Zp, r.nZ, cellSOC, a, b);
+    iZu = a > b ? a : b; iZl = a < b ? a : b;
+  }
+  if (r.nT > 1) {
+    int a, b;
+    two_nearest(Tp, r.nT, T, a, b);
+    iTu = a > b ? a : b; iTl = a < b ? a : b;
+  }
+  // this lane's corner: mm = {Tl Zl, Tl Zu, Tu Zl, Tu Zu}[j]
+  const int mj = ((j & 2) ? iTu : iTl) * r.nZ + ((j & 1) ? iZu : iZl);
+  double *bx = s.bigx + ((size_t)c * r.NM + mj) * 6;
+  double xs[6];
+  {
+    const double2 *p = reinterpret_cast<const double2 *>(bx);
+    const double2 q0 = p[0], q1 = p[1], q2 = p[2];
+    xs[0] = q0.x; xs[1] = q0.y; xs[2] = q1.x; xs[3] = q1.y; xs[4] = q2.x; xs[5] = q2.y;
+  }
+  const int tsj = lazy_t ? s.ts_plant[c * r.NM + mj] : 0;
+  // the per-cell scalar chain runs while the corner gathers are in flight
+  const double Cdleffn = et.f(0, EF_CDL, SOC0n), Cdleffp = et.f(1, EF_CDL, SOC0p);  // OB_step.m:212-219
+  double dUn = et.f(0, EF_DU, SOCnAvg), dUp = et.f(1, EF_DU, SOCpAvg);
+  double dQn = fabs(r.th100n - r.th0n), dQp = fabs(r.th100p - r.th0p);
+  double res0n = -dQn / (3600 * r.Q - Cdleffn * dQn * dUn);
+  double res0p = dQp / (3600 * r.Q - Cdleffp * dQp * dUp);
+  SOCnAvg = SOCnAvg + res0n * Iapp * r.Ts;
+  SOCpAvg = SOCpAvg + res0p * Iapp * r.Ts;
+  if (SOCnAvg < 0) SOCnAvg = 0;
+  if (SOCnAvg > 1) SOCnAvg = 1;
+  if (SOCpAvg < 0) SOCpAvg = 0;
+  if (SOCpAvg > 1) SOCpAvg = 1;
+  const double Zu = Zp[iZu], Zl = Zp[iZl], Tu = Tp[iTu], Tl = Tp[iTl];
+  double aZ = 0.0, aT = 0.0;
+  if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
+  if (Tu != Tl) aT = (T - Tl) / (Tu - Tl);
+  const double *a = L + mj * PREC + NPLANT * NX + 2 * NPLANT;
+  if (lazy_t)
+    for (int k = tsj + 1; k < lazy_t; ++k) {  // OB_step.m:198-200 for the skipped steps
+      const double u = s.hist_u[(size_t)(k % LAZY_H) * s.n + c];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) xs[e] = __builtin_fma(a[e], xs[e], u);
+    }
+  const double *B = L + mj * PREC;
+  double yk[NPLANT];
+#pragma unroll
+  for (int q = 0; q < NPLANT; ++q) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) acc = acc + B[q * NX + k] * xs[k];
+    acc = acc + B[NPLANT * NX + q] * xs[5];
+    const double y = acc + B[NPLANT * NX + NPLANT + q] * Iapp;
+    const double y0 = qbc<0>(y), y1 = qbc<1>(y), y2 = qbc<2>(y), y3 = qbc<3>(y);
+    yk[q] = (1 - aT) * ((1 - aZ) * y0 + aZ * y1) + aT * ((1 - aZ) * y2 + aZ * y3);
+    __builtin_amdgcn_sched_barrier(0);  // one row's LDS operands at a time: 128 VGPRs at 4 waves/SIMD
+  }
+  double th0 = fmin(fmax(yk[R_TH0] + SOC0n, 1e-6), 1 - 1e-6);
+  double th3 = fmin(fmax(yk[R_TH3] + SOC0p, 1e-6), 1 - 1e-6);
+  double te1 = fmax(yk[R_TE1] + 1, 1e-6);
+  double teE = fmax(yk[R_TEE] + 1, 1e-6);
+  double i0n = et.f(0, EF_K0, negSOC) * sqrt(te1 * (1 - th0) * th0);  // OB_step.m:329-332
+  double i0p = et.f(1, EF_K0, posSOC) * sqrt(teE * (1 - th3) * th3);
+  double negEta0 = 2 * r.R * T / r.F * dasinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * T / r.F * dasinh(yk[R_IF3] / (2 * i0p));
+  double Uocpn0 = et.f(0, EF_U, th0), Uocpp3 = et.f(1, EF_U, th3);
+  const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
+  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
+  V = V - r.Rc * Iapp;
+  if (j == 0) {
+    s.SOCn[c] = SOCnAvg;
+    s.SOCp[c] = SOCpAvg;
+    vout[c] = V;
+  }
+  // advance this corner through step t in place (eager mode: k_bulk does all models); a
+  // duplicate corner (single-set-point grids) is written by two lanes with the same bits
+  if (lazy_t && tsj < lazy_t) {
+    double2 *p = reinterpret_cast<double2 *>(bx);
+    double x[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) x[e] = __builtin_fma(a[e], xs[e], Iapp);
+    p[0] = make_double2(x[0], x[1]);
+    p[1] = make_double2(x[2], x[3]);
+    p[2] = make_double2(x[4], x[5]);
+    s.ts_plant[c * r.NM + mj] = lazy_t;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_bulk: all-model plant advance and EKF time update (HBM streaming)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_bulk(const KRom r, const KCfg cf, const KState s, const double *iapp,
@@ -3310,6 +3451,16 @@ bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
 int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
                  void *stream) {
   if (s.n == 0) return 0;
+  if (MPCEKF_PLANT_QUAD) {
+    const dim3 g(grid_for(4 * s.n, PLANT4_BLOCK)), b(PLANT4_BLOCK);
+    if (r.rom_global)
+      hipLaunchKernelGGL(k_plant4<true>, g, b, plant_lds_bytes(r), (hipStream_t)stream, r, s, iapp, vout, lazy_t,
+                         tc_in);
+    else
+      hipLaunchKernelGGL(k_plant4<false>, g, b, plant_lds_bytes(r), (hipStream_t)stream, r, s, iapp, vout, lazy_t,
+                         tc_in);
+    return (int)hipGetLastError();
+  }
   if (r.rom_global)
     hipLaunchKernelGGL(k_plant<true>, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r,
                        s, iapp, vout, lazy_t, tc_in);

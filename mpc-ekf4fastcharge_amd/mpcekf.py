@@ -25,7 +25,7 @@ from . import _lib
 from ._lib import LIN_SIZE, MpcekfError, check, dptr, iptr
 from .rom import ROM, TF_CODE
 
-__all__ = ["Context", "make_config", "predMat", "constraintsMPC", "hildreth", "runMPC", "MpcekfError",
+__all__ = ["Context", "DeviceBuffer", "hip_runtimes", "tc_grid", "make_config", "predMat", "constraintsMPC", "hildreth", "runMPC", "MpcekfError",
            "LIN_SIZE"]
 
 LIN_FIELDS = dict(A=slice(0, 6), Csoc=slice(6, 12), Dsoc=12, Cv=slice(13, 19), Dv=19,
@@ -91,6 +91,103 @@ class _PackedRom:
         self.s = r
 
 
+def tc_grid(tc, nsteps, ncells):
+    """A temperature argument as the [nsteps, ncells] grid of per-step TC (degC): a scalar,
+    a 1-D per-step profile [nsteps] or per-cell vector [ncells], [nsteps, 1], [1, ncells]
+    or the full array.  A 1-D vector whose length is both nsteps and ncells is ambiguous
+    and refused (oracle/oracle_c.py reads temperature arguments by the same rule)."""
+    a = np.asarray(tc, dtype=np.float64)
+    if a.ndim == 1 and a.size != 1:
+        if a.size == nsteps and a.size == ncells:
+            raise ValueError(f"tc: a 1-D vector of length {a.size} = nsteps = ncells is ambiguous; "
+                             "pass [nsteps, 1] (per step) or [1, ncells] (per cell)")
+        if a.size == nsteps:
+            a = a.reshape(nsteps, 1)
+        elif a.size == ncells:
+            a = a.reshape(1, ncells)
+        else:
+            raise ValueError(f"tc: length {a.size} is neither nsteps ({nsteps}) nor ncells ({ncells})")
+    return np.ascontiguousarray(np.broadcast_to(a, (nsteps, ncells)))
+
+
+class DeviceBuffer:
+    """A C-contiguous device array allocated by the library's own HIP runtime
+    (mpcekf_dev_alloc), for outputs_on_device calls: the host process then holds one
+    HIP runtime only, and no foreign runtime's pointers reach the kernels."""
+
+    def __init__(self, shape, dtype=np.float64, device=0):
+        self.L = _lib.load()
+        self.shape = tuple(int(x) for x in np.atleast_1d(shape))
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = C.c_void_p()
+        check(self.L.mpcekf_dev_alloc(int(device), self.nbytes, C.byref(p)))
+        self.ptr = p.value or 0
+
+    def free(self):
+        if getattr(self, "ptr", 0):
+            self.L.mpcekf_dev_free(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.free()
+
+    def row_bytes(self):
+        return self.nbytes // self.shape[0] if self.shape and self.shape[0] else 0
+
+    def to_host(self, rows=None):
+        """The first ``rows`` leading-axis rows (default all) as a numpy array."""
+        rows = self.shape[0] if rows is None else int(rows)
+        out = np.empty((rows,) + self.shape[1:], dtype=self.dtype)
+        check(self.L.mpcekf_dev_copy(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes,
+                                     _lib.COPY_D2H))
+        return out
+
+    def sampled(self, rows, stride):
+        """[rows, ncells] buffer -> its every ``stride``-th column of the first ``rows`` rows
+        (a pitched device-to-host copy: only the sampled elements cross PCIe)."""
+        n = self.shape[1]
+        if len(self.shape) != 2 or n % stride:
+            raise ValueError("sampled: 2-D buffer with ncells divisible by stride expected")
+        it = self.dtype.itemsize
+        out = np.empty((rows, n // stride), dtype=self.dtype)
+        check(self.L.mpcekf_dev_copy2d(out.ctypes.data_as(C.c_void_p), it, C.c_void_p(self.ptr), stride * it, it,
+                                       rows * (n // stride), _lib.COPY_D2H))
+        return out
+
+    def from_host(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.nbytes > self.nbytes:
+            raise ValueError("from_host: array larger than the buffer")
+        check(self.L.mpcekf_dev_copy(C.c_void_p(self.ptr), a.ctypes.data_as(C.c_void_p), a.nbytes, _lib.COPY_H2D))
+
+
+def hip_runtimes():
+    """Paths of the HIP / HSA runtime libraries mapped into this process ({'hip': [...],
+    'hsa': [...]}): one of each when the library's runtime is the only one."""
+    out = {"hip": set(), "hsa": set()}
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.split() else ""
+                if "libamdhip64" in p:
+                    out["hip"].add(p)
+                elif "libhsa-runtime64" in p:
+                    out["hsa"].add(p)
+    except OSError:
+        pass
+    return {k: sorted(v) for k, v in out.items()}
+
+
 class Context:
     """One device, one stream, ``ncells`` independent cells (mpcekf_ctx)."""
 
@@ -149,13 +246,10 @@ class Context:
         diagnostics x (x_store), zk / zbk (zkEst / zkBound), J_unc, J_fin, norm_du, nviol
         (mpcData.cost), poles ([.., 7, 2] re/im of eig(CL)) and sv (svd(CL)), the stability
         diagnostics of iterMPC.m:53-60 (returned as complex [nsteps, ncells, 7] for poles).
-        ``tc``: the TC of each step in degC (runMPC.m:85-92), anything numpy broadcasts to
-        [nsteps, ncells]: a scalar, a per-cell vector [ncells], a per-step column [nsteps, 1]
-        or the full array; None keeps every cell's current temperature."""
+        ``tc``: the TC of each step in degC (runMPC.m:85-92), see :func:`tc_grid`; None keeps
+        every cell's current temperature."""
         n = self.n
-        tcs = None
-        if tc is not None:
-            tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc, dtype=np.float64), (nsteps, n)))
+        tcs = None if tc is None else tc_grid(tc, nsteps, n)
         out = {}
         tr = _lib.Traj()
         for k in outputs:
@@ -172,9 +266,14 @@ class Context:
         return out
 
     def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
-        """Fused steps writing [nsteps][ncells] outputs to device pointers (ints)."""
-        p = [C.c_void_p(x) if x else None for x in (u, v, soc, phise, nexec)]
+        """Fused steps writing [nsteps][ncells] outputs to device pointers (ints or
+        DeviceBuffer; allocate them with DeviceBuffer / mpcekf_dev_alloc)."""
+        p = [C.c_void_p(x.ptr if isinstance(x, DeviceBuffer) else x) if x else None for x in (u, v, soc, phise, nexec)]
         check(self.L.mpcekf_step(self.h, int(nsteps), None, *p, 1))
+
+    def sync(self):
+        """Wait for every launch on the context's device (mpcekf_sync)."""
+        check(self.L.mpcekf_sync(self.h))
 
     def set_graph(self, enable=True):
         """Replay repeated fused-call shapes from captured hipGraphs (mpcekf_set_graph)."""
@@ -293,6 +392,21 @@ class Context:
                        iptr(st["warn"]), iptr(st["status"]), dptr(st.get("mb")))
         check(self.L.mpcekf_get_state(self.h, C.byref(s)))
         return st
+
+    SCALARS = ("SOCnAvg", "SOCpAvg", "x0", "SigmaX0", "priorI", "uk_1", "uk", "vk")  # MPCEKF_S_* order
+
+    def get_scalars(self, names=("SOCnAvg", "SOCpAvg"), flags=False):
+        """The named per-cell scalars ({name: [ncells]}; names from SCALARS) and, with
+        flags=True, warn / status -- only these bytes cross PCIe (mpcekf_get_scalars)."""
+        slots = np.array([self.SCALARS.index(k) for k in names], dtype=np.int32)
+        sc = np.empty((self.n, len(slots)))
+        warn = np.empty(self.n, np.int32) if flags else None
+        status = np.empty(self.n, np.int32) if flags else None
+        check(self.L.mpcekf_get_scalars(self.h, iptr(slots), len(slots), dptr(sc), iptr(warn), iptr(status)))
+        out = {k: sc[:, j] for j, k in enumerate(names)}
+        if flags:
+            out.update(warn=warn, status=status)
+        return out
 
     def set_state(self, st):
         a = {k: (np.ascontiguousarray(v, dtype=np.int32 if k in ("warn", "status") else np.float64)

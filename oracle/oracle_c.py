@@ -158,6 +158,23 @@ class _Traj(C.Structure):
                 ("nviol", _ip), ("tc", _dp)]
 
 
+def _tc_grid(tc, nsteps, n):
+    """[nsteps, n] per-step temperatures: scalar, 1-D per step [nsteps] or per cell [n]
+    (refused when nsteps == n), [nsteps, 1], [1, n] or the full grid (the library's
+    mpcekf.tc_grid rule, restated here so the checker imports nothing of the product)."""
+    a = np.asarray(tc, dtype=np.float64)
+    if a.ndim == 1 and a.size != 1:
+        if a.size == nsteps and a.size == n:
+            raise ValueError("tc_traj: 1-D vector with nsteps == ncells is ambiguous")
+        if a.size == nsteps:
+            a = a.reshape(nsteps, 1)
+        elif a.size == n:
+            a = a.reshape(1, n)
+        else:
+            raise ValueError("tc_traj: length is neither nsteps nor ncells")
+    return np.ascontiguousarray(np.broadcast_to(a, (nsteps, n)))
+
+
 def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, tc_traj=None, **cfg):
     """Batched closed loop on the CPU. Returns dict of [nsteps, ncells] arrays.
 
@@ -177,8 +194,7 @@ def run(rom, soc0, tc, nsteps, nthreads=0, want_zk=False, traj=False, tc_traj=No
     tr = None
     tcs = None
     if tc_traj is not None:
-        tcs = np.ascontiguousarray(np.broadcast_to(np.asarray(tc_traj, dtype=np.float64).reshape(nsteps, -1),
-                                                   (nsteps, n)))
+        tcs = _tc_grid(tc_traj, nsteps, n)
         tr = _Traj()
         tr.tc = _p(tcs)
     if traj:

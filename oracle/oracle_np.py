@@ -1026,6 +1026,11 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
     out["poles"] = np.full((nsteps, 7), NAN + 0j)
     out["sv"] = np.full((nsteps, 7), NAN)
     out["CL"] = np.full((nsteps, 7, 7), NAN)
+    # test infrastructure (tools/make_golden.py make_envelopes): cfg["ulp_kick"] = (seed, K)
+    # moves each step's command by a random -K..K ulps, a stand-in for the ulp-level
+    # differences between implementations of the same arithmetic (BLAS order, libm)
+    kick = c.get("ulp_kick")
+    krng = np.random.Generator(np.random.PCG64(kick[0])) if kick else None
     for k in range(nsteps):
         if tc_traj is not None:
             TC = float(tc_traj[k])
@@ -1039,6 +1044,11 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
         phise = dot(MPC["Cphi"], xhat) + uk * MPC["Dphi"] + MPC["bphi"]
         mpc["SOCk_1"] = zk[-1]
         uk, info = iter_mpc(xhat, MPC, mpc)
+        if krng is not None and np.isfinite(uk):
+            steps = int(krng.integers(-kick[1], kick[1] + 1))
+            for _ in range(abs(steps)):
+                uk = float(np.nextafter(uk, np.inf if steps > 0 else -np.inf))
+            mpc["uk_1"] = uk
         out["u"][k] = uk
         out["v"][k] = V
         out["soc"][k] = zk[-1]

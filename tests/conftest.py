@@ -43,14 +43,6 @@ def batch_inputs(n, seed=0x5EED):
     return rng.uniform(5, 30, n), rng.uniform(20, 30, n)
 
 
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_runtime_first(request):
-    """GPU sessions: initialise torch's HIP runtime before the first library context.  With
-    the library's contexts created first, a later first torch.cuda call (device buffers of
-    tests/test_gpu_configs3.py) once reported "No HIP GPUs are available" on the box; the
-    driver's full-suite order happened to initialise torch first."""
-    if any(item.get_closest_marker("gpu") for item in request.session.items):
-        import torch
-        if torch.cuda.device_count() > 0:
-            torch.cuda.init()
-    yield
+@pytest.fixture(scope="session")
+def M(P):
+    return importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")

@@ -16,6 +16,7 @@ extern "C" {
 
 void mexErrMsgIdAndTxt(const char *id, const char *fmt, ...) __attribute__((noreturn));
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]);
+int mexAtExit(void (*fn)(void));
 
 #ifdef __cplusplus
 }

@@ -259,3 +259,17 @@ int shim_call(int nlhs, mxArray **plhs, int nrhs, mxArray **prhs) {
   free_blocks();
   return 0;
 }
+
+/* mexAtExit: MATLAB runs the registered function at `clear mex` / exit; the shim runs
+ * it from shim_clear_mex() (the last registration wins, as in MATLAB). */
+static void (*g_atexit)(void);
+int mexAtExit(void (*fn)(void)) {
+  g_atexit = fn;
+  return 0;
+}
+int shim_clear_mex(void) {
+  if (!g_atexit) return 0;
+  g_atexit();
+  g_atexit = NULL;
+  return 1;
+}

@@ -57,6 +57,7 @@ def load():
         L.shim_destroy.argtypes = [vp]
         L.shim_last_error.restype = C.c_char_p
         L.shim_call.argtypes = [C.c_int, C.POINTER(vp), C.c_int, C.POINTER(vp)]
+        L.shim_clear_mex.restype = C.c_int
         _lib = L
     return _lib
 
@@ -142,6 +143,11 @@ def mex(cmd, *args, nargout=1):
         for p in ins:
             L.shim_destroy(p)
     return outs[0] if nargout == 1 else tuple(outs)
+
+
+def clear_mex():
+    """MATLAB's `clear mex`: runs the gateway's mexAtExit function; True if one was set."""
+    return bool(load().shim_clear_mex())
 
 
 def rom_struct(rom):

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     src = open(os.path.join(ROOT, "include", "mpcekf.h")).read()
-    return sorted(set(re.findall(r"\b(mpcekf_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(mpcekf_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol(P):
@@ -90,7 +90,7 @@ def test_mex_gateway_calls_only_declared_entry_points():
     import re
     src = open(os.path.join(ROOT, "matlab", "mpcekf_mex.c")).read()
     src_code = re.sub(r"/\*.*?\*/", "", src, flags=re.S)  # comments name MATLAB helpers too
-    called = set(re.findall(r"\b(mpcekf_[a-z_]+)\s*\(", src_code)) - {"mpcekf_mex"}
+    called = set(re.findall(r"\b(mpcekf_[a-z0-9_]+)\s*\(", src_code)) - {"mpcekf_mex"}
     assert called <= set(declared_symbols()), called - set(declared_symbols())
     for sym in ("mpcekf_ctx_create", "mpcekf_init_cells", "mpcekf_step", "mpcekf_plant_step", "mpcekf_ekf_step",
                 "mpcekf_linearize", "mpcekf_mpc_step_ex", "mpcekf_hildreth", "mpcekf_predmat", "mpcekf_get_state",

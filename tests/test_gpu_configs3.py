@@ -11,7 +11,8 @@ MI355X's 288 GB).  Checks:
     sample, bit for bit (runMPC.m:83-112 has no cross-cell term, so the shard boundaries
     cannot change any cell's bits).
 
-Outputs go to device buffers in 101-step chunks; only the sampled columns come back.
+Outputs go to library-allocated device buffers in 101-step chunks; only the sampled
+columns come back (pitched copies).
 """
 import os
 
@@ -34,28 +35,27 @@ def M(P):
 
 
 def _run_sampled(M, rom, soc0, tc):
-    """One context over these cells, STEPS steps, device outputs; the STRIDE-sampled
-    columns of every store plus the final status, on the host."""
-    import torch
+    """One context over these cells, STEPS steps, device outputs (library-allocated
+    buffers); the STRIDE-sampled columns of every store plus the final status, on the
+    host."""
     n = len(soc0)
-    dev = torch.device("cuda", 0)
-    bufs = [torch.empty((CHUNK, n), dtype=torch.float64, device=dev) for _ in range(4)]
-    nex = torch.empty((CHUNK, n), dtype=torch.int32, device=dev)
-    ptrs = [b.data_ptr() for b in bufs] + [nex.data_ptr()]
+    bufs = [M.DeviceBuffer((CHUNK, n), np.float64) for _ in range(4)] + [M.DeviceBuffer((CHUNK, n), np.int32)]
     parts = {k: [] for k in KEYS}
-    with M.Context(rom, n, None) as ctx:
-        ctx.init_cells(soc0, tc)
-        done = 0
-        while done < STEPS:
-            k = min(CHUNK, STEPS - done)
-            ctx.step_device(k, *ptrs)
-            torch.cuda.synchronize(dev)
-            for nm, b in zip(KEYS, bufs + [nex]):
-                parts[nm].append(b[:k, ::STRIDE].cpu().numpy())
-            done += k
-        status = ctx.get_state()["status"][::STRIDE]
-    del bufs, nex
-    torch.cuda.empty_cache()
+    try:
+        with M.Context(rom, n, None) as ctx:
+            ctx.init_cells(soc0, tc)
+            done = 0
+            while done < STEPS:
+                k = min(CHUNK, STEPS - done)
+                ctx.step_device(k, *bufs)
+                ctx.sync()
+                for nm, b in zip(KEYS, bufs):
+                    parts[nm].append(b.sampled(k, STRIDE))
+                done += k
+            status = ctx.get_state()["status"][::STRIDE]
+    finally:
+        for b in bufs:
+            b.free()
     out = {k: np.concatenate(v) for k, v in parts.items()}
     out["status"] = status
     return out

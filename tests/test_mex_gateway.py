@@ -178,10 +178,16 @@ def test_state_round_trip_mb_context(shim, rom, M):
         b = shim.mex("step", h, 15.0, nargout=5)
         for x, y, nm in zip(a, b, ("u", "v", "soc", "phise", "nexec")):
             _same(x, y, f"rerun {nm}")
-        bad = dict(ck)
-        bad.pop("mb")
-        with pytest.raises(shim.MexError, match="missing field mb"):
-            shim.mex("set_state", h, bad, nargout=0)
+        # a checkpoint without st.mb (saved before the field existed) restores the other
+        # fields and keeps the context's blend state
+        c = shim.mex("step", h, 15.0, nargout=5)
+        nomb = dict(ck)
+        nomb.pop("mb")
+        mb_now = shim.mex("get_state", h)["mb"]
+        shim.mex("set_state", h, nomb, nargout=0)
+        _same(shim.mex("get_state", h)["mb"], mb_now, "mb kept by a checkpoint without it")
+        _same(shim.mex("get_state", h)["ekf"], ck["ekf"], "ekf restored")
+        del c
         bad = dict(ck, warn=ck["warn"].astype(np.float64))
         with pytest.raises(shim.MexError, match="warn: expected"):
             shim.mex("set_state", h, bad, nargout=0)
@@ -212,3 +218,51 @@ def test_hildreth_and_predmat_through_gateway(shim, M):
         Phi_c, G_c = M.predMat(a[None], Cr[None], np.array([0.3]), Np, Nc)
         _same(Phi_m, Phi_c[0], f"Phi {Np}/{Nc}")
         _same(G_m, G_c[0], f"G {Np}/{Nc}")
+
+
+@pytest.mark.gpu
+def test_scalars_command_reads_only_requested_slots(shim, rom, M):
+    """mpcekf_mex('scalars', h, idx): the drop-ins' per-step state read (OB_step's SOCnAvg /
+    SOCpAvg, iterEKF's x0 / SigmaX0 / priorI, warn, status) equals the same rows of a full
+    get_state, and the ctypes get_scalars."""
+    n = 48
+    soc0, tc = batch_inputs(n, seed=3)
+    h = _create(shim, rom, n, {"flags": 1.0})
+    try:
+        shim.mex("init", h, soc0, tc, nargout=0)
+        shim.mex("step", h, 7.0, nargout=1)
+        st = shim.mex("get_state", h)
+        s12 = shim.mex("scalars", h, np.array([[1.0, 2.0]]))
+        assert s12.shape == (2, n)
+        _same(s12, st["scal"][0:2], "SOCnAvg/SOCpAvg")
+        s, warn, status = shim.mex("scalars", h, np.array([[3.0, 4.0, 5.0]]), nargout=3)
+        _same(s, st["scal"][2:5], "x0/SigmaX0/priorI")
+        _same(warn, st["warn"], "warn")
+        _same(status, st["status"], "status")
+        _same(shim.mex("scalars", h, np.array([[8.0, 1.0]])), st["scal"][[7, 0]], "any order")
+        with pytest.raises(shim.MexError, match="not a slot"):
+            shim.mex("scalars", h, np.array([[0.0]]))
+        with pytest.raises(shim.MexError, match="not a slot"):
+            shim.mex("scalars", h, np.array([[9.0]]))
+    finally:
+        shim.mex("destroy", h, nargout=0)
+    with M.Context(rom, n) as ctx:
+        ctx.init_cells(soc0, tc)
+        ctx.step(7, outputs=())
+        g = ctx.get_scalars(("SOCnAvg", "SOCpAvg", "vk"), flags=True)
+        full = ctx.get_state()
+    _same(np.stack([g["SOCnAvg"], g["SOCpAvg"], g["vk"]]), full["scal"][:, [0, 1, 7]].T, "ctypes get_scalars")
+    _same(g["status"], full["status"], "ctypes status")
+
+
+@pytest.mark.gpu
+def test_clear_mex_destroys_live_contexts(shim, rom):
+    """`clear mex` runs the gateway's mexAtExit function: every live context is destroyed
+    (its device memory freed) and its handle is no longer accepted."""
+    hs = [_create(shim, rom, 16) for _ in range(3)]
+    shim.mex("destroy", hs[1], nargout=0)
+    assert shim.clear_mex()
+    for h in hs:
+        with pytest.raises(shim.MexError, match="not a live mpcekf context"):
+            shim.mex("init", h, np.zeros(16) + 20, np.zeros(16) + 25, nargout=0)
+    assert not shim.clear_mex()        # nothing registered until the next create

@@ -6,14 +6,17 @@ import sys
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
+
+# torch is imported inside the tests and workers only: a GPU session collects this module
+# too, and torch's bundled HIP runtime must never be mapped next to the library's
+# (tests/test_gpu_runtime.py).
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _worker(rank, world, port, cpg, steps, q):
+    import torch
+    import torch.distributed as dist
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -41,6 +44,7 @@ def _worker(rank, world, port, cpg, steps, q):
 
 def test_two_rank_shards_equal_single_process(oc, rom):
     import bench
+    import torch.multiprocessing as mp
     world, cpg, steps = 2, 24, 40
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
