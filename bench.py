@@ -36,7 +36,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s peak (spec)
 METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=32, Np=5, Nc=2):
+LAZY_H = 64  # the library's input-ring length = flush period (mpcekf_kernels.hpp MPCEKF_LAZY_H)
+
+
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2):
     """Algorithmic HBM bytes each kernel moves per cell per launch:
     the state it must read and write once, with nothing re-read.
 
@@ -374,9 +377,11 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
     # steps (the library default; every flush step is sampled); the rolling schedule
     # (MPCEKF_FLUSH_ROLL=1) flushes one slice of ncell / period cells every step on a second
     # stream beside k_bounds / Hildreth
-    period = int(os.environ.get("MPCEKF_FLUSH_PERIOD", "32"))
     roll = os.environ.get("MPCEKF_FLUSH_ROLL", "0") != "0"
-    n_flush = K if roll else K // period + (1 if K % period else 0)
+    # every flush step is sampled (--timing-every divides the flush period), so the sampled
+    # flush launches are the timed region's flushes
+    n_flush = K if roll else tim.get("flush", (0.0, 0))[1]
+    period = int(os.environ.get("MPCEKF_FLUSH_PERIOD", str(LAZY_H)))  # the rolling schedule's slices
     cells_per_launch = {k: (ncell / period if (k == "flush" and roll) else ncell) for k in tim}
     per_kernel = {k: dict(ms_per_launch=tim[k][0] / max(tim[k][1], 1), launches_timed=tim[k][1],
                           launches=(n_flush if k == "flush" else K))

@@ -283,9 +283,10 @@ int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
 #define MPCEKF_PROB_DOUBLES 51
 int mpcekf_get_hild_problems(mpcekf_ctx *ctx, double *prob, int32_t *hflag);
 /* Profiling builds only (-DMPCEKF_STAMPS, tools/stamps.py): shader-clock stamps at the
- * MPCEKF_NSTAMPS section boundaries of the EKF/MPC kernel for the last fused step,
- * [MPCEKF_NSTAMPS][ncells].  *nstamps = 0 (and nothing written) in normal builds. */
-#define MPCEKF_NSTAMPS 12
+ * section boundaries of the EKF/MPC kernel (rows 0..11) and the plant kernel (rows
+ * 12..19) for the last fused step, [MPCEKF_NSTAMPS][ncells].  *nstamps = 0 (and nothing
+ * written) in normal builds. */
+#define MPCEKF_NSTAMPS 20
 int mpcekf_get_stamps(mpcekf_ctx *ctx, int64_t *stamps, int32_t *nstamps);
 
 /* ---- device memory (not part of the reference interface) ----

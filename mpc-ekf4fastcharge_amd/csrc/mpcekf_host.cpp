@@ -530,6 +530,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.ts_ekf = X->d_ts; s.ts_plant = X->d_ts + n * NM;
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
   s.mb = X->d_mb;
+  s.stamps = X->d_stamps;
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n;
   if (X->wide) {

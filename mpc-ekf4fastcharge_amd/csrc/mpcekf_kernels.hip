@@ -63,9 +63,16 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
   do {                                                                                    \
     if (io.stamps) io.stamps[(size_t)(i) * s.n + c] = (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
+#define STAMPP(i)                                                                                  \
+  do {                                                                                             \
+    if (s.stamps) s.stamps[(size_t)(12 + (i)) * s.n + c] = (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define STAMP(i) \
   do {           \
+  } while (0)
+#define STAMPP(i) \
+  do {            \
   } while (0)
 #endif
 
@@ -1348,6 +1355,20 @@ __device__ __forceinline__ void stage_lds(double *dst, const double *src, int le
   if ((len & 1) && threadIdx.x == 0) dst[len - 1] = src[len - 1];
 }
 
+// The ring inputs of a replay are loaded RCH steps at a time, all in flight together:
+// a model first touched after a set-point crossing has up to LAZY_H - 1 skipped steps,
+// and a load per step inside the loop waited one memory round trip each.  The FMAs then
+// run in step order, so the bits are the per-step loop's.
+#ifndef MPCEKF_RING_CHUNK
+#define MPCEKF_RING_CHUNK 8
+#endif
+constexpr int RCH = MPCEKF_RING_CHUNK;
+// ring[k % LAZY_H] for k = k0 .. k0 + RCH - 1 (clamped to kmax: a valid slot)
+__device__ __forceinline__ void ring_chunk(const double *ring, const KState &s, int64_t c, int k0, int kmax,
+                                           double v[RCH]) {
+#pragma unroll
+  for (int i = 0; i < RCH; ++i) v[i] = ring[(size_t)(min(k0 + i, kmax) % LAZY_H) * s.n + c];
+}
 // ---------------------------------------------------------------------------
 // k_plant: OB_step simStep outputs for every cell (lane per cell)
 // ---------------------------------------------------------------------------
@@ -1504,6 +1525,12 @@ template <bool GR>
 __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KState s, const double *iapp,
                                                          double *vout, const int lazy_t, const double *tc_in) {
   extern __shared__ double lds[];
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = (int)(gt & 3);
+  const int64_t c = gt >> 2;  // a quad is one cell: every exit below is quad-uniform
+#ifdef MPCEKF_STAMPS
+  if (c < s.n && j == 0 && s.stamps) s.stamps[(size_t)19 * s.n + c] = (long long)__builtin_amdgcn_s_memtime();
+#endif
   const int lo = GR ? r.plant_tab : 0;
   stage_lds(lds, r.plant_blob + lo, r.plant_len - lo);
   __syncthreads();
@@ -1511,11 +1538,9 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
   const double *L = GR ? r.plant_blob : lds;
   const double *Tp = tb + r.plant_tab + r.plant_tablen;
   const double *Zp = Tp + MAXT;
-  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int j = (int)(gt & 3);
-  const int64_t c = gt >> 2;  // a quad is one cell: every exit below is quad-uniform
   if (gt == 0 && lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
   if (c >= s.n) return;
+  STAMPP(0);
   const double Iapp = iapp[c];
   const double tcs = tc_in ? tc_in[c] : s.Tc[c];
   const double priorI = s.priorI[c];
@@ -1549,6 +1574,7 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
     two_nearest(Tp, r.nT, T, a, b);
     iTu = a > b ? a : b; iTl = a < b ? a : b;
   }
+  STAMPP(1);
   // this lane's corner: mm = {Tl Zl, Tl Zu, Tu Zl, Tu Zu}[j]
   const int mj = ((j & 2) ? iTu : iTl) * r.nZ + ((j & 1) ? iZu : iZl);
   double *bx = s.bigx + ((size_t)c * r.NM + mj) * 6;
@@ -1575,13 +1601,19 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
   double aZ = 0.0, aT = 0.0;
   if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
   if (Tu != Tl) aT = (T - Tl) / (Tu - Tl);
+  STAMPP(2);
   const double *a = L + mj * PREC + NPLANT * NX + 2 * NPLANT;
-  if (lazy_t)
-    for (int k = tsj + 1; k < lazy_t; ++k) {  // OB_step.m:198-200 for the skipped steps
-      const double u = s.hist_u[(size_t)(k % LAZY_H) * s.n + c];
+  if (lazy_t)  // OB_step.m:198-200 for the skipped steps, RCH ring inputs per round trip
+    for (int k0 = tsj + 1; k0 < lazy_t; k0 += RCH) {
+      double u[RCH];
+      ring_chunk(s.hist_u, s, c, k0, lazy_t - 1, u);
 #pragma unroll
-      for (int e = 0; e < 6; ++e) xs[e] = __builtin_fma(a[e], xs[e], u);
+      for (int i = 0; i < RCH; ++i)
+        if (k0 + i < lazy_t)
+#pragma unroll
+          for (int e = 0; e < 6; ++e) xs[e] = __builtin_fma(a[e], xs[e], u[i]);
     }
+  STAMPP(3);
   const double *B = L + mj * PREC;
   double yk[NPLANT];
 #pragma unroll
@@ -1595,6 +1627,7 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
     yk[q] = (1 - aT) * ((1 - aZ) * y0 + aZ * y1) + aT * ((1 - aZ) * y2 + aZ * y3);
     __builtin_amdgcn_sched_barrier(0);  // one row's LDS operands at a time: 128 VGPRs at 4 waves/SIMD
   }
+  STAMPP(4);
   double th0 = fmin(fmax(yk[R_TH0] + SOC0n, 1e-6), 1 - 1e-6);
   double th3 = fmin(fmax(yk[R_TH3] + SOC0p, 1e-6), 1 - 1e-6);
   double te1 = fmax(yk[R_TE1] + 1, 1e-6);
@@ -1607,6 +1640,7 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
   const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
   double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
   V = V - r.Rc * Iapp;
+  STAMPP(5);
   if (j == 0) {
     s.SOCn[c] = SOCnAvg;
     s.SOCp[c] = SOCpAvg;
@@ -1624,6 +1658,7 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
     p[2] = make_double2(x[4], x[5]);
     s.ts_plant[c * r.NM + mj] = lazy_t;
   }
+  STAMPP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -1885,11 +1920,20 @@ __global__ void __launch_bounds__(256) k_flush_coal(const KRom r, const KCfg cf,
 // The skipped time updates of one model, steps ts+1..t (pt = the step-t input).
 __device__ __forceinline__ void replay_x(double x[NX], const double *a, int ts, int t, double pt, const KState &s,
                                         int64_t c) {
-  for (int k = ts + 1; k <= t; ++k) {
-    const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+  if (ts + 1 < t) {  // steps before t: their inputs from the ring
+    for (int k0 = ts + 1; k0 < t; k0 += RCH) {
+      double p[RCH];
+      ring_chunk(s.hist_p, s, c, k0, t - 1, p);
 #pragma unroll
-    for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], x[e], p);
+      for (int i = 0; i < RCH; ++i)
+        if (k0 + i < t)
+#pragma unroll
+          for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], x[e], p[i]);
+    }
   }
+  if (ts < t)
+#pragma unroll
+    for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], x[e], pt);
 }
 // a: the model's diag(A) [NX] followed by its a_p a_q coefficients [NPK] (cell blob)
 __device__ __forceinline__ void replay_S(double S[NPK], const double *a, int ts, int t, double W) {
@@ -1926,12 +1970,19 @@ __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc
   for (int j = 0; j < 4; ++j) {
     if (!need[j]) continue;
     const double *a = cc.L + m[j] * cc.stride + NZ * NX + NZ;  // diag(A) of the model (cell blob)
-    for (int k = ts[j] + 1; k <= t; ++k) {
-      const double p = k == t ? pt : s.hist_p[(size_t)(k % LAZY_H) * s.n + c];
+    for (int k0 = ts[j] + 1; k0 <= t; k0 += RCH) {
+      double p[RCH];
+      if (k0 < t) ring_chunk(s.hist_p, s, c, k0, t - 1, p);
 #pragma unroll
-      for (int e = 0; e < NX; ++e) x[j][e] = __builtin_fma(a[e], x[j][e], p);
+      for (int i = 0; i < RCH; ++i) {
+        const int k = k0 + i;
+        if (k > t) break;
+        const double pk_ = k == t ? pt : p[i];
 #pragma unroll
-      for (int i = 0; i < NPK; ++i) S[j][i] = __builtin_fma(a[NX + i], S[j][i], W);
+        for (int e = 0; e < NX; ++e) x[j][e] = __builtin_fma(a[e], x[j][e], pk_);
+#pragma unroll
+        for (int q = 0; q < NPK; ++q) S[j][q] = __builtin_fma(a[NX + q], S[j][q], W);
+      }
     }
   }
 #pragma unroll
@@ -3022,6 +3073,15 @@ __device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int6
   }
 }
 
+#ifndef MPCEKF_HILD_INLINE_SLOW  // k_hild finishes its slow lanes itself (no k_hild_slow launch)
+#define MPCEKF_HILD_INLINE_SLOW 1
+#endif
+__device__ __forceinline__ void hild_slow_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c);
+// out of line: the exact-rule path keeps its registers out of the fast sweep's allocation
+__device__ __noinline__ void hild_slow_wave(const KCfg &cf, const KState &s, const KIO &io, int64_t c) {
+  hild_slow_cell(cf, s, io, c);
+}
+
 // hildreth.m + iterMPC.m:68-95, lane per cell: the fast solve (hild_fast).
 __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -3044,12 +3104,21 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
   extern __shared__ double2 hlds[];
   int nexec;
   const bool slow = hild_fast(Cn, E, lam, cf.max_hild, cf.hild_tol, K, !qp, hild_lane_lds(hlds), s.lam + c, n, nexec);
-  if (__any(slow) && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))
-    atomicAdd(s.hslow, 1);  // one add per wave: k_hild_slow has work
-  if (!qp) return;
-  if (slow) {  // k_hild_slow finishes it (warm start still in s.lam)
-    s.hflag[c] = 2;
-    return;
+  if (MPCEKF_HILD_INLINE_SLOW) {
+    // the rare wave with a lane outside the fast form's domain redoes that lane with the
+    // exact rules here (warm start still in s.lam), the wave's other lanes riding along on
+    // the dummy problem: no second kernel, whose launch cost ~4 us a step even when empty
+    if (qp && slow) s.hflag[c] = 2;
+    if (__any(slow)) hild_slow_wave(cf, s, io, c);
+    if (!qp || slow) return;
+  } else {
+    if (__any(slow) && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))
+      atomicAdd(s.hslow, 1);  // one add per wave: k_hild_slow has work
+    if (!qp) return;
+    if (slow) {  // k_hild_slow finishes it (warm start still in s.lam)
+      s.hflag[c] = 2;
+      return;
+    }
   }
   double Mtl[NC];
   hild_mtl(Cn, lam, Mtl);
@@ -3636,8 +3705,10 @@ int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
     attr = true;
   }
   hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), hild_lds_bytes(), (hipStream_t)stream, c, s, io);
-  const int gs = grid_for(s.n, 64) < 256 ? grid_for(s.n, 64) : 256;
-  hipLaunchKernelGGL(k_hild_slow, dim3(gs), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);
+  if (!MPCEKF_HILD_INLINE_SLOW) {
+    const int gs = grid_for(s.n, 64) < 256 ? grid_for(s.n, 64) : 256;
+    hipLaunchKernelGGL(k_hild_slow, dim3(gs), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);
+  }
   return (int)hipGetLastError();
 }
 

@@ -16,7 +16,14 @@ constexpr int MAXZ = 40;   // max SOC set-points
 constexpr int MAXROWS = 64;
 constexpr int NPLANT = 9;  // role rows the plant needs (OB_step.m:289-344)
 constexpr int PREC = NPLANT * NX + NPLANT + NPLANT + 6;  // plant blob record per model: C[9][5], res0[9], D[9], a[6]
-constexpr int LAZY_H = 32;  // deferred time update: input ring length = flush period (steps)
+// 64: with the ring inputs of a replay loaded 8 steps per round trip (mpcekf_kernels.hip
+// ring_chunk), the longer replays of a 64-step ring cost less than the halved flush saves
+// (same-box A/B, profiles/r04f_ab_lazy64.txt: 2.64e8 vs 2.60e8); at 32 steps with a load per
+// replayed step it had been the other way round
+#ifndef MPCEKF_LAZY_H
+#define MPCEKF_LAZY_H 64
+#endif
+constexpr int LAZY_H = MPCEKF_LAZY_H;  // deferred time update: input ring length = flush period (steps)
 constexpr int MAXTT = 8;
 constexpr int MBREC = 42;   // model-blend state per cell: xhat[5], pad, Sigma 6x6 row-major
 constexpr int KF_MB = 1 << 8;  // KCfg.flags: model-blend EKF (mpcekf_config.method == 1)    // max electrode-table temperatures (mpcekf_rom.tab_ntemp)
@@ -77,6 +84,7 @@ struct KState {
   // of the last LAZY_H steps sit in per-cell rings
   int *ts_ekf, *ts_plant;    // [n][NM]
   double *hist_p, *hist_u;   // [LAZY_H][n] priorI (EKF) and Iapp (plant) of step t at slot t % LAZY_H
+  long long *stamps;         // [NSTAMPS][n] section clocks (-DMPCEKF_STAMPS builds only, else null)
 };
 
 // Inputs/outputs of one cell-kernel launch.  Any pointer may be null.
@@ -102,7 +110,7 @@ struct KIO {
   double *junc_out, *jfin_out, *normdu_out;  // [n] J_uncon, J_final, norm_DU
   int *nviol_out;         // [n] viol
 };
-constexpr int NSTAMPS = 12;
+constexpr int NSTAMPS = 20;  // k_cell sections 0..11, k_plant 12..19
 // k_cell -> k_bounds record: g[4], m[4], getChatZ's getChatV scalars at the updated state
 // (Rfn, Rfp, Rctn, Rctp, dUn0, dUp3 of chat_k; its Chat0), res0n, res0p, dUn, dUp
 // (iterEKF.m:562-580), SigmaX0.  k_bounds reads corner 1's Sigma from the EKF record

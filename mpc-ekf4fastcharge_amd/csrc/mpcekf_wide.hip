@@ -633,13 +633,21 @@ __device__ __forceinline__ double row_m(int i, const double *mp) {
 // X's columns 8 .. Nc-1 (lanes 0 .. Nc-9 of a group use them) are held spread over the
 // group: row u's pair sits in lanes 2q, 2q + 1 (q = u % 4) at register slot u / 4, and is
 // moved into lanes 0, 1 by one row_shl:2q when row u runs.  80 more doubles per lane for
-// column k + 8 did not fit beside column k's 80.  The other lanes receive stray values
-// there (finite: X is finite on this path), which every use masks: their M entries for
-// columns >= 8 are read from the zero row, and the Cu rows select on the lane.
+// column k + 8 did not fit beside column k's 80.  The other lanes receive the values of
+// lanes further up the group, or +0 where the shift reads past the 16-lane DPP row
+// (bound_ctrl: a defined zero, not a stale register), which every use masks: their M
+// entries for columns >= 8 are read from the zero row, and the Cu rows select on the lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp64_zf(double v) {  // invalid source lanes read +0
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 template <int Q>
 __device__ __forceinline__ double x1_to_lanes01(double v) {
   if constexpr (Q == 0) return v;
-  else return dpp64<0x100 + 2 * Q>(v);  // row_shl:2Q
+  else return dpp64_zf<0x100 + 2 * Q>(v);  // row_shl:2Q
 }
 __device__ __forceinline__ double x1_to_lanes01(double v, int q) {  // q a constant after unrolling
   switch (q) {

@@ -218,14 +218,38 @@ def test_runmpc_cell_full_charge(rom, oc, M):
         assert _rel(out[k][:agree], g[k][:agree]).max() <= RTOL_NORTH_STAR, k
 
 
+def test_runmpc_tail_inside_ulp_envelope(rom, M):
+    """configs[0]'s last ~200 steps, where the single numpy fixture cannot hold any
+    implementation (test_runmpc_cell_full_charge): the GPU trajectory lies inside the
+    per-step envelope of the MATLAB-faithful restatement's ulp ensemble (SOC0 -8..+8 ulps,
+    and 32 members with a random -1..1 ulp kick of the command every step) widened by
+    north_star's 1e-6, at every step of 2,800-3,001, and reaches 90 % SOC at the step the
+    ensemble does (tests/envelope.py; tools/make_golden.py make_envelopes)."""
+    import envelope
+    out = M.runMPC(rom, np.array([10.0]), np.array([25.0]), 3001)
+    envelope.check_run(out, envelope.load("env_runmpc_3001"))
+
+
+def test_wide_near_limit_tails_in_ensemble_distribution(rom, M):
+    """The Np = 20 near-limit cells over steps 25-200 (the dense-H fixture test holds only
+    the first 25 of three cells): their closed loops are chaotic, so the GPU's window mean,
+    10th / 90th percentiles of u, v, soc, phise and final SOC are held inside the range of
+    the same statistics over the MATLAB-faithful restatement's 25-member ulp ensemble
+    (tests/envelope.py)."""
+    import envelope
+    w = envelope.load("env_wide_near4_200")
+    out = M.runMPC(rom, w["soc0"], w["tc"], 200, cfg=M.make_config(Np=20, Nc=10))
+    envelope.check_near(out, w)
+
+
 def test_deferred_time_update_is_schedule_invariant(rom, M):
-    """The fused step defers the all-model time update (ring of LAZY_H = 32 inputs,
-    flush every 32 steps and at the end of each call).  Splitting the same run into
+    """The fused step defers the all-model time update (ring of LAZY_H = 64 inputs,
+    flush every 64 steps and at the end of each call).  Splitting the same run into
     calls that straddle the flush boundaries must give bit-identical trajectories
     and an identical full state (every local model's record and plant state)."""
     n = 2048
     soc0, tc = batch_inputs(n, seed=9)
-    chunks = [1, 31, 32, 33, 53, 250]
+    chunks = [1, 31, 32, 33, 53, 63, 64, 65, 250]
     with M.Context(rom, n) as a, M.Context(rom, n) as b:
         a.init_cells(soc0, tc)
         b.init_cells(soc0, tc)
@@ -260,10 +284,10 @@ def test_flush_period_is_exact(rom, M):
     """The deferred time update gives the same bits for any flush period <= the ring, with
     every cell flushed at once on the step's stream (the default) and with the rolling
     schedule (MPCEKF_FLUSH_ROLL=1: one cell slice per step on a second stream)."""
-    n = 1000  # slices of unequal size for P = 7 and 32
+    n = 1000  # slices of unequal size for P = 7, 32 and 64
     soc0, tc = batch_inputs(n, seed=22)
     runs = [_run_with_env(M, rom, soc0, tc, 300, MPCEKF_FLUSH_PERIOD=p, MPCEKF_FLUSH_ROLL=roll)
-            for p, roll in ((32, 0), (1, 0), (7, 0), (32, 1), (7, 1))]
+            for p, roll in ((64, 0), (1, 0), (7, 0), (32, 0), (64, 1), (7, 1))]
     for r in runs[1:]:
         for k in ("u", "v", "soc", "phise", "nexec"):
             np.testing.assert_array_equal(r[k], runs[0][k], err_msg=k)

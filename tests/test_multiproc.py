@@ -67,7 +67,7 @@ def test_bench_algorithmic_bytes():
     import bench
     b = bench.algorithmic_bytes_per_cell(63, 23, True)
     # 416*NM state bytes, + model timestamps and the two input rings
-    assert b["flush"] == 416 * 63 + 2 * 2 * 4 * 63 + 2 * 8 * 32
+    assert b["flush"] == 416 * 63 + 2 * 2 * 4 * 63 + 2 * 8 * bench.LAZY_H
     assert bench.survey_bytes_per_cell_step(63, 23) == 26736
 
 

@@ -332,3 +332,29 @@ def test_c_oracle_temperature_profile_matches_golden(P, oc):
     # the profile matters: a constant TC gives different trajectories
     c = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=4)
     assert rel(c["v"], g["v"]).max() > 1e-4
+
+
+def test_c_oracle_tails_inside_ulp_envelopes(rom, oc):
+    """The C oracle's defined arithmetic (the GPU's, bit for bit) against the MATLAB-faithful
+    restatement's ulp ensembles where single trajectories part (tests/envelope.py): the
+    runMPC.m cell inside the per-step envelope over steps 2,800-3,001 with the same step
+    to 90 % SOC; the Np = 20 near-limit cells inside the members' window statistics over
+    steps 25-200."""
+    import envelope
+    e = envelope.load("env_runmpc_3001")
+    envelope.check_run(oc.run(rom, np.array([10.0]), np.array([25.0]), 3001, nthreads=1), e)
+    w = envelope.load("env_wide_near4_200")
+    envelope.check_near(oc.run(rom, w["soc0"], w["tc"], 200, nthreads=4, Np=20, Nc=10), w)
+
+
+def test_ulp_envelopes_are_not_vacuous():
+    """The envelopes do bind: in the runMPC tail the members spread by O(1e-2) relative in u
+    (the single-fixture window ends where that spread starts), and before step ~2,890 the
+    envelope is ulp-tight; the near-limit members' window means differ between cells."""
+    import envelope
+    e = envelope.load("env_runmpc_3001")
+    spread = (e["u_max"] - e["u_min"]) / np.abs(e["u_max"]).clip(1e-9)
+    assert spread[:2850].max() < 1e-6 and spread[2900:].max() > 1e-3
+    w = envelope.load("env_wide_near4_200")
+    assert (w["u_wmean"].max(1) - w["u_wmean"].min(1) >= 0).all()
+    assert np.ptp(w["soc_wmean"].mean(1)) > 0.01

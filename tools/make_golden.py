@@ -111,6 +111,9 @@ def _env_cell(args):
     return {k: o[k] for k in ("u", "v", "soc", "phise", "nexec")}
 
 
+NEAR_WINDOW = (25, 200)  # the near-limit cells' steps the single-fixture test cannot hold
+
+
 def make_envelopes(rom, hsh):
     """Tail envelopes of the MATLAB-faithful restatement where single trajectories part
     (VERDICT r03 item 5).  Near the end of the runMPC.m charge (steps ~2,900-3,001) and on
@@ -155,6 +158,12 @@ def make_envelopes(rom, hsh):
     for k in ("u", "v", "soc", "phise"):
         a = np.stack([np.stack([near[c * per + j][k] for j in range(per)], 1) for c in range(4)], 1)  # [200, 4, m]
         env[k + "_min"], env[k + "_max"] = a.min(2), a.max(2)
+        # the chaotic cells' members range over the attractor (u between the current limits):
+        # per-member window statistics [4, m] hold a trajectory in distribution (tests/envelope.py)
+        w = a[NEAR_WINDOW[0]:NEAR_WINDOW[1]]
+        env[k + "_wmean"] = w.mean(0)
+        env[k + "_wlo"], env[k + "_whi"] = np.percentile(w, 10, axis=0), np.percentile(w, 90, axis=0)
+    env["soc_end"] = np.stack([np.stack([near[c * per + j]["soc"][-1] for j in range(per)]) for c in range(4)])
     np.savez_compressed(os.path.join(OUT, "env_wide_near4_200.npz"), rom_hash=hsh, soc0=soc0n, tc=tcn, Np=20, Nc=10,
                         ulps=ks9, kicked=NK_NEAR, **env)
 

@@ -28,17 +28,27 @@ soc0, tc = bench.batch_inputs(n)
 ctx = M.Context(rom, n, M.make_config(bounds=True))
 ctx.init_cells(soc0, tc)
 acc = []
+pacc = []
+PNAMES = ["entry: blob staging + barrier", "scalar loads + bracket + two_nearest", "corner gather issue + Cdleff/res0/SOC", "corner replay",
+          "rows + blend (DPP)", "clamps, k0, asinh, Uocp, Rf, V", "stores + corner advance"]
 for k in range(steps):
     ctx.step(1, outputs=())
     if k % 25 == 5:
         st = ctx.get_stamps()
         if st is None:
             sys.exit("not a profiling build: set MPCEKF_LIB to _build/libmpcekf_stamps.so")
-        w = st.reshape(st.shape[0], -1, 64).max(axis=2).astype(np.float64)  # [stamp][wave]
-        d = np.diff(w, axis=0)                                              # [section][wave]
+        w = st.reshape(st.shape[0], -1, 64).max(axis=2).astype(np.float64)  # [stamp][64 cells]
+        d = np.diff(w[:12], axis=0)                                         # [section][wave]
         acc.append(np.median(d, axis=1))
+        dp = np.diff(np.concatenate([w[19:20], w[12:19]]), axis=0)  # k_plant(4): entry, sections
+        pacc.append(np.median(dp, axis=1))
 a = np.array(acc)
 tot = a.sum(1)
 print(f"k_cell sections (median over waves, shader cycles; {len(a)} sampled steps, total median {np.median(tot):.0f}):")
 for i, nm in enumerate(NAMES):
     print(f"  {nm:28s} {np.median(a[:, i]):9.0f}  ({100 * np.median(a[:, i] / tot):4.1f} %)")
+p = np.array(pacc)
+ptot = p.sum(1)
+print(f"k_plant sections (median, shader cycles; total median {np.median(ptot):.0f}):")
+for i, nm in enumerate(PNAMES):
+    print(f"  {nm:40s} {np.median(p[:, i]):9.0f}  ({100 * np.median(p[:, i] / ptot):4.1f} %)")
