@@ -39,7 +39,7 @@ METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 LAZY_H = 64  # the library's input-ring length = flush period (mpcekf_kernels.hpp MPCEKF_LAZY_H)
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2):
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, bounds_kernel=False, plant_kernel=False):
     """Algorithmic HBM bytes each kernel moves per cell per launch:
     the state it must read and write once, with nothing re-read.
 
@@ -49,10 +49,11 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2):
     cell : the 4 corner EKF records read + written, their timestamps, the step's
            ring input, per-cell scalars/constants, outputs u/v/soc/phise, zk,
            the QP record (+ the 14-double boundzk hand-off record).
-    bounds: the hand-off record and corner 1's packed Sigma read, 4 per-cell
-           constants read, boundzk (28) written.
+    bounds: (k_bounds, when launched) the hand-off record and corner 1's packed Sigma
+           read, 4 per-cell constants read, boundzk (28) written; by default k_cell
+           evaluates boundzk itself (corner 1's Sigma read, boundzk written, no record).
     plant: the 4 corner plant states read + written, timestamps, ring writes,
-           per-cell scalars.
+           per-cell scalars (k_cell's own bytes when it runs the plant, the default).
     hild : the QP record read, lambda read + written, outputs.
     """
     flush = 2 * 8 * NM * (20 + 6) + 2 * 2 * 4 * NM + 2 * 8 * lazy_h
@@ -68,8 +69,13 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2):
         cell = cell - 51 * 8 + 36 * 8
         hild = 2 * 8 * (36 + prob + ncon * (Nc + 2)) + 2 * 8 * ncon + 4 * 8
     out = dict(flush=flush, cell=cell, plant=plant, hild=hild)
-    if bounds:
+    if not plant_kernel:  # k_cell runs OB_step's simStep first (KRom::cell_plant): its bytes are k_cell's
+        out["cell"] = cell = cell + plant
+        del out["plant"]
+    if bounds and bounds_kernel:
         out["bounds"] = 14 * 8 + 15 * 8 + 4 * 8 + 28 * 8
+    elif bounds:  # k_cell evaluates boundzk: no hand-off record; corner 1's Sigma read, boundzk written
+        out["cell"] = cell - 14 * 8 + 15 * 8 + 28 * 8
     return out
 
 
@@ -371,7 +377,10 @@ def main():
 def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, soc0_all, tc_all, world):
     """Rank 0's roofline / per-kernel / CPU-baseline objects (rank 0's shard timings)."""
     ncon = 4 * args.nc + 3 * args.np
-    bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc)
+    # boundzk is evaluated inside k_cell unless a k_bounds launch was timed
+    bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc,
+                                     bounds_kernel=tim.get("bounds", (0.0, 0))[1] > 0,
+                                     plant_kernel=tim.get("plant", (0.0, 0))[1] > 0)
     # HIP-event averages over the sampled launches (--timing-every), so a kernel's share of
     # a step is its average x its launches per step.  k_flush flushes every cell each period
     # steps (the library default; every flush step is sampled); the rolling schedule

@@ -344,36 +344,47 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       const double *t = fn == 0 ? e->Uocp : fn == 1 ? e->dUocp : fn == 2 ? e->k0 : fn == 3 ? e->Rf : e->Cdleff;
       tabs.insert(tabs.end(), t, t + (size_t)nte * nth);
     }
-  const size_t cell_tablen = tabs.size() - (size_t)2 * nte * nth;  // k_cell / k_bounds: no Cdleff
+  // k_cell / k_bounds need no Cdleff table, unless k_cell also runs the plant (cell_plant)
+  const char *cpe = getenv("MPCEKF_CELL_PLANT");
+  bool cell_plant = !(cpe && atoi(cpe) == 0);
+  auto cell_tablen_of = [&](bool cp) { return tabs.size() - (cp ? 0 : (size_t)2 * nte * nth); };
   std::vector<double> pts(MAXT + MAXZ, 0.0);
   for (int t = 0; t < nT; ++t) pts[t] = R->T_degC[t] + 273.15;  // ROMmdls(t,z).T (initKF.m:58)
   for (int z = 0; z < nZ; ++z) pts[MAXT + z] = R->SOC_pct[z] / 100;  // ROMmdls(t,z).SOC
   auto Cval = [&](int m, int q, int k) { return R->C[((size_t)m * nz + q) * n1 + k]; };
   auto Dval = [&](int m, int q) { return R->D[(size_t)m * nz + q]; };
   // cell blob: per model [C nzp x 5][D nzp][a 5][a_p a_q, packed Sigma order 15]
-  // An odd stride in doubles: lanes reading one offset of different models then spread
-  // over all LDS banks (an even stride such as 176 folds them onto 2 bank positions).
-  r.cell_stride = (nzp * NX + nzp + NX + NPK) | 1;
+  // (+ [res0 of the 9 plant rows] when k_cell runs the plant).  An odd stride in doubles:
+  // lanes reading one offset of different models then spread over all LDS banks (an even
+  // stride such as 176 folds them onto 2 bank positions).
   int pr[NPK], pc[NPK];
   for (int p = 0, i = 0; p < NX; ++p)
     for (int q = p; q < NX; ++q, ++i) { pr[i] = p; pc[i] = q; }
-  std::vector<double> cb((size_t)NM * r.cell_stride, 0.0);
-  for (int m = 0; m < NM; ++m) {
-    double *b = cb.data() + (size_t)m * r.cell_stride;
-    for (int q = 0; q < nz; ++q) {
-      for (int k = 0; k < NX; ++k) b[q * NX + k] = Cval(m, perm[q], k);  // initKF.m:91 strips res0
-      b[nzp * NX + q] = Dval(m, perm[q]);
+  std::vector<double> cb;
+  auto make_cell_blob = [&](bool cp) {
+    r.cell_stride = (nzp * NX + nzp + NX + NPK + (cp ? NPLANT : 0)) | 1;
+    cb.assign((size_t)NM * r.cell_stride, 0.0);
+    for (int m = 0; m < NM; ++m) {
+      double *b = cb.data() + (size_t)m * r.cell_stride;
+      for (int q = 0; q < nz; ++q) {
+        for (int k = 0; k < NX; ++k) b[q * NX + k] = Cval(m, perm[q], k);  // initKF.m:91 strips res0
+        b[nzp * NX + q] = Dval(m, perm[q]);
+      }
+      for (int k = 0; k < NX; ++k) b[nzp * NX + nzp + k] = R->A[(size_t)m * n1 + k];
+      for (int i = 0; i < NPK; ++i)  // Sigma time update coefficients (iterEKF.m:78)
+        b[nzp * NX + nzp + NX + i] = R->A[(size_t)m * n1 + pr[i]] * R->A[(size_t)m * n1 + pc[i]];
+      if (cp)  // the plant's res0 column (OB_step.m:272-275; Phise rows are not among the 9)
+        for (int q = 0; q < NPLANT; ++q) b[nzp * NX + nzp + NX + NPK + q] = Cval(m, perm[q], NX);
     }
-    for (int k = 0; k < NX; ++k) b[nzp * NX + nzp + k] = R->A[(size_t)m * n1 + k];
-    for (int i = 0; i < NPK; ++i)  // Sigma time update coefficients (iterEKF.m:78)
-      b[nzp * NX + nzp + NX + i] = R->A[(size_t)m * n1 + pr[i]] * R->A[(size_t)m * n1 + pc[i]];
-  }
-  if (cb.size() & 1) cb.push_back(0.0);  // tables at an even offset: 16-byte staging in rom_global mode
-  r.cell_tab = (int)cb.size();
-  r.cell_tablen = (int)cell_tablen;
-  cb.insert(cb.end(), tabs.begin(), tabs.begin() + cell_tablen);
-  cb.insert(cb.end(), pts.begin(), pts.end());
-  r.cell_len = (int)cb.size();
+    if (cb.size() & 1) cb.push_back(0.0);  // tables at an even offset: 16-byte staging in rom_global mode
+    r.cell_tab = (int)cb.size();
+    r.cell_tablen = (int)cell_tablen_of(cp);
+    cb.insert(cb.end(), tabs.begin(), tabs.begin() + r.cell_tablen);
+    cb.insert(cb.end(), pts.begin(), pts.end());
+    r.cell_len = (int)cb.size();
+    r.cell_plant = cp;
+  };
+  make_cell_blob(cell_plant);
   // plant blob: per model [C 9 x 5][res0 9][D 9] over role rows 0..8
   std::vector<double> pb((size_t)NM * PREC, 0.0);
   for (int m = 0; m < NM; ++m) {
@@ -407,6 +418,9 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   auto lds_need = [&]() { return std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r)), plant_lds_bytes(r)); };
   const char *gev = getenv("MPCEKF_ROM_GLOBAL");
   r.rom_global = gev && atoi(gev) == 1;
+  // the plant's extras (res0 column, Cdleff tables) only while the whole cell blob still
+  // fits the LDS; otherwise the plain blob and the separate k_plant
+  if (cell_plant && !r.rom_global && cell_lds_bytes(r) > 160 * 1024) make_cell_blob(false);
   if (lds_need() > 160 * 1024) r.rom_global = 1;
   if (lds_need() > 160 * 1024)
     return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of electrode tables exceed the 160 KiB LDS", lds_need());
@@ -687,6 +701,11 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   if (!tr) tr = &none;
   const bool bounds = X->cfg.flags & MPCEKF_CF_BOUNDS;
   if (tr->zbk && !bounds) return fail(MPCEKF_E_ARG, "step_ex: a boundzk trajectory needs MPCEKF_CF_BOUNDS");
+  // boundzk in k_cell itself, or from its hand-off record in k_bounds (the lane-quad
+  // k_ekf4 path writes only the record; MB writes boundzk in k_cell)
+  const bool bnd_kernel = bounds && !X->mb && (!cell_computes_bounds() || X->quad);
+  // OB_step's simStep inside k_cell (KRom::cell_plant): no k_plant launch
+  const bool plant_in_cell = X->r.cell_plant && !X->mb && !X->quad;
   const size_t n = (size_t)X->n, per = n * (size_t)nsteps, nzz = (size_t)X->nz + 2;
   // the output fields, their element size and elements per cell-step
   struct F {
@@ -755,13 +774,16 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       hipEvent_t *E = sample ? &X->ev[(size_t)k * NEV] : nullptr;
       if (E) HIPCHK(hipEventRecord(E[0], X->stream));
       if (diag) HIPCHK(hipMemcpyAsync(X->d_uk1p, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
-      if ((rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
+      if (!plant_in_cell &&
+          (rc = lerr(launch_plant(X->r, X->s, X->s.uk, X->s.vk, t, dtc ? dtc + (size_t)k * n : nullptr, X->stream),
                      "plant")))
         return rc;
       if (E) HIPCHK(hipEventRecord(E[1], X->stream));
       KIO io{};
       io.mode = MODE_FUSED;
       io.lazy_t = t;
+      io.plant = plant_in_cell;
+      io.tc_in = plant_in_cell && dtc ? dtc + (size_t)k * n : nullptr;
       io.stamps = X->d_stamps;
       io.u = (double *)row(0, k);
       io.v = (double *)row(1, k);
@@ -772,7 +794,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       io.zk = f[6].dev ? (double *)row(6, k) : X->d_zk;
       double *zbk_k = f[7].dev ? (double *)row(7, k) : X->d_zbk;
       io.zbk = bounds ? zbk_k : nullptr;
-      io.bnd = bounds ? X->d_bnd : nullptr;
+      io.bnd = bnd_kernel ? X->d_bnd : nullptr;
       io.junc_out = (double *)row(8, k);
       io.jfin_out = (double *)row(9, k);
       io.normdu_out = (double *)row(10, k);
@@ -808,6 +830,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         io2.xm_out = nullptr;
         io2.xg_out = nullptr;
         io2.zk_in = io.zk;
+        io2.plant = 0;
+        io2.tc_in = nullptr;
         io2.xm_in = X->d_xm;
         io2.xg_in = X->d_xg;
         if ((rc = lerr(launch_cell(X->r, X->k, X->s, io2, X->stream, P_MPC), "cell"))) return rc;
@@ -832,7 +856,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         flushed[k] = hi > lo;
       }
       // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
-      if (bounds && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
+      if (bnd_kernel && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
       if (E) HIPCHK(hipEventRecord(E[3], X->stream));
       if (X->wide) {
         if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
@@ -884,7 +908,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     for (int k = 0; k < nsteps; ++k)
       for (int j = 0; j < 5; ++j) {
         if ((k + 1) % X->timing_every != 0 && k != nsteps - 1) continue;
-        if ((j == 4 && !flushed[k]) || (j == 2 && !bounds)) continue;
+        if ((j == 4 && !flushed[k]) || (j == 2 && !bnd_kernel) || (j == 0 && plant_in_cell)) continue;
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + e0[j]], X->ev[(size_t)k * NEV + e0[j] + 1]));
         X->t_ms[slot[j]] += ms;
@@ -1061,11 +1085,12 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   io.ik_in = dik;
   io.zk = dzk;
   io.zbk = boundzk ? dzb : nullptr;
-  io.bnd = boundzk ? X->d_bnd : nullptr;
+  const bool bnd_kernel = boundzk && !X->mb && !cell_computes_bounds();
+  io.bnd = bnd_kernel ? X->d_bnd : nullptr;
   io.xm_out = dxm;
   io.xg_out = dxg;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-  if (boundzk && !X->mb && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
+  if (bnd_kernel && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
   HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));

@@ -2163,6 +2163,220 @@ __device__ __forceinline__ void meas_cov_mb(double S[NA6 * NA6], const double L[
 // ---------------------------------------------------------------------------
 // k_cell: iterEKF measurement update + EKFmatsHandler + iterMPC (lane per cell)
 // ---------------------------------------------------------------------------
+// row' * Sigma * row in symmetric form: T = Sigma with doubled off-diagonals,
+// u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, explicit fma at every step
+// (orc qform: 20 operations instead of the 60 of Sigma*row then row'*(.)).
+__device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]) {
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < NX; ++k) {
+    double u = T[pk(k, k)] * rw[k];
+#pragma unroll
+    for (int l = k + 1; l < NX; ++l) u = __builtin_fma(T[pk(k, l)], rw[l], u);
+    q = k == 0 ? rw[0] * u : __builtin_fma(rw[k], u, q);
+  }
+  return q;
+}
+
+// OB_step's simStep (OB_step.m:188-357) for one cell at the start of k_cell's fused step:
+// k_plant's arithmetic, read from the cell blob (the plant's 9 role rows are the blob's
+// first C rows, D at nzp*5, diag(A) after them -- the integrator's a = 1 exactly, checked
+// by build_rom -- and the res0 column after the Sigma coefficients).  Returns Vcell; the
+// plant state, averages, ring inputs and timestamps are stored as k_plant stores them.
+template <int NZ>
+__device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, const double *L, const double *tb,
+                                             const double *Tp, const double *Zp, int64_t c, int lazy_t, double Iapp,
+                                             double tcs, int st) {
+  constexpr int OA = NZ * NX + NZ, OR0 = NZ * NX + NZ + NX + NPK, OD = NZ * NX;
+  const int stride = r.cell_stride;
+  if (lazy_t) {  // this step's inputs, for the deferred updates of every model
+    const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
+    s.hist_u[slot] = Iapp;
+    s.hist_p[slot] = s.priorI[c];
+  }
+  if (st & ST_ERROR) return __builtin_nan("");
+  const double T = tcs + 273.15;  // OB_step.m:75
+  const ETab et = etab(r, tb + r.cell_tab, T);
+  double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
+  const double SOC0n = s.SOC0n[c], SOC0p = s.SOC0p[c];
+  const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
+  double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
+  int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
+  if (r.nZ > 1) {
+    int a, b;
+    two_nearest(Zp, r.nZ, cellSOC, a, b);
+    iZu = a > b ? a : b; iZl = a < b ? a : b;
+  }
+  if (r.nT > 1) {
+    int a, b;
+    two_nearest(Tp, r.nT, T, a, b);
+    iTu = a > b ? a : b; iTl = a < b ? a : b;
+  }
+  const int mm[4] = {iTl * r.nZ + iZl, iTl * r.nZ + iZu, iTu * r.nZ + iZl, iTu * r.nZ + iZu};
+  double *bx = s.bigx + (size_t)c * r.NM * 6;
+  // the 4 corner states as of step t-1: all loads before any store (duplicate corners)
+  double xs[4][6];
+  int tsj[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double2 *p = reinterpret_cast<const double2 *>(bx + (size_t)mm[j] * 6);
+    const double2 q0 = p[0], q1 = p[1], q2 = p[2];
+    xs[j][0] = q0.x; xs[j][1] = q0.y; xs[j][2] = q1.x; xs[j][3] = q1.y; xs[j][4] = q2.x; xs[j][5] = q2.y;
+    if (lazy_t) tsj[j] = s.ts_plant[c * r.NM + mm[j]];
+  }
+  // the per-cell scalar chain while the corner gathers are in flight
+  const double Cdleffn = et.f(0, EF_CDL, SOC0n), Cdleffp = et.f(1, EF_CDL, SOC0p);  // OB_step.m:212-219
+  double dUn = et.f(0, EF_DU, SOCnAvg), dUp = et.f(1, EF_DU, SOCpAvg);
+  double dQn = fabs(r.th100n - r.th0n), dQp = fabs(r.th100p - r.th0p);
+  double res0n = -dQn / (3600 * r.Q - Cdleffn * dQn * dUn);
+  double res0p = dQp / (3600 * r.Q - Cdleffp * dQp * dUp);
+  SOCnAvg = SOCnAvg + res0n * Iapp * r.Ts;
+  SOCpAvg = SOCpAvg + res0p * Iapp * r.Ts;
+  if (SOCnAvg < 0) SOCnAvg = 0;
+  if (SOCnAvg > 1) SOCnAvg = 1;
+  if (SOCpAvg < 0) SOCpAvg = 0;
+  if (SOCpAvg > 1) SOCpAvg = 1;
+  if (lazy_t) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // OB_step.m:198-200 for the skipped steps, RCH inputs per round trip
+      const double *a = L + mm[j] * stride + OA;
+      for (int k0 = tsj[j] + 1; k0 < lazy_t; k0 += RCH) {
+        double u[RCH];
+        ring_chunk(s.hist_u, s, c, k0, lazy_t - 1, u);
+#pragma unroll
+        for (int i = 0; i < RCH; ++i)
+          if (k0 + i < lazy_t) {
+#pragma unroll
+            for (int e = 0; e < NX; ++e) xs[j][e] = __builtin_fma(a[e], xs[j][e], u[i]);
+            xs[j][NX] = __builtin_fma(1.0, xs[j][NX], u[i]);  // the integrator: a = 1
+          }
+      }
+    }
+  }
+  double y[4][NPLANT];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const double *B = L + mm[j] * stride;
+#pragma unroll
+    for (int q = 0; q < NPLANT; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < NX; ++k) acc = acc + B[q * NX + k] * xs[j][k];
+      acc = acc + B[OR0 + q] * xs[j][5];
+      y[j][q] = acc + B[OD + q] * Iapp;
+      launder(y[j][q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const double Zu = Zp[iZu], Zl = Zp[iZl], Tu = Tp[iTu], Tl = Tp[iTl];
+  double aZ = 0.0, aT = 0.0;
+  if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
+  if (Tu != Tl) aT = (T - Tl) / (Tu - Tl);
+  double yk[NPLANT];
+#pragma unroll
+  for (int q = 0; q < NPLANT; ++q)
+    yk[q] = (1 - aT) * ((1 - aZ) * y[0][q] + aZ * y[1][q]) + aT * ((1 - aZ) * y[2][q] + aZ * y[3][q]);
+  double th0 = fmin(fmax(yk[R_TH0] + SOC0n, 1e-6), 1 - 1e-6);
+  double th3 = fmin(fmax(yk[R_TH3] + SOC0p, 1e-6), 1 - 1e-6);
+  double te1 = fmax(yk[R_TE1] + 1, 1e-6);
+  double teE = fmax(yk[R_TEE] + 1, 1e-6);
+  double i0n = et.f(0, EF_K0, negSOC) * sqrt(te1 * (1 - th0) * th0);  // OB_step.m:329-332
+  double i0p = et.f(1, EF_K0, posSOC) * sqrt(teE * (1 - th3) * th3);
+  double negEta0 = 2 * r.R * T / r.F * dasinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * T / r.F * dasinh(yk[R_IF3] / (2 * i0p));
+  double Uocpn0 = et.f(0, EF_U, th0), Uocpp3 = et.f(1, EF_U, th3);
+  const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
+  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
+  V = V - r.Rc * Iapp;
+  s.SOCn[c] = SOCnAvg;
+  s.SOCp[c] = SOCpAvg;
+  if (lazy_t) {  // advance the corners through step t in place
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (tsj[j] >= lazy_t) continue;
+      const double *a = L + mm[j] * stride + OA;
+      double2 *p = reinterpret_cast<double2 *>(bx + (size_t)mm[j] * 6);
+      double x[6];
+#pragma unroll
+      for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], xs[j][e], Iapp);
+      x[NX] = __builtin_fma(1.0, xs[j][NX], Iapp);
+      p[0] = make_double2(x[0], x[1]);
+      p[1] = make_double2(x[2], x[3]);
+      p[2] = make_double2(x[4], x[5]);
+      s.ts_plant[c * r.NM + mm[j]] = lazy_t;
+    }
+  }
+  return V;
+}
+
+// boundzk (iterEKF.m:186-205; getChatZ iterEKF.m:523-602, diagonal only) inside k_cell,
+// lane per cell: for each corner j in order, its getChatV row and the 26 quadratic forms
+// row' * Sigma1 * row with Sigma of the first corner (iterEKF.m:192), summed over the
+// corners as ((((0 + q0) + q1) + q2) + q3) -- k_bounds' quad order, so the bits are
+// k_bounds' -- plus the constant-column term.  It replaces a kernel whose launch, blob
+// staging and record round trip (~22 us at 65,536 cells) cost more than the forms.
+#ifndef MPCEKF_CELL_BOUNDS
+#define MPCEKF_CELL_BOUNDS 1
+#endif
+bool cell_computes_bounds() { return MPCEKF_CELL_BOUNDS != 0; }
+template <int NZ>
+__device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, const XI &xi, const BoundK &b, double S0,
+                                            double *zo) {
+  double S1b[NPK];
+  load_S(cc.erec + (size_t)xi.m[0] * REC, S1b);  // the record k_cell just stored (or caught up)
+#pragma unroll
+  for (int k = 0; k < NX; ++k)
+#pragma unroll
+    for (int l = k + 1; l < NX; ++l) S1b[pk(k, l)] = 2 * S1b[pk(k, l)];
+  const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+  double ChV[4][NX], cph0[4][NX];
+  const double *Cm[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    Cm[j] = cc.L + xi.m[j] * cc.stride;
+    chat_row(r, b.K, Cm[j], xi.g[j], ChV[j]);
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      double v = xi.g[j] * Cm[j][R_PHISE0 * NX + k];
+      if (ph0pp) v = v + ChV[j][k];
+      cph0[j][k] = v;
+    }
+  }
+  // the constant-column term (c0 * S0) * c0 of each kind (C0_*), picked per row
+  const double cv1 = b.C0, cv2 = b.r0n, cv3 = b.r0p, cv4 = b.dUn * b.r0n, cv5 = b.dUp * b.r0p, cv6 = -b.dUn * b.r0n;
+#pragma unroll 1
+  for (int q = 0; q < r.nz; ++q) {  // one form at a time
+    const unsigned f = r.flags[q];
+    double sz = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double g = xi.g[j];
+      double row[NX];
+      if (f & G_PPHIS) {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) row[k] = __builtin_fma(g, Cm[j][q * NX + k], ChV[j][k]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) row[k] = g * Cm[j][q * NX + k];
+      }
+      if (f & G_PHIE)
+#pragma unroll
+        for (int k = 0; k < NX; ++k) row[k] = row[k] - cph0[j][k];
+      sz = sz + qform(S1b, row);
+    }
+    const int kd = r.c0k[q];
+    const double cv = kd == 1 ? cv1 : kd == 2 ? cv2 : kd == 3 ? cv3 : kd == 4 ? cv4 : kd == 5 ? cv5 : kd == 6 ? cv6 : 0.0;
+    zo[r.perm[q]] = 3 * sqrt(sz + (cv * S0) * cv);
+  }
+  double sv = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sv = sv + qform(S1b, ChV[j]);
+  sv = sv + b.C0 * S0 * b.C0;
+  const double rr = -r.Ts / (3600 * r.Q);
+  zo[r.nz] = 3 * sqrt(sv);
+  zo[r.nz + 1] = 3 * sqrt(rr * S0 * rr);
+}
+
 template <int NZ, int PARTS, bool MB = false, bool GR = false>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
@@ -2182,7 +2396,9 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   cc.Zp = Zp;
   cc.erec = s.ekf + (size_t)c * r.NM * REC;
   cc.stride = r.cell_stride;
-  const double Tc = s.Tc[c];
+  const bool fplant = (PARTS & P_EKF) && !MB && io.plant;  // OB_step's simStep runs here (KRom::cell_plant)
+  const double Tc = fplant && io.tc_in ? io.tc_in[c] : s.Tc[c];
+  if (fplant && io.tc_in) s.Tc[c] = Tc;  // this step's TC (runMPC.m:85-92), read by every later kernel
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
   cc.et = etab(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
@@ -2220,13 +2436,21 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   double vhat = 0.0, Zsoc = 0.0;
   XI xi;
   double ik = 0.0, vk = 0.0;
+  double vplant = 0.0;
+  if constexpr ((PARTS & P_EKF) && !MB) {
+    if (fplant) {  // runMPC.m:85: [voltage, ...] = OB_step(uk, TC, cellState, ROM)
+      if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
+      vplant = cell_plant<NZ>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
+      s.vk[c] = vplant;
+    }
+  }
   if ((PARTS & P_EKF) && (io.mode & (MODE_EKF | MODE_FUSED))) {
     if (st & ST_ERROR) {
       fail_outputs();
       return;
     }
     ik = fused ? s.uk[c] : io.ik_in[c];
-    vk = fused ? s.vk[c] : io.vk_in[c];
+    vk = fused ? (fplant ? vplant : s.vk[c]) : io.vk_in[c];
     int warn = s.warn[c];
     if (warn > cf.max_warn) {  // iterEKF.m:55-59
       st |= ST_LOCKOUT | ST_ERROR;
@@ -2541,6 +2765,9 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { io.xm_out[c * 4 + j] = xi.m[j]; io.xg_out[c * 4 + j] = xi.g[j]; }
     }
+    if (MPCEKF_CELL_BOUNDS && io.zbk && !io.bnd)
+      cell_bounds<NZ>(r, cc, xi, bound_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3]),
+                      S0, io.zbk + c * (nz + 2));
     }  // OB
   }
   if (!(PARTS & (P_MPC | P_LIN))) return;
@@ -2865,21 +3092,6 @@ __device__ __forceinline__ double quad_sum_seq(double v) {  // (((0 + v0) + v1) 
 constexpr int BOUNDS_BLOCK = 1024;
 // k_bounds stages only the models of the cell blob (its getChatV scalars come from k_cell)
 __host__ __device__ inline int bounds_c0_base(const KRom &r) { return r.rom_global ? 0 : r.cell_tab + 1; }
-// row' * Sigma * row in symmetric form: T = Sigma with doubled off-diagonals,
-// u_k = T_kk r_k + sum_{l>k} T_kl r_l, q = sum_k r_k u_k, explicit fma at every step
-// (orc qform: 20 operations instead of the 60 of Sigma*row then row'*(.)).
-__device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]) {
-  double q = 0.0;
-#pragma unroll
-  for (int k = 0; k < NX; ++k) {
-    double u = T[pk(k, k)] * rw[k];
-#pragma unroll
-    for (int l = k + 1; l < NX; ++l) u = __builtin_fma(T[pk(k, l)], rw[l], u);
-    q = k == 0 ? rw[0] * u : __builtin_fma(rw[k], u, q);
-  }
-  return q;
-}
-
 template <int NZ, bool GR>
 __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KState s, const double *bd, double *zbk) {
   extern __shared__ double lds[];

@@ -54,6 +54,10 @@ struct KRom {
   // 1: the model rows of both blobs do not fit the 160 KiB LDS (large NM); the kernels
   // stage only the tables (from *_tab, even offsets) and read the model rows from HBM/L2
   int rom_global;
+  // 1: the cell blob also carries the plant's res0 column per model (after the Sigma
+  // coefficients) and the Cdleff tables, and the fused step runs OB_step's simStep at the
+  // start of k_cell (no k_plant launch)
+  int cell_plant;
 };
 
 struct KCfg {
@@ -109,6 +113,10 @@ struct KIO {
   double *x_out;          // [n][6] x_store: the EKFmatsHandler xhat
   double *junc_out, *jfin_out, *normdu_out;  // [n] J_uncon, J_final, norm_DU
   int *nviol_out;         // [n] viol
+  // fused step with KRom::cell_plant: OB_step's simStep runs first in k_cell (no k_plant);
+  // tc_in (device [n] degC, may be null) is the step's TC, stored into s.Tc
+  int plant;
+  const double *tc_in;
 };
 constexpr int NSTAMPS = 20;  // k_cell sections 0..11, k_plant 12..19
 // k_cell -> k_bounds record: g[4], m[4], getChatZ's getChatV scalars at the updated state
@@ -171,6 +179,7 @@ int launch_hildreth_structured(int64_t n, const double *E, const double *F, cons
                                double *DU, int *nexec, void *stream);
 int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream);
 bool cell_kernel_supported(int nzp);
+bool cell_computes_bounds();  // k_cell evaluates boundzk itself (no k_bounds launch, no hand-off record)
 
 // wide-horizon MPC stage (mpcekf_wide.hip)
 bool wide_supported(int Np, int Nc);

@@ -2,7 +2,7 @@
 # Round-4 GPU pass on the current build: the GPU suite, the default bench line (CPU leg
 # included), a same-box A/B against variant libraries, k_cell / k_plant section stamps,
 # and the rocprofv3 kernel trace + PMC traffic of the default bench command.
-#   gpurun --timeout 1100 -- 'bash tools/gpu_r04_pass.sh TAG [variant.so ...]'
+#   gpurun --timeout 1100 -- 'ENV_AB="VAR=value" bash tools/gpu_r04_pass.sh TAG [variant.so ...]'
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,6 +13,11 @@ timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 if [ $# -gt 0 ]; then
   bash tools/ab_libs.sh $TAG/ab "" mpc-ekf4fastcharge_amd/_build/libmpcekf.so "$@" > $O/ab.txt 2>&1 || exit 1
+fi
+if [ -n "$ENV_AB" ]; then  # the product library under an environment override, twice
+  for rep in 1 2; do
+    env $ENV_AB timeout -k 10 300 python bench.py --no-cpu > $O/env_ab_$rep.json 2> $O/env_ab_$rep.err || exit 1
+  done
 fi
 if [ -f mpc-ekf4fastcharge_amd/_build/libmpcekf_stamps.so ]; then
   for N in 65536 1024; do
