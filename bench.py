@@ -39,7 +39,8 @@ METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 LAZY_H = 64  # the library's input-ring length = flush period (mpcekf_kernels.hpp MPCEKF_LAZY_H)
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, bounds_kernel=False, plant_kernel=False):
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, bounds_kernel=False, plant_kernel=False,
+                               hild_kernel=True):
     """Algorithmic HBM bytes each kernel moves per cell per launch:
     the state it must read and write once, with nothing re-read.
 
@@ -72,6 +73,9 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, boun
     if not plant_kernel:  # k_cell runs OB_step's simStep first (KRom::cell_plant): its bytes are k_cell's
         out["cell"] = cell = cell + plant
         del out["plant"]
+    if not hild_kernel:  # hildreth.m at the end of k_cell (Np = 5 fused step): its bytes are k_cell's
+        out["cell"] = cell = cell + hild
+        del out["hild"]
     if bounds and bounds_kernel:
         out["bounds"] = 14 * 8 + 15 * 8 + 4 * 8 + 28 * 8
     elif bounds:  # k_cell evaluates boundzk: no hand-off record; corner 1's Sigma read, boundzk written
@@ -380,7 +384,8 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
     # boundzk is evaluated inside k_cell unless a k_bounds launch was timed
     bpc = algorithmic_bytes_per_cell(rom.NM, ncon, bool(args.bounds), Np=args.np, Nc=args.nc,
                                      bounds_kernel=tim.get("bounds", (0.0, 0))[1] > 0,
-                                     plant_kernel=tim.get("plant", (0.0, 0))[1] > 0)
+                                     plant_kernel=tim.get("plant", (0.0, 0))[1] > 0,
+                                     hild_kernel=tim.get("hild", (0.0, 0))[1] > 0)
     # HIP-event averages over the sampled launches (--timing-every), so a kernel's share of
     # a step is its average x its launches per step.  k_flush flushes every cell each period
     # steps (the library default; every flush step is sampled); the rolling schedule

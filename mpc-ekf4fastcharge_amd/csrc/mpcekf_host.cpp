@@ -706,6 +706,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   const bool bnd_kernel = bounds && !X->mb && (!cell_computes_bounds() || X->quad);
   // OB_step's simStep inside k_cell (KRom::cell_plant): no k_plant launch
   const bool plant_in_cell = X->r.cell_plant && !X->mb && !X->quad;
+  // hildreth.m at the end of k_cell (Np = 5, one k_cell per step): no k_hild launch
+  const bool hild_in_cell = cell_runs_hild() && !X->wide && !X->split_cell && !X->quad;
   const size_t n = (size_t)X->n, per = n * (size_t)nsteps, nzz = (size_t)X->nz + 2;
   // the output fields, their element size and elements per cell-step
   struct F {
@@ -784,6 +786,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       io.lazy_t = t;
       io.plant = plant_in_cell;
       io.tc_in = plant_in_cell && dtc ? dtc + (size_t)k * n : nullptr;
+      io.hild = hild_in_cell;
       io.stamps = X->d_stamps;
       io.u = (double *)row(0, k);
       io.v = (double *)row(1, k);
@@ -860,7 +863,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
       if (E) HIPCHK(hipEventRecord(E[3], X->stream));
       if (X->wide) {
         if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
-      } else if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
+      } else if (!hild_in_cell && (rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
         return rc;
       }
       if (diag) {
@@ -908,7 +911,9 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
     for (int k = 0; k < nsteps; ++k)
       for (int j = 0; j < 5; ++j) {
         if ((k + 1) % X->timing_every != 0 && k != nsteps - 1) continue;
-        if ((j == 4 && !flushed[k]) || (j == 2 && !bnd_kernel) || (j == 0 && plant_in_cell)) continue;
+        if ((j == 4 && !flushed[k]) || (j == 2 && !bnd_kernel) || (j == 0 && plant_in_cell) ||
+            (j == 3 && hild_in_cell && !diag))
+          continue;
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + e0[j]], X->ev[(size_t)k * NEV + e0[j] + 1]));
         X->t_ms[slot[j]] += ms;

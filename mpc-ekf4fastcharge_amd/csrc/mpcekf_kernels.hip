@@ -53,6 +53,9 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_FLUSH_COAL  // k_flush_coal (coalesced chunks, NM <= 64): measured slower, off
 #define MPCEKF_FLUSH_COAL 0
 #endif
+#ifndef MPCEKF_HILD_INLINE_SLOW  // k_hild finishes its slow lanes itself (no k_hild_slow launch)
+#define MPCEKF_HILD_INLINE_SLOW 1
+#endif
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
 #endif
@@ -2377,6 +2380,12 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
   zo[r.nz + 1] = 3 * sqrt(rr * S0 * rr);
 }
 
+#ifndef MPCEKF_CELL_HILD  // k_cell also runs hildreth.m (the fused step's k_hild) after a block barrier
+#define MPCEKF_CELL_HILD 1
+#endif
+// (with its slow lanes finished in the same kernel: MPCEKF_HILD_INLINE_SLOW)
+bool cell_runs_hild() { return MPCEKF_CELL_HILD != 0 && MPCEKF_HILD_INLINE_SLOW != 0; }
+__device__ __forceinline__ void hild_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c);
 template <int NZ, int PARTS, bool MB = false, bool GR = false>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
@@ -2387,6 +2396,9 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   const double *Tp = tb + r.cell_tab + r.cell_tablen;
   const double *Zp = Tp + MAXT;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the per-cell work as a lambda: its early exits return here, so every lane of the block
+  // reaches the barrier of the fused Hildreth below
+  auto body = [&]() {
   if (c >= s.n) return;
   const int nz = r.nz;
   const double NaN = __builtin_nan("");
@@ -2874,6 +2886,14 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
   }
 #endif
+  };
+  body();
+  if constexpr (MPCEKF_CELL_HILD && (PARTS & P_MPC) != 0) {
+    if (io.hild) {  // hildreth.m in the same kernel (no k_hild launch): the blob's LDS becomes the
+      __syncthreads();  // per-lane Hildreth slots once every wave of the block is done with it
+      if (c < s.n) hild_cell(cf, s, io, c);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -3285,19 +3305,15 @@ __device__ __forceinline__ void hild_finish(const KState &s, const KIO &io, int6
   }
 }
 
-#ifndef MPCEKF_HILD_INLINE_SLOW  // k_hild finishes its slow lanes itself (no k_hild_slow launch)
-#define MPCEKF_HILD_INLINE_SLOW 1
-#endif
 __device__ __forceinline__ void hild_slow_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c);
 // out of line: the exact-rule path keeps its registers out of the fast sweep's allocation
 __device__ __noinline__ void hild_slow_wave(const KCfg &cf, const KState &s, const KIO &io, int64_t c) {
   hild_slow_cell(cf, s, io, c);
 }
 
-// hildreth.m + iterMPC.m:68-95, lane per cell: the fast solve (hild_fast).
-__global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= s.n) return;
+// hildreth.m + iterMPC.m:68-95, lane per cell: the fast solve (hild_fast).  Blocks of 256
+// lanes (hild_lane_lds); k_hild, or the end of k_cell in the fused step.
+__device__ __forceinline__ void hild_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c) {
   // every lane of the wave stays in the solve; cells without a QP this step ride
   // along on a finite dummy problem and store nothing
   const bool qp = s.hflag[c] != 0;
@@ -3337,6 +3353,11 @@ __global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, con
 #pragma unroll
   for (int i = 0; i < NCON; ++i) s.lam[(size_t)i * n + c] = lam[i];  // iterMPC.m:68
   hild_finish(s, io, c, Cn, Mtl, nexec);
+}
+__global__ void __launch_bounds__(256) k_hild(const KCfg cf, const KState s, const KIO io) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.n) return;
+  hild_cell(cf, s, io, c);
 }
 
 // The exact-rule solve of the cells k_hild flagged (hflag 2): one wave per block over a
@@ -3783,6 +3804,7 @@ template <int NZ, int PARTS, bool MB, bool GR>
 static void launch_cell_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   int lds = cell_lds_bytes(r);
+  if (io.hild) lds = lds > (int)(4 * HILD_LDS_PER_WAVE) ? lds : (int)(4 * HILD_LDS_PER_WAVE);  // the Hildreth slots
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);

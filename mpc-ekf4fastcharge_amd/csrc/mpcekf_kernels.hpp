@@ -117,6 +117,7 @@ struct KIO {
   // tc_in (device [n] degC, may be null) is the step's TC, stored into s.Tc
   int plant;
   const double *tc_in;
+  int hild;  // fused step, Np = 5: hildreth.m at the end of k_cell (no k_hild launch)
 };
 constexpr int NSTAMPS = 20;  // k_cell sections 0..11, k_plant 12..19
 // k_cell -> k_bounds record: g[4], m[4], getChatZ's getChatV scalars at the updated state
@@ -180,6 +181,7 @@ int launch_hildreth_structured(int64_t n, const double *E, const double *F, cons
 int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double *sx0, void *stream);
 bool cell_kernel_supported(int nzp);
 bool cell_computes_bounds();  // k_cell evaluates boundzk itself (no k_bounds launch, no hand-off record)
+bool cell_runs_hild();        // the fused step's k_cell also runs hildreth.m when KIO::hild is set
 
 // wide-horizon MPC stage (mpcekf_wide.hip)
 bool wide_supported(int Np, int Nc);
