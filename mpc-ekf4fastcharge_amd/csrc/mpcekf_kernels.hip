@@ -53,8 +53,11 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_FLUSH_COAL  // k_flush_coal (coalesced chunks, NM <= 64): measured slower, off
 #define MPCEKF_FLUSH_COAL 0
 #endif
-#ifndef MPCEKF_HILD_INLINE_SLOW  // k_hild finishes its slow lanes itself (no k_hild_slow launch)
-#define MPCEKF_HILD_INLINE_SLOW 1
+// k_hild finishes its slow lanes itself (no k_hild_slow launch).  Off: the exact-rule
+// path's registers moved the fast sweep's allocation (AGPRs 34 -> 242) and k_hild took
+// 89.5 instead of ~75 us, more than the ~5 us a k_hild_slow launch costs (r04g A/B)
+#ifndef MPCEKF_HILD_INLINE_SLOW
+#define MPCEKF_HILD_INLINE_SLOW 0
 #endif
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
@@ -2316,10 +2319,11 @@ __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, con
 // lane per cell: for each corner j in order, its getChatV row and the 26 quadratic forms
 // row' * Sigma1 * row with Sigma of the first corner (iterEKF.m:192), summed over the
 // corners as ((((0 + q0) + q1) + q2) + q3) -- k_bounds' quad order, so the bits are
-// k_bounds' -- plus the constant-column term.  It replaces a kernel whose launch, blob
-// staging and record round trip (~22 us at 65,536 cells) cost more than the forms.
+// k_bounds'.  Off by default: on k_cell's one-wave-per-SIMD chain the forms took as long
+// as the lane-quad k_bounds at 4 waves per SIMD (r04g A/B: 2.48e8 vs 2.50e8), which also
+// saved nothing by skipping the hand-off record.
 #ifndef MPCEKF_CELL_BOUNDS
-#define MPCEKF_CELL_BOUNDS 1
+#define MPCEKF_CELL_BOUNDS 0
 #endif
 bool cell_computes_bounds() { return MPCEKF_CELL_BOUNDS != 0; }
 template <int NZ>
@@ -2380,8 +2384,11 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
   zo[r.nz + 1] = 3 * sqrt(rr * S0 * rr);
 }
 
-#ifndef MPCEKF_CELL_HILD  // k_cell also runs hildreth.m (the fused step's k_hild) after a block barrier
-#define MPCEKF_CELL_HILD 1
+// k_cell also runs hildreth.m (the fused step's k_hild) after a block barrier.  Off by
+// default: it needs the in-kernel slow path (MPCEKF_HILD_INLINE_SLOW), and k_cell + Hildreth
+// as one kernel measured 255.7 us against 161 + 89.5 as two (r04g A/B)
+#ifndef MPCEKF_CELL_HILD
+#define MPCEKF_CELL_HILD 0
 #endif
 // (with its slow lanes finished in the same kernel: MPCEKF_HILD_INLINE_SLOW)
 bool cell_runs_hild() { return MPCEKF_CELL_HILD != 0 && MPCEKF_HILD_INLINE_SLOW != 0; }

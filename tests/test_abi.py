@@ -101,3 +101,26 @@ def test_mex_gateway_calls_only_declared_entry_points():
     cmds = set(re.findall(r"mpcekf_mex\('([a-z_]+)'", drop))
     for c in cmds:
         assert f'"{c}"' in src, c
+
+
+def test_temperature_argument_rule_is_shared(P):
+    """Context.step's tc and oracle_c.run's tc_traj read a temperature argument by one rule
+    (ADVICE r03): scalar, a 1-D per-step profile [nsteps], a 1-D per-cell vector [ncells],
+    [nsteps, 1], [1, ncells] or the full grid; a 1-D vector of length nsteps == ncells is
+    refused as ambiguous instead of being read as per-cell."""
+    import numpy as np
+    import pytest
+    from importlib import import_module
+    import oracle_c
+    m = import_module("mpc-ekf4fastcharge_amd.mpcekf")
+    for f in (m.tc_grid, oracle_c._tc_grid):
+        prof = np.arange(5.0)
+        np.testing.assert_array_equal(f(prof, 5, 3), np.repeat(prof[:, None], 3, axis=1))   # per step
+        cells = np.array([20.0, 21.0, 22.0])
+        np.testing.assert_array_equal(f(cells, 5, 3), np.repeat(cells[None, :], 5, axis=0))  # per cell
+        np.testing.assert_array_equal(f(25.0, 2, 3), np.full((2, 3), 25.0))
+        np.testing.assert_array_equal(f(prof[:, None], 5, 3), np.repeat(prof[:, None], 3, axis=1))
+        with pytest.raises(ValueError, match="ambiguous"):
+            f(np.arange(4.0), 4, 4)
+        with pytest.raises(ValueError):
+            f(np.arange(7.0), 5, 3)

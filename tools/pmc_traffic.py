@@ -16,7 +16,7 @@ from collections import defaultdict
 
 # kernel (exact name prefix) -> bench stage; a stage's per-step figure is the sum of
 # its kernels' per-dispatch averages (each launches once per step)
-KERNELS = {"k_plant(": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild_slow(": "hild",
+KERNELS = {"k_plant(": "plant", "k_plant4<": "plant", "k_flush(": "flush", "k_cell<": "cell", "k_hild(": "hild", "k_hild_slow(": "hild",
            "k_bounds<": "bounds", "k_bulk(": "bulk",
            # wide horizons (mpcekf_wide.hip): bench.py's "cell" slot times k_cell + k_mpc_wide,
            # its "hild" slot the whole hildreth.m pipeline (prep, binning, sweeps, exact path, finish)
