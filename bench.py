@@ -64,11 +64,12 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, boun
     hild = 51 * 8 + 2 * 8 * ncon + 4 * 8
     if (Np, Nc) != (5, 2):
         # wide horizons (mpcekf_wide.hip): k_cell hands over the 35-double linearisation
-        # record + zk(end); the QP record E, F, Hv, He, Hs, gamma, e, Ru, uk_1 and the
-        # hildreth.m setup X (ncon x Nc), K, H_ii are written by k_mpc_wide and read back
+        # record + zk(end); the QP record E, F, Hv, He, Hs, gamma, e, Ru, uk_1 is written by
+        # k_mpc_wide and read back; k_hild_prep hands k_hild_wide chol(E) (Nc(Nc+1)/2) and K
+        # (ncon), and k_hild_wide forms X and H_ii itself (MPCEKF_WIDE_XPRO, the default)
         prob = Nc * Nc + Nc + 4 * Np + ncon + 2
         cell = cell - 51 * 8 + 36 * 8
-        hild = 2 * 8 * (36 + prob + ncon * (Nc + 2)) + 2 * 8 * ncon + 4 * 8
+        hild = 2 * 8 * (36 + prob + Nc * (Nc + 1) // 2 + ncon) + 2 * 8 * ncon + 4 * 8
     out = dict(flush=flush, cell=cell, plant=plant, hild=hild)
     if not plant_kernel:  # k_cell runs OB_step's simStep first (KRom::cell_plant): its bytes are k_cell's
         out["cell"] = cell = cell + plant

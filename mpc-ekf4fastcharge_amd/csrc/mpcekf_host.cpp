@@ -552,7 +552,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
     w.Np = cfg->Np; w.Nc = cfg->Nc; w.ncon = X->ncon;
     const size_t nc = (size_t)X->ncon;
     if ((rc = dalloc(&w.prob, n * wide_prob_doubles(w.Np, w.Nc))) || (rc = dalloc(&w.X, nc * n * w.Nc)) ||
-        (rc = dalloc(&w.K, nc * n)) || (rc = dalloc(&w.hii, nc * n)) || (rc = dalloc(&w.it, n)) ||
+        (rc = dalloc(&w.R, (size_t)n * (w.Nc * (w.Nc + 1) / 2))) || (rc = dalloc(&w.K, nc * n)) || (rc = dalloc(&w.hii, nc * n)) || (rc = dalloc(&w.it, n)) ||
         (rc = dalloc(&w.smin, (size_t)w.Nc * w.Nc + 1)) || (rc = dalloc(&X->d_lin, n * MPCEKF_LIN_SIZE)) ||
         (rc = dalloc(&w.q, 1)) || (rc = dalloc(&w.list, n)) || (rc = dalloc(&w.hist, 128)) ||
         (rc = dalloc(&X->d_zsoc, n))) {
@@ -581,7 +581,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (X->ev_join) (void)hipEventDestroy(X->ev_join);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
-                  X->w.prob, X->w.X, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
+                  X->w.prob, X->w.X, X->w.R, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
                   X->w.q, X->w.list, X->w.hist};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);

@@ -2384,6 +2384,11 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
   zo[r.nz + 1] = 3 * sqrt(rr * S0 * rr);
 }
 
+// 1: k_cell's simStep after the EKF's first record reads are issued, so the plant's chain
+// overlaps their round trip; measured slower (r04i same-box A/B: k_cell 143 vs 134 us)
+#ifndef MPCEKF_CELL_PLANT_LATE
+#define MPCEKF_CELL_PLANT_LATE 0
+#endif
 // k_cell also runs hildreth.m (the fused step's k_hild) after a block barrier.  Off by
 // default: it needs the in-kernel slow path (MPCEKF_HILD_INLINE_SLOW), and k_cell + Hildreth
 // as one kernel measured 255.7 us against 161 + 89.5 as two (r04g A/B)
@@ -2456,22 +2461,32 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   XI xi;
   double ik = 0.0, vk = 0.0;
   double vplant = 0.0;
-  if constexpr ((PARTS & P_EKF) && !MB) {
-    if (fplant) {  // runMPC.m:85: [voltage, ...] = OB_step(uk, TC, cellState, ROM)
-      if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
-      vplant = cell_plant<NZ>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
-      s.vk[c] = vplant;
+  bool planted = false;
+  // runMPC.m:85: [voltage, ...] = OB_step(uk, TC, cellState, ROM), first (with
+  // MPCEKF_CELL_PLANT_LATE once the EKF's first record reads are issued; every path below
+  // runs it before it returns)
+  auto run_plant = [&]() {
+    if constexpr ((PARTS & P_EKF) && !MB) {
+      if (fplant && !planted) {
+        if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
+        vplant = cell_plant<NZ>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
+        s.vk[c] = vplant;
+        planted = true;
+      }
     }
-  }
+  };
+  if (!MPCEKF_CELL_PLANT_LATE) run_plant();
   if ((PARTS & P_EKF) && (io.mode & (MODE_EKF | MODE_FUSED))) {
     if (st & ST_ERROR) {
+      run_plant();
       fail_outputs();
       return;
     }
     ik = fused ? s.uk[c] : io.ik_in[c];
-    vk = fused ? (fplant ? vplant : s.vk[c]) : io.vk_in[c];
+    vk = fused ? s.vk[c] : io.vk_in[c];  // the plant's Vcell replaces it once the plant has run
     int warn = s.warn[c];
     if (warn > cf.max_warn) {  // iterEKF.m:55-59
+      run_plant();
       st |= ST_LOCKOUT | ST_ERROR;
       s.status[c] = st;
       if (fused) s.uk[c] = NaN;
@@ -2479,6 +2494,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       return;
     }
     if constexpr (MB) {
+    run_plant();
     // iterEKF.m:90-102 ('MB' time update), 106-108, 125-128 (gain), 160-176 (update),
     // 181-183, 199-203 (boundzk); the per-model records are never touched
     const double rs = r.Ts / (3600 * r.Q);
@@ -2641,7 +2657,11 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       else load_x(cc.erec + (size_t)xi.m[j] * REC, xr[j]);
       tsj[j] = t ? s.ts_ekf[c * r.NM + xi.m[j]] : 0;
     }
-    const double pt = t ? s.hist_p[(size_t)(t % LAZY_H) * s.n + c] : 0.0;
+    // step t's ring input: the plant stores this cell's priorI there (k_plant, or cell_plant
+    // below, which may not have run yet)
+    const double pt = t ? (fplant ? s.priorI[c] : s.hist_p[(size_t)(t % LAZY_H) * s.n + c]) : 0.0;
+    run_plant();  // the records above are in flight while the plant's chain runs
+    if (planted) vk = vplant;
     if (t) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)

@@ -137,7 +137,8 @@ enum { P_EKF = 1, P_MPC = 2, P_ALL = 3, P_LIN = 4 };  // P_EKF | P_LIN: iterEKF 
 struct KWide {
   int Np, Nc, ncon;
   double *prob;    // [wide_prob_doubles][n]: E, F, Hv, He, Hs, gamma, e, Ru, uk_1
-  double *X;       // [ncon][n][Nc]  X(:,i) = E\M(i,:)'
+  double *X;       // [ncon][n][Nc]  X(:,i) = E\M(i,:)' (the exact path's; k_hild_wide forms its own)
+  double *R;       // [Nc(Nc+1)/2][n] chol(E) upper triangle by rows (k_hild_prep -> k_hild_wide)
   double *K, *hii; // [ncon][n]
   int *it;         // [n] hildreth.m sweeps (nexec)
   int *q;          // [1] fast-path cells this step (k_hild_sort)

@@ -7,10 +7,12 @@
 //                                     unconstrained LS solve, constraintsMPC.m and the
 //                                     violation test, streamed row by row (no M or
 //                                     gamma arrays live); finishes cells that need no QP
-//   k_hild_prep       lane per cell   hildreth.m:17-29: R = chol(E), X(:,i) = E\M(i,:)'
-//                                     for the 80 distinct rows, K = M*(E\F) + gamma, H_ii
-//   k_hild_wide       8-lane group    hildreth.m:32-42 sweeps: lane k holds v_k (and v_k+8) and
-//                     per cell        column k of X in registers; row values are summed
+//   k_hild_prep       lane per cell   hildreth.m:17-29: R = chol(E) (handed over), K =
+//                                     M*(E\F) + gamma (MPCEKF_WIDE_XPRO=0: also X(:,i) =
+//                                     E\M(i,:)' for the 80 distinct rows and H_ii)
+//   k_hild_wide       8-lane group    X and H_ii from R in its prologue (XPRO), then the
+//                     per cell        hildreth.m:32-42 sweeps: lane k holds v_k (and v_k+8)
+//                                     and column k of X in registers; row values are summed
 //                                     by a DPP butterfly (oracle hild_row_t)
 //   k_hild_wide_slow  lane per cell   the exact rules (inf/NaN rows, non-finite X or M,
 //                                     non-SPD E, divisions outside the fast form's
@@ -32,6 +34,12 @@
 #endif
 #ifndef MPCEKF_WIDE_SORT
 #define MPCEKF_WIDE_SORT 1
+#endif
+// 1: k_hild_wide forms X(:,i) = E\M(i,:)' and H_ii itself from chol(E) (k_hild_prep hands
+// over R, 55 doubles per cell, instead of writing X, 800, to HBM for k_hild_wide to read
+// back); 0: k_hild_prep writes X and H_ii
+#ifndef MPCEKF_WIDE_XPRO
+#define MPCEKF_WIDE_XPRO 1
 #endif
 #include <cmath>
 #include <cstdint>
@@ -359,7 +367,7 @@ __device__ __forceinline__ void prep_row(const KWide &w, const double *pb, int64
     fin = fin && isfinite(b[k]);
   }
   if (act) w.K[(size_t)c * NCON + i] = kk + gam;
-  if (neg) return;  // H_ii of -b equals that of b (stored with the b row)
+  if (neg || MPCEKF_WIDE_XPRO) return;  // H_ii of -b equals that of b (stored with the b row)
   double x[NC];
   chol_apply<NC>(R, b, x);
   double h = 0.0;
@@ -392,7 +400,8 @@ __device__ __forceinline__ void prep_row(const KWide &w, const double *pb, int64
 // k_hild_prep: hildreth.m:28-29 for the cells that run it (hflag == 1)
 // ---------------------------------------------------------------------------
 // hflag after: 1 = k_hild_wide, 2 = exact path with X/K/H_ii ready, 3 = exact path
-// that must build them (E not SPD: MATLAB's \ falls back to LU).
+// that must build them (E not SPD: MATLAB's \ falls back to LU), 4 (XPRO) = exact path
+// that builds X/H_ii from the stored R (K ready).
 template <int NP, int NC>
 __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w) {
   using T = W<NP, NC>;
@@ -409,6 +418,13 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
   if (!chol_n<NC>(E, R) && act) {
     s.hflag[c] = 3;
     act = false;
+  }
+  if (MPCEKF_WIDE_XPRO && act) {
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < NC; ++a)
+#pragma unroll
+      for (int b = a; b < NC; ++b) w.R[(size_t)(e++) * n + c] = R[a][b];
   }
 #pragma unroll
   for (int a = 0; a < NC; ++a) F[a] = pb[(T::F + a) * n + cr];
@@ -452,7 +468,9 @@ __global__ void __launch_bounds__(64) k_hild_prep(const KState s, const KWide w)
       prep_row<NP, NC>(w, pb, n, cr, i, false, i - 2 * NC, false, R, y, b, gi, fin, xt, act);
     }
   }
-  if (act && !fin) s.hflag[c] = 2;
+  // a non-finite M entry (XPRO: X is checked by k_hild_wide): the exact path, which with
+  // XPRO builds X and H_ii from R first (hflag 4)
+  if (act && !fin) s.hflag[c] = MPCEKF_WIDE_XPRO ? 4 : 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -675,9 +693,76 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
                     2 * (T::ZERO_LDS + T::GROUPS * T::CELL_LDS + T::WAVES * T::JUNK) * 8 <= 160 * 1024,
                 "two blocks per CU");
   for (int i = threadIdx.x; i < NCON; i += blockDim.x) zero[i] = 0.0;
+  if (MPCEKF_WIDE_XPRO && (int64_t)blockIdx.x * T::GROUPS >= w.q[0]) return;  // block-uniform: nothing listed
   const bool act = slot < w.q[0];            // k_hild_sort's count
   const int64_t c = act ? w.list[slot] : 0;  // cells in k_hild_bin<true>'s order
   bool ok = true;
+  static_assert(NC <= LN + 2 && T::NX_ROWS % LN == 0, "columns >= 8 spread as pairs over 4 lane pairs");
+  double X0[T::NX_ROWS], X1[T::NX_ROWS / 4];
+#if MPCEKF_WIDE_XPRO
+  // hildreth.m:28's X(:,i) = E\M(i,:)' and H_ii = M(i,:)*X(:,i) for the group's cell, from
+  // k_hild_prep's R = chol(E): lane k solves the distinct rows u = 8j + k (chol_apply, the
+  // arithmetic k_hild_prep would use), and the group transposes each chunk of 8 solutions
+  // through LDS so that lane k keeps columns k (and k + 8 spread over the lane pairs) of
+  // every row.  X never goes through HBM.  Inactive groups of the block run it on cell 0's
+  // data (results unused) so that every lane reaches the barriers.
+  for (int j = k; j < 3 * HPW; j += LN) {
+    const int b = j / HPW, q = j % HPW;
+    hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
+  }
+  double R[NC][NC];
+  {
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < NC; ++a)
+#pragma unroll
+      for (int b = a; b < NC; ++b) R[a][b] = w.R[(size_t)(e++) * n + c];
+  }
+  __syncthreads();                 // hp
+  double *xb = lam;                // a chunk's 8 solutions [8][NC]; lam / K are filled after
+#pragma unroll
+  for (int j = 0; j < T::NX_ROWS / LN; ++j) {
+    const int u = LN * j + k;
+    // M(i,:) of the distinct row u, as mrow_vec / k_hild_prep build it: the Cu rows, the I
+    // rows, then the Toeplitz blocks (+-H(r - m), +-0 beyond r)
+    const int tu = u >= 2 * NC ? u - 2 * NC : 0, blk = tu / NP, r = tu % NP;
+    double b[NC], x[NC];
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      const double hv = hp[blk * HPW + (NC - 1) + r - m];
+      b[m] = u < NC ? (m <= u ? 1.0 : 0.0) : u < 2 * NC ? (u - NC == m ? 1.0 : 0.0) : (blk == 1 ? -hv : hv);
+    }
+    chol_apply<NC>(R, b, x);
+    double h = 0.0;
+#pragma unroll
+    for (int m = 0; m < NC; ++m) {
+      h = h + b[m] * x[m];
+      ok = ok && isfinite(x[m]);
+      xb[k * NC + m] = x[m];
+    }
+    const int i = u < NC ? u : u < 2 * NC ? u + NC : u + 2 * NC;  // constraint row (+ NC: its negated copy)
+    const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && h == 0.0;  // (H(0), 0, ..) rows
+    const double ay = fabs(h);
+    ok = ok && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
+    const double2 hh = make_double2(h, zrow ? __builtin_amdgcn_rcp(h) : rcp_refined_w(h));
+    hr[i] = hh;
+    if (u < 2 * NC) hr[i + NC] = hh;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < LN; ++q) X0[LN * j + q] = xb[q * NC + k];
+    X1[2 * j] = xb[(k >> 1) * NC + LN + (k & 1)];
+    X1[2 * j + 1] = xb[(4 + (k >> 1)) * NC + LN + (k & 1)];
+    __syncthreads();
+  }
+  if (act) {
+    for (int i = k; i < NCON; i += LN) {
+      const double li = s.lam[(size_t)i * n + c];
+      ok = ok && isfinite(li);
+      lam[i] = li;
+      Kl[i] = w.K[(size_t)c * NCON + i];
+    }
+  }
+#else
   if (act) {
     for (int i = k; i < NCON; i += LN) {
       const double li = s.lam[(size_t)i * n + c];
@@ -694,11 +779,13 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       hp[j] = q < NC - 1 ? 0.0 : w.prob[(T::HV + b * NP + q - (NC - 1)) * n + c];
     }
   }
+#endif
   __syncthreads();
   if (!act) return;
   const int gshift = LN * (g % (64 / LN));
+  constexpr int SLOW = MPCEKF_WIDE_XPRO ? 4 : 2;  // the exact path (4: it builds X / H_ii first)
   if ((__ballot(!ok) >> gshift) & 0xFFull) {  // outside the fast form's domain
-    if (k == 0) s.hflag[c] = 2;
+    if (k == 0) s.hflag[c] = SLOW;
     return;
   }
   const double *kp = k == 0 ? Kl : zero;
@@ -712,8 +799,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   // exec-masked store splits the wave's control flow inside the row)
   double *lst = lam;
   if (k != 0) lst = lds + T::ZERO_LDS + T::GROUPS * T::CELL_LDS + (threadIdx.x >> 6) * T::JUNK + (threadIdx.x & 63);
-  static_assert(NC <= LN + 2 && T::NX_ROWS % 4 == 0, "columns >= 8 spread as pairs over 4 lane pairs");
-  double X0[T::NX_ROWS], X1[T::NX_ROWS / 4];
+#if !MPCEKF_WIDE_XPRO
 #pragma unroll
   for (int u = 0; u < T::NX_ROWS; ++u) X0[u] = k < NC ? w.X[((size_t)u * n + c) * NC + k] : 0.0;
 #pragma unroll
@@ -721,6 +807,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     const int u = 4 * sl + (k >> 1), col = LN + (k & 1);
     X1[sl] = col < NC ? w.X[((size_t)u * n + c) * NC + col] : 0.0;
   }
+#endif
   // X(:, i) of constraint row i for lane k's two columns (the -Cu / -I rows negated)
   auto xrow = [&](int i, double &x0, double &x1) {
     const int u = xslot<NP, NC>(i);
@@ -834,7 +921,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     v1 = u1;
   }
   if (slow) {
-    if (k == 0) s.hflag[c] = 2;
+    if (k == 0) s.hflag[c] = SLOW;
     return;
   }
   if (it > maxIter) it = maxIter;
@@ -843,7 +930,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
 }
 
 // ---------------------------------------------------------------------------
-// k_hild_wide_slow: orc_hildreth with every rule, lane per cell (hflag 2 / 3)
+// k_hild_wide_slow: orc_hildreth with every rule, lane per cell (hflag 2 / 3 / 4)
 // ---------------------------------------------------------------------------
 template <int NP, int NC>
 __device__ __forceinline__ double xval_g(const double *X, int64_t n, int64_t c, int i, int k) {
@@ -935,6 +1022,29 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
 #pragma unroll
         for (int k = 0; k < NC; ++k) w.X[((size_t)xslot<NP, NC>(i) * n + c) * NC + k] = x[k];
       }
+    }
+  } else if (s.hflag[c] == 4) {  // X(:,i) and H_ii from k_hild_prep's R, as k_hild_prep would build them
+    double R[NC][NC];
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < NC; ++a)
+#pragma unroll
+      for (int b = a; b < NC; ++b) R[a][b] = w.R[(size_t)(e++) * n + c];
+#pragma unroll 1
+    for (int i = 0; i < NCON; ++i) {
+      if (xneg<NC>(i)) continue;  // H_ii of -b is stored with the b row
+      double b[NC], x[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) b[k] = mval_rt<NP, NC>(Hall, i, k);
+      chol_apply<NC>(R, b, x);
+      double h = 0.0;
+#pragma unroll
+      for (int k = 0; k < NC; ++k) {
+        h = h + b[k] * x[k];
+        w.X[((size_t)xslot<NP, NC>(i) * n + c) * NC + k] = x[k];
+      }
+      w.hii[(size_t)c * NCON + i] = h;
+      if (i < NC || (i >= 2 * NC && i < 3 * NC)) w.hii[(size_t)c * NCON + i + NC] = h;
     }
   }
 #pragma unroll 1

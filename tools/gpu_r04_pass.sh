@@ -14,6 +14,12 @@ timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || exit 1
 if [ $# -gt 0 ]; then
   bash tools/ab_libs.sh $TAG/ab "" mpc-ekf4fastcharge_amd/_build/libmpcekf.so "$@" > $O/ab.txt 2>&1 || exit 1
 fi
+if [ -n "$WIDE_AB" ]; then  # configs[4]: A/B against variant libraries, kernel trace + traffic of the product library
+  bash tools/ab_libs.sh $TAG/ab_wide "--np 20 --nc 10" mpc-ekf4fastcharge_amd/_build/libmpcekf.so $WIDE_AB > $O/ab_wide.txt 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $O/wide_trace -o run -- \
+    python3 bench.py --no-cpu --np 20 --nc 10 > $O/bench_wide_under_trace.json 2> $O/bench_wide_under_trace.err || exit 1
+  bash tools/wide_pmc.sh $TAG --steps 200 --warmup 400 || exit 1
+fi
 if [ -n "$ENV_AB" ]; then  # the product library under an environment override, twice
   for rep in 1 2; do
     env $ENV_AB timeout -k 10 300 python bench.py --no-cpu > $O/env_ab_$rep.json 2> $O/env_ab_$rep.err || exit 1
