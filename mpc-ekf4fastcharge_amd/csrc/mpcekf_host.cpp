@@ -96,6 +96,11 @@ struct mpcekf_ctx {
   bool flush_roll = false;
   hipStream_t fstream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // small batches (ncells <= MPCEKF_BOUNDS_SIDE, default 16384): k_bounds on fstream beside
+  // Hildreth.  Both read only what k_cell wrote and neither writes what the other reads;
+  // at 1,024 cells each is one wave's chain on a few CUs, so they overlap instead of adding.
+  bool bounds_side = false;
+  hipEvent_t ev_bfork = nullptr, ev_bjoin = nullptr;
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -509,11 +514,18 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   if (const char *e = std::getenv("MPCEKF_GRAPH")) X->graph = std::atoi(e) != 0;  // as mpcekf_set_graph
   // MPCEKF_FLUSH_ROLL=1: the rolling flush schedule (results identical)
   if (const char *e = std::getenv("MPCEKF_FLUSH_ROLL")) X->flush_roll = std::atoi(e) != 0;
+  {
+    int64_t side_max = 16384;
+    if (const char *e = std::getenv("MPCEKF_BOUNDS_SIDE")) side_max = std::atoll(e);
+    X->bounds_side = ncells <= side_max;
+  }
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
-  if (e == hipSuccess && X->flush_roll) {
+  if (e == hipSuccess && (X->flush_roll || X->bounds_side)) {
     e = hipStreamCreateWithFlags(&X->fstream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_join, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_bfork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&X->ev_bjoin, hipEventDisableTiming);
   }
   if (e != hipSuccess) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "stream: %s", hipGetErrorString(e)); }
   const size_t n = (size_t)ncells, NM = (size_t)X->NM;
@@ -579,6 +591,8 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   if (X->ev_fork) (void)hipEventDestroy(X->ev_fork);
   if (X->ev_join) (void)hipEventDestroy(X->ev_join);
+  if (X->ev_bfork) (void)hipEventDestroy(X->ev_bfork);
+  if (X->ev_bjoin) (void)hipEventDestroy(X->ev_bjoin);
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.R, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
@@ -742,7 +756,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   // and the uk_1 the step's iterMPC used
   const bool diag = f[12].dev || f[13].dev;
   if (diag && (rc = X->diag_bufs())) return rc;
-  constexpr int NEV = 7;  // events per step: plant | cell | bounds | hild (+ diag) |, then | flush |
+  constexpr int NEV = 8;  // events per step: plant | cell | bounds | hild (+ diag) |, then | flush |, hild start (side)
   if (X->timing && X->ev.size() < (size_t)nsteps * NEV) {
     size_t old = X->ev.size();
     X->ev.resize((size_t)nsteps * NEV);
@@ -765,6 +779,9 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   const bool capturing = X->graph && !X->timing && nsteps > 0;
   const bool roll = X->flush_roll;
   const bool fork = roll && X->fstream && !capturing;
+  // k_bounds beside Hildreth (bounds_side); under graph capture it stays on the step's stream
+  const bool side = X->bounds_side && bnd_kernel && X->fstream && !capturing;
+  const int hstart = side ? 7 : 3;  // the event that opens the Hildreth interval
   const int P = X->flush_period;
   std::vector<char> flushed((size_t)nsteps, 0);
   auto run_steps = [&]() -> int {
@@ -859,8 +876,18 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         flushed[k] = hi > lo;
       }
       // MB: k_cell writes boundzk itself (one 6x6 covariance per cell)
-      if (bnd_kernel && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, X->stream), "bounds"))) return rc;
-      if (E) HIPCHK(hipEventRecord(E[3], X->stream));
+      if (bnd_kernel) {
+        hipStream_t bs = X->stream;
+        if (side) {
+          HIPCHK(hipEventRecord(X->ev_bfork, X->stream));
+          HIPCHK(hipStreamWaitEvent(X->fstream, X->ev_bfork, 0));
+          bs = X->fstream;
+        }
+        if ((rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, zbk_k, bs), "bounds"))) return rc;
+        if (E && side) HIPCHK(hipEventRecord(E[3], bs));
+        if (side) HIPCHK(hipEventRecord(X->ev_bjoin, bs));
+      }
+      if (E) HIPCHK(hipEventRecord(E[hstart], X->stream));
       if (X->wide) {
         if ((rc = lerr(launch_hild_wide(X->k, X->s, iow, X->w, X->stream), "hild_wide"))) return rc;
       } else if (!hild_in_cell && (rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) {
@@ -873,6 +900,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
         if ((rc = lerr(rc, "cl_diag"))) return rc;
       }
       if (E) HIPCHK(hipEventRecord(E[4], X->stream));
+      // k_bounds done before k_flush or the next step's k_cell rewrites the records it reads
+      if (side) HIPCHK(hipStreamWaitEvent(X->stream, X->ev_bjoin, 0));
       if (slice && fork) HIPCHK(hipStreamWaitEvent(X->stream, X->ev_join, 0));
       if (roll ? t == nsteps : (t % P == 0 || t == nsteps)) {
         const bool timed = E && !roll;  // the rolling schedule times its slices only
@@ -915,7 +944,8 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
             (j == 3 && hild_in_cell && !diag))
           continue;
         float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + e0[j]], X->ev[(size_t)k * NEV + e0[j] + 1]));
+        const int a = j == 3 ? hstart : e0[j], b = j == 3 ? 4 : e0[j] + 1;
+        HIPCHK(hipEventElapsedTime(&ms, X->ev[(size_t)k * NEV + a], X->ev[(size_t)k * NEV + b]));
         X->t_ms[slot[j]] += ms;
         X->t_n[slot[j]] += 1;
       }

@@ -295,6 +295,41 @@ def test_flush_period_is_exact(rom, M):
             np.testing.assert_array_equal(r["state"][k], runs[0]["state"][k], err_msg=k)
 
 
+def test_bounds_side_stream_is_exact(rom, M):
+    """Small batches run k_bounds on a second stream beside Hildreth (MPCEKF_BOUNDS_SIDE:
+    up to 16,384 cells by default) and join it before k_flush / the next k_cell rewrite the
+    records it reads: boundzk and the loop give the bits of k_bounds on the step's stream,
+    over two flush windows, with per-kernel timing on (its events straddle the streams)."""
+    import os
+    n = 1000
+    soc0, tc = batch_inputs(n, seed=23)
+    outs = []
+    for side in ("0", "1000000"):
+        old = os.environ.get("MPCEKF_BOUNDS_SIDE")
+        os.environ["MPCEKF_BOUNDS_SIDE"] = side
+        try:
+            with M.Context(rom, n, M.make_config(bounds=True)) as ctx:
+                ctx.init_cells(soc0, tc)
+                ctx.set_timing(True)
+                out = ctx.step(140, outputs=("u", "v", "zk", "zbk"))
+                out["state"] = ctx.get_state()
+                out["timing"] = ctx.get_timing()
+        finally:
+            if old is None:
+                os.environ.pop("MPCEKF_BOUNDS_SIDE", None)
+            else:
+                os.environ["MPCEKF_BOUNDS_SIDE"] = old
+        outs.append(out)
+    for k in ("u", "v", "zk", "zbk"):
+        np.testing.assert_array_equal(outs[1][k], outs[0][k], err_msg=k)
+    for k in ("ekf", "bigX"):
+        np.testing.assert_array_equal(outs[1]["state"][k], outs[0]["state"][k], err_msg=k)
+    for t in outs:
+        for k in ("bounds", "hild"):
+            ms, launches = t["timing"][k]
+            assert ms > 0 and launches == 140, (k, ms, launches)
+
+
 def test_structured_hildreth_edge_paths_match_oracle(oc, M):
     """The fused step's QP solver (rank-2 sweep with its careful and dense fallbacks)
     against the C oracle on structured problems built to reach every path:
