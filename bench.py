@@ -214,7 +214,14 @@ def coordinator_main():
     os.dup2(2, 1)
     import torch
     import torch.distributed as dist
-    dist.init_process_group("gloo")
+    if "RANK" in os.environ:
+        dist.init_process_group("gloo")
+    else:  # --force-dist outside a launcher: a world of one on a private loopback store
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     print(dist.get_backend(), file=reply, flush=True)
     for line in sys.stdin:
         w = line.split()

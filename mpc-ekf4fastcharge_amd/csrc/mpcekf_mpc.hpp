@@ -64,10 +64,24 @@ __device__ __forceinline__ void lu_solve_n(const double Ain[N][N], const double 
   }
 #pragma unroll
   for (int k = 0; k < N; ++k) {
+    // first row of largest |A(i,k)| (strictly greater replaces; NaN never does), with the
+    // running maximum in a register: A[p][k] with a run-time p would put A in scratch
     int p = k;
+#if MPCEKF_LU_SCRATCH_PIVOT  // the round-3 form, for A/B
 #pragma unroll
     for (int i = k + 1; i < N; ++i)
       if (fabs(A[i][k]) > fabs(A[p][k])) p = i;
+#else
+    double pv = fabs(A[k][k]);
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      const double a = fabs(A[i][k]);
+      if (a > pv) {
+        p = i;
+        pv = a;
+      }
+    }
+#endif
     // row swap k <-> p with compile-time indices only
 #pragma unroll
     for (int i = k + 1; i < N; ++i) {

@@ -295,6 +295,40 @@ def test_flush_period_is_exact(rom, M):
             np.testing.assert_array_equal(r["state"][k], runs[0]["state"][k], err_msg=k)
 
 
+def test_mpc_stage_edge_records(rom, oc, M):
+    """iterMPC (Np = 5, k_cell's MPC part + k_hild / k_hild_slow) on linearisation records
+    built to leave the fast rank-2 sweep, next to plain ones: overflowing and infinite G
+    rows, H_ii outside [2^-400, 2^400], a NaN bound.  uk, nexec and lambda bitwise against
+    the oracle (NaN where the oracle has NaN)."""
+    n = 64
+    soc0, tc = batch_inputs(n, seed=51)
+    with M.Context(rom, n) as ctx:
+        ctx.init_cells(soc0, tc)
+        uk = np.zeros(n)
+        for _ in range(4):
+            v = ctx.OB_step(uk)
+            zk, _, xind = ctx.iterEKF(v, uk)
+            lin = ctx.EKFmatsHandler(zk, xind)
+            uk, _ = ctx.iterMPC(lin, zk[:, -1])
+        v = ctx.OB_step(uk)
+        zk, _, xind = ctx.iterEKF(v, uk)
+        lin = np.array(ctx.EKFmatsHandler(zk, xind), dtype=np.float64)
+        g = np.arange(n) % 8
+        lin[g == 1, 13:19] *= 1e300   # Cv: G_v rows overflow
+        lin[g == 2, 19] = 1e200        # Dv: H_ii overflows
+        lin[g == 3, 20:26] = np.inf    # Cphi: G_e rows non-finite
+        lin[g == 4, 27] = np.nan       # bv: a NaN bound
+        lin[g == 5, 13:20] *= 1e-170   # G_v rows tiny: H_ii below 2^-400
+        zend = zk[:, -1]
+        st = ctx.get_state()
+        uk_r, ne_r, _, lam_r = oc.mpc_lin(rom, lin, zend, st["scal"][:, 5], st["lam"])
+        uk, ne = ctx.iterMPC(lin, zend)
+        lam = ctx.get_state()["lam"]
+    for k, (a, b) in {"uk": (uk, uk_r), "lam": (lam, lam_r)}.items():
+        assert np.array_equal(a, b, equal_nan=True), (k, np.nonzero(~((a == b) | (np.isnan(a) & np.isnan(b))))[0][:8])
+    np.testing.assert_array_equal(ne, ne_r)
+
+
 def test_bounds_side_stream_is_exact(rom, M):
     """Small batches run k_bounds on a second stream beside Hildreth (MPCEKF_BOUNDS_SIDE:
     up to 16,384 cells by default) and join it before k_flush / the next k_cell rewrite the

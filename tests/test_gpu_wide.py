@@ -95,6 +95,41 @@ def test_wide_mpc_stage_open_loop_near_limit(rom, oc, M):
         assert saw_maxiter
 
 
+def test_wide_mpc_stage_edge_records(rom, oc, M):
+    """iterMPC on linearisation records built to leave k_hild_wide's fast form, next to
+    plain ones: overflowing G_v rows and an infinite Cphi (non-finite M: k_hild_prep hands
+    the cell to k_hild_wide_slow, which forms X and H_ii from R first), H_ii beyond 2^400
+    and below 2^-400 (k_hild_wide's domain check after it formed X in its prologue), a NaN
+    bound.  uk, nexec and lambda bitwise against the oracle (NaN where the oracle has NaN)."""
+    n = 64
+    soc0, tc = batch_inputs(n, seed=49)
+    with M.Context(rom, n, _cfg(M)) as ctx:
+        ctx.init_cells(soc0, tc)
+        uk = np.zeros(n)
+        for _ in range(4):
+            v = ctx.OB_step(uk)
+            zk, _, xind = ctx.iterEKF(v, uk)
+            lin = ctx.EKFmatsHandler(zk, xind)
+            uk, _ = ctx.iterMPC(lin, zk[:, -1])
+        v = ctx.OB_step(uk)
+        zk, _, xind = ctx.iterEKF(v, uk)
+        lin = np.array(ctx.EKFmatsHandler(zk, xind), dtype=np.float64)
+        g = np.arange(n) % 8
+        lin[g == 1, 13:19] *= 1e300   # Cv: G_v rows overflow
+        lin[g == 2, 19] = 1e200        # Dv: H_ii overflows
+        lin[g == 3, 20:26] = np.inf    # Cphi: G_e rows non-finite
+        lin[g == 4, 27] = np.nan       # bv: a NaN bound
+        lin[g == 5, 13:20] *= 1e-170   # G_v rows tiny: H_ii below 2^-400
+        zend = zk[:, -1]
+        st = ctx.get_state()
+        uk_r, ne_r, _, lam_r = oc.mpc_lin(rom, lin, zend, st["scal"][:, 5], st["lam"], Np=NP, Nc=NC)
+        uk, ne = ctx.iterMPC(lin, zend)
+        lam = ctx.get_state()["lam"]
+    for k, (a, b) in {"uk": (uk, uk_r), "lam": (lam, lam_r)}.items():
+        assert np.array_equal(a, b, equal_nan=True), (k, np.nonzero(~((a == b) | (np.isnan(a) & np.isnan(b))))[0][:8])
+    np.testing.assert_array_equal(ne, ne_r)
+
+
 def test_wide_stage_entry_points_match_fused(rom, M):
     n, steps = 128, 12
     soc0, tc = batch_inputs(n, seed=43)

@@ -126,8 +126,8 @@ def test_bench_refuses_world_size_mismatch():
 
 
 def test_bench_force_dist_at_world_size_one():
-    """--force-dist creates the process group at WORLD_SIZE 1 (the RCCL leg on a one-GPU
-    box; gloo here with --dry-run) and runs the timing collectives through it; without it
+    """--force-dist creates the gloo process group at WORLD_SIZE 1 (the timing coordinator
+    on a one-GPU box; here with --dry-run) and runs the timing collectives through it; without it
     a single rank runs no collective."""
     import socket
     with socket.socket() as s:
@@ -138,3 +138,6 @@ def test_bench_force_dist_at_world_size_one():
     assert "process group: gloo" in err and line["config"]["timing_collectives"] == "gloo"
     line, err = _bench("--gpus", "1", "--dry-run", "--steps", "3")
     assert "process group: none" in err and line["config"]["timing_collectives"] == "none"
+    # outside a launcher (no RANK / MASTER_*): the coordinator makes a world of one itself
+    line, err = _bench("--gpus", "1", "--dry-run", "--force-dist", "--steps", "3")
+    assert "process group: gloo" in err and line["config"]["timing_collectives"] == "gloo"

@@ -19,7 +19,7 @@ import bench  # noqa: E402
 
 M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
 P = importlib.import_module("mpc-ekf4fastcharge_amd")
-NAMES = ["scalar loads + lockout", "get_xind1", "catch-up1", "get_vars1", "chatV+gains", "meas_update x4",
+NAMES = ["plant (simStep) + scalar loads + lockout", "get_xind1", "catch-up1", "get_vars1", "chatV+gains", "meas_update x4",
          "get_xind2 + catch-up2", "get_vars2", "boundzk record", "mats_handler", "mpc_setup"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
@@ -46,9 +46,11 @@ a = np.array(acc)
 tot = a.sum(1)
 print(f"k_cell sections (median over waves, shader cycles; {len(a)} sampled steps, total median {np.median(tot):.0f}):")
 for i, nm in enumerate(NAMES):
-    print(f"  {nm:28s} {np.median(a[:, i]):9.0f}  ({100 * np.median(a[:, i] / tot):4.1f} %)")
+    print(f"  {nm:44s} {np.median(a[:, i]):9.0f}  ({100 * np.median(a[:, i] / tot):4.1f} %)")
 p = np.array(pacc)
 ptot = p.sum(1)
+if not np.any(ptot):
+    sys.exit(0)  # the plant ran inside k_cell (its first section): no k_plant launch to report
 print(f"k_plant sections (median, shader cycles; total median {np.median(ptot):.0f}):")
 for i, nm in enumerate(PNAMES):
     print(f"  {nm:40s} {np.median(p[:, i]):9.0f}  ({100 * np.median(p[:, i] / ptot):4.1f} %)")
