@@ -736,29 +736,39 @@ using MpcSetup = MpcSetupT<NP, NC>;
 // EKFmatsHandler.m:26-114.  zTE1.. are the role rows of zk, Zsoc = zk(end).
 // EKFmatsHandler.m:26-31: the corner of largest weight, first of equals; max()
 // skips NaN weights.
-__device__ __forceinline__ int corner_max(const XI &xi) {
-  int imax = 0;
+// The running maximum and its model index are carried in registers: xi.g[imax] / xi.m[imax]
+// with a run-time imax would keep the whole XI in scratch.
+__device__ __forceinline__ int corner_max(const XI &xi, int *mmax = nullptr) {
+  int imax = 0, m = xi.m[0];
+  double gm = xi.g[0];
 #pragma unroll
-  for (int j = 1; j < 4; ++j)
-    if (xi.g[j] > xi.g[imax] || (xi.g[imax] != xi.g[imax] && xi.g[j] == xi.g[j])) imax = j;
+  for (int j = 1; j < 4; ++j) {
+    const double gj = xi.g[j];
+    int mj = xi.m[j];
+    asm("" : "+v"(mj));  // a value: a select of two loads would be folded into one indexed load
+    if (gj > gm || (gm != gm && gj == gj)) {
+      imax = j;
+      gm = gj;
+      m = mj;
+    }
+  }
+  if (mmax) *mmax = m;
   return imax;
 }
 
-// xm: that corner's xhat when the caller holds it (k_cell's fused step), else read
+// xm (use_xm): that corner's xhat when the caller holds it in registers (k_cell's fused
+// step), else read from its record
 template <int NZ>
 __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
-                                             double Zsoc, double TK, Lin &L, double xend = 0.0,
-                                             const double *xm = nullptr) {
-  const int imax = corner_max(xi);
-  int m = xi.m[0];
-#pragma unroll
-  for (int j = 1; j < 4; ++j)
-    if (imax == j) m = xi.m[j];
+                                             double Zsoc, double TK, Lin &L, double xend, const double (&xm)[NX],
+                                             bool use_xm) {
+  int m;
+  (void)corner_max(xi, &m);
   const double *Cm = cc.L + m * cc.stride;
   const double *Dm = Cm + NZ * NX;
   const double *am = Dm + NZ;
   double x[NX];
-  if (xm) {
+  if (use_xm) {
 #pragma unroll
     for (int k = 0; k < NX; ++k) x[k] = xm[k];
   } else {
@@ -2830,7 +2840,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { xi.m[j] = io.xm_in[c * 4 + j]; xi.g[j] = io.xg_in[c * 4 + j]; }
     }
-    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0, fused && (PARTS & P_EKF) && have_xmax ? xmax : nullptr);
+    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0, xmax, fused && (PARTS & P_EKF) && have_xmax);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
     if (io.x_out)
 #pragma unroll
