@@ -69,6 +69,14 @@ def test_bench_algorithmic_bytes():
     # 416*NM state bytes, + model timestamps and the two input rings
     assert b["flush"] == 416 * 63 + 2 * 2 * 4 * 63 + 2 * 8 * bench.LAZY_H
     assert bench.survey_bytes_per_cell_step(63, 23) == 26736
+    # the plant runs inside k_cell (no "plant" kernel) and boundzk comes from k_bounds' record
+    assert "plant" not in b and set(b) == {"flush", "cell", "hild"}
+    bk = bench.algorithmic_bytes_per_cell(63, 23, True, bounds_kernel=True)
+    assert bk["bounds"] == (14 + 15 + 4 + 28) * 8
+    # Np = 20 / Nc = 10: k_hild_prep hands k_hild_wide chol(E) (55) and K (100), not X (800 per cell)
+    w = bench.algorithmic_bytes_per_cell(63, 100, True, Np=20, Nc=10)
+    prob = 10 * 10 + 10 + 4 * 20 + 100 + 2
+    assert w["hild"] == 2 * 8 * (36 + prob + 55 + 100) + 2 * 8 * 100 + 4 * 8
 
 
 def test_shard_ranges_cover_the_batch():
