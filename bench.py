@@ -105,6 +105,7 @@ def rom_grid(args):
         kw["T_degC"] = tuple(np.linspace(15.0, 35.0, args.rom_temps)) if args.rom_temps > 1 else (25.0,)
     if args.rom_socs:
         kw["SOC_pct"] = tuple(np.linspace(0.0, 100.0, args.rom_socs))
+    kw["lookup"] = getattr(args, "rom_lookup", "linear")
     return kw
 
 
@@ -254,6 +255,9 @@ def main():
     ap.add_argument("--rom-temps", type=int, default=0,
                     help="SURVEY.md 8(d) sensitivity: temperature set-points of the synthetic ROM (default 3)")
     ap.add_argument("--rom-socs", type=int, default=0, help="SOC set-points of the synthetic ROM (default 21)")
+    ap.add_argument("--rom-lookup", default="quintic", choices=("linear", "cubic", "quintic"),
+                    help="electrode tables (DESIGN.md §3): quintic = ABI v3 theta quintics + Arrhenius "
+                         "factor, within 1e-6 of the closed-form handles; linear = the v2 tables")
     ap.add_argument("--cpu-cells", type=int, default=32768)
     ap.add_argument("--cpu-steps", type=int, default=0, help="default: warmup + steps (the GPU run's steps)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: the cores this process may use")
@@ -369,6 +373,7 @@ def main():
                 "total_cells": total, "cells_per_gpu": [shard_range(total, world, r)[1] - shard_range(total, world, r)[0]
                                                         for r in range(world)],
                 "Np": args.np, "Nc": args.nc, "models_per_cell": rom.NM if rom else None,
+                "rom_lookup": args.rom_lookup,
                 "rom_outputs": rom.nz if rom else None,
                 "parallelism": f"cell-shard x{world} (no data-path collective)",
                 "timing_collectives": backend,
@@ -422,7 +427,8 @@ def report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id, 
         except (OSError, ValueError):
             pmc = {}
     pmc_ok = pmc.get("build_id") == build_id and pmc.get("cells") == ncell and \
-        pmc.get("Np", 5) == args.np and pmc.get("bounds", 1) == args.bounds
+        pmc.get("Np", 5) == args.np and pmc.get("bounds", 1) == args.bounds and \
+        pmc.get("rom_lookup", "linear") == args.rom_lookup
     traffic = pmc.get("per_launch_bytes", {}).get(dom) if pmc_ok else None
     flops = pmc.get("fp64_flops_per_launch", {}).get(dom) if pmc_ok else None
     fp64 = None

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPCEKF_ABI_VERSION 2
+#define MPCEKF_ABI_VERSION 3
 
 /* return codes */
 #define MPCEKF_OK 0
@@ -68,7 +68,16 @@ enum {
 /* One electrode's cellData.function.{neg,pos} handles in tabulated form.
  * The 2-D tables are [ntemp][ntheta] (row j = the handle at T = rom.tab_T_K[j] over a
  * uniform theta grid on [0, 1]) and are evaluated by the defined bilinear interpolation
- * (theta clamped to [0, 1], T clamped to the grid ends; ntemp == 1: theta only):
+ * (theta clamped to [0, 1], T clamped to the grid ends; ntemp == 1: theta only).
+ * ABI v3 (rom.tab_npoly = 4 or 6): each row is instead a piecewise polynomial in theta,
+ * *_p [ntemp][ntheta-1][tab_npoly] (Uocp1_p [ntheta-1][tab_npoly]): on interval i of the
+ * grid, with s = theta (ntheta-1) - i in [0, 1], c0 + s (c1 + s (... + s c_last)) (the
+ * exporter fits Hermite cubics / quintics to the handles' values and theta-derivatives);
+ * the node tables above stay required (the v2 route and the checks read them).  Ea[f]
+ * != 0 multiplies function f (EF order Uocp, dUocp, k0, Rf, Cdleff), after the T
+ * interpolation, by its Arrhenius factor exp(Ea/R (1/Tref - 1/T)) with the call's T
+ * (unclamped); its rows then hold f / that factor.  So a handle k(th)exp(Ea/R(1/Tref - 1/T))
+ * is exact in T, an OCP U0(th) + (T - Tref) dUdT(th) is exact in T between table rows:
  *   soc(z,T)     = soc0(T) + z*(soc100(T) - soc0(T))   iterEKF.m:282-283,439-440,497-498;
  *                                                      EKFmatsHandler.m:57-58; OB_step.m:64-65
  *   Uocp(th,T)   = Uocp       OB_step.m:313-314,337-338; iterEKF.m:362-363,404-405; EKFmatsHandler.m:84-85
@@ -83,6 +92,10 @@ typedef struct {
   const double *soc0, *soc100;                 /* [ntemp] soc(0,T), soc(1,T)       */
   const double *Uocp, *dUocp, *k0, *Rf, *Cdleff; /* [ntemp][ntheta] each            */
   const double *Uocp1;                         /* [ntheta]                         */
+  /* ABI v3: theta polynomials of the same functions (NULL when tab_npoly == 0) */
+  const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p; /* [ntemp][ntheta-1][tab_npoly] */
+  const double *Uocp1_p;                                   /* [ntheta-1][tab_npoly]        */
+  double Ea[5];            /* J/mol: Arrhenius factor of Uocp, dUocp, k0, Rf, Cdleff; 0 = none */
 } mpcekf_electrode;
 
 /* The ROM struct of runMPC.m:5 as plain arrays.  Set-points ascending. */
@@ -102,6 +115,7 @@ typedef struct {
   int32_t tab_ntheta;      /* theta grid points of the electrode tables (>= 2)     */
   int32_t tab_ntemp;       /* temperature grid points (>= 1)                       */
   const double *tab_T_K;   /* [tab_ntemp] ascending, Kelvin                        */
+  int32_t tab_npoly;       /* ABI v3: 0 = linear tables; 4 / 6 = cubic / quintic *_p */
   mpcekf_electrode neg, pos;
 } mpcekf_rom;
 

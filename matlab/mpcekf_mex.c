@@ -136,6 +136,34 @@ static const mxArray *field(const mxArray *s, const char *name) {
   return f;
 }
 
+/* ABI v3 (optional): e.poly.{Uocp,dUocp,k0,Rf,Cdleff} ntemp x (ntheta-1) x npoly and
+ * e.poly.Uocp1 (ntheta-1) x npoly theta polynomials; e.Ea 1 x 5 Arrhenius energies (J/mol)
+ * of Uocp, dUocp, k0, Rf, Cdleff.  Returns npoly (0: no polynomials). */
+static int electrode_v3(const mxArray *e, mpcekf_electrode *out, int ntemp, int ntheta) {
+  const mxArray *ea = mxGetField(e, 0, "Ea");
+  if (ea && !mxIsEmpty(ea)) {
+    const double *v = dvec(ea, 5, "Ea");
+    for (int i = 0; i < 5; ++i) out->Ea[i] = v[i];
+  }
+  const mxArray *p = mxGetField(e, 0, "poly");
+  if (!p || mxIsEmpty(p)) return 0;
+  if (!mxIsStruct(p)) mexErrMsgIdAndTxt("mpcekf:arg", "poly: expected a struct");
+  const mxArray *u1 = field(p, "Uocp1");
+  const int np = (int)mxGetN(u1);
+  if ((np != 4 && np != 6) || mxGetM(u1) != (size_t)(ntheta - 1))
+    mexErrMsgIdAndTxt("mpcekf:arg", "poly.Uocp1: expected (ntheta-1) x 4 or x 6");
+  out->Uocp1_p = rowmajor(u1, "poly.Uocp1");
+  const char *names[5] = {"Uocp", "dUocp", "k0", "Rf", "Cdleff"};
+  const double **dst[5] = {&out->Uocp_p, &out->dUocp_p, &out->k0_p, &out->Rf_p, &out->Cdleff_p};
+  for (int i = 0; i < 5; ++i) {
+    const mxArray *t = field(p, names[i]);
+    if (mxGetNumberOfElements(t) != (size_t)ntemp * (ntheta - 1) * np)
+      mexErrMsgIdAndTxt("mpcekf:arg", "poly.%s: expected ntemp x (ntheta-1) x %d", names[i], np);
+    *dst[i] = rowmajor(t, names[i]);
+  }
+  return np;
+}
+
 static void electrode(const mxArray *e, mpcekf_electrode *out, int ntemp, int ntheta) {
   out->theta0 = scalar(field(e, "theta0"), "theta0");
   out->theta100 = scalar(field(e, "theta100"), "theta100");
@@ -182,6 +210,10 @@ static void rom_from_struct(const mxArray *R, mpcekf_rom *r) {
   r->tab_ntheta = (int32_t)mxGetNumberOfElements(field(field(R, "neg"), "Uocp1"));
   electrode(field(R, "neg"), &r->neg, r->tab_ntemp, r->tab_ntheta);
   electrode(field(R, "pos"), &r->pos, r->tab_ntemp, r->tab_ntheta);
+  const int npn = electrode_v3(field(R, "neg"), &r->neg, r->tab_ntemp, r->tab_ntheta);
+  const int npp = electrode_v3(field(R, "pos"), &r->pos, r->tab_ntemp, r->tab_ntheta);
+  if (npn != npp) mexErrMsgIdAndTxt("mpcekf:arg", "ROM: poly tables for both electrodes or neither, same order");
+  r->tab_npoly = npn;
 }
 
 static void cfg_from_struct(const mxArray *s, mpcekf_config *c) {

@@ -29,7 +29,9 @@ _ip = C.POINTER(C.c_int32)
 
 class Electrode(C.Structure):
     _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
-                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp)]
+                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp),
+                ("Uocp_p", _dp), ("dUocp_p", _dp), ("k0_p", _dp), ("Rf_p", _dp), ("Cdleff_p", _dp),
+                ("Uocp1_p", _dp), ("Ea", C.c_double * 5)]
 
 
 class Rom(C.Structure):
@@ -37,7 +39,8 @@ class Rom(C.Structure):
                 ("T_degC", _dp), ("SOC_pct", _dp), ("Ts", C.c_double), ("A", _dp), ("C", _dp),
                 ("D", _dp), ("tf_code", _ip), ("tf_xloc", _dp), ("F", C.c_double), ("R", C.c_double),
                 ("Q", C.c_double), ("Rc", C.c_double), ("Tref", C.c_double), ("tab_ntheta", C.c_int32),
-                ("tab_ntemp", C.c_int32), ("tab_T_K", _dp), ("neg", Electrode), ("pos", Electrode)]
+                ("tab_ntemp", C.c_int32), ("tab_T_K", _dp), ("tab_npoly", C.c_int32), ("neg", Electrode),
+                ("pos", Electrode)]
 
 
 class Config(C.Structure):
@@ -80,6 +83,7 @@ EXPORTS = [
 ]
 
 COPY_H2D, COPY_D2H, COPY_D2D = 0, 1, 2
+ABI_VERSION = 3   # include/mpcekf.h MPCEKF_ABI_VERSION
 
 _lib = None
 
@@ -136,7 +140,7 @@ def load():
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_build_id"):
             getattr(L, nm).restype = C.c_int
-    if L.mpcekf_abi_version() != 2:
+    if L.mpcekf_abi_version() != ABI_VERSION:
         raise MpcekfError("ABI version mismatch")
     _lib = L
     return L

@@ -66,7 +66,7 @@ struct mpcekf_ctx {
   KState s{};
   mpcekf_config cfg{};
   // device buffers owned by the context
-  double *d_cell_blob = nullptr, *d_plant_blob = nullptr, *d_bulk = nullptr;
+  double *d_cell_blob = nullptr, *d_plant_blob = nullptr, *d_bulk = nullptr, *d_poly = nullptr;
   double *d_const = nullptr;  // 8 per-cell constant arrays
   double *d_mb = nullptr;     // model-blend EKF state [n][MBREC] (method MB)
   bool mb = false;
@@ -219,6 +219,15 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   for (const mpcekf_electrode *e : {&R->neg, &R->pos})
     if (!e->soc0 || !e->soc100 || !e->Uocp || !e->dUocp || !e->k0 || !e->Rf || !e->Cdleff || !e->Uocp1)
       return fail(MPCEKF_E_ROM, "rom: electrode table missing");
+  // ABI v3: theta polynomials (both electrodes, every function) and Arrhenius energies
+  if (R->tab_npoly != 0 && R->tab_npoly != 4 && R->tab_npoly != KPOLY)
+    return fail(MPCEKF_E_ARG, "rom: tab_npoly = %d (0: linear tables, 4: cubic, 6: quintic)", R->tab_npoly);
+  for (const mpcekf_electrode *e : {&R->neg, &R->pos}) {
+    if (R->tab_npoly && (!e->Uocp_p || !e->dUocp_p || !e->k0_p || !e->Rf_p || !e->Cdleff_p || !e->Uocp1_p))
+      return fail(MPCEKF_E_ROM, "rom: tab_npoly = %d but a polynomial table is missing", R->tab_npoly);
+    for (int f = 0; f < 5; ++f)
+      if (!std::isfinite(e->Ea[f])) return fail(MPCEKF_E_ROM, "rom: Ea[%d] is not finite", f);
+  }
   for (int i = 1; i < R->nT; ++i)
     if (!(R->T_degC[i] > R->T_degC[i - 1])) return fail(MPCEKF_E_ROM, "rom: T set-points not ascending");
   for (int i = 1; i < R->nZ; ++i)
@@ -332,10 +341,13 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   r.th0n = R->neg.theta0; r.th100n = R->neg.theta100; r.th0p = R->pos.theta0; r.th100p = R->pos.theta100;
 
   // --- electrode tables (mpcekf_kernels.hip ETab): header, then [fn][side][nte][nth] ---
+  // (v3: the header without Uocp1, and the rows as polynomials in a global table)
   const int nth = r.nth, nte = r.nte;
+  const bool poly = R->tab_npoly != 0;
   const mpcekf_electrode *els[2] = {&R->neg, &R->pos};
   std::vector<double> tabs;
-  for (const mpcekf_electrode *e : els) tabs.insert(tabs.end(), e->Uocp1, e->Uocp1 + nth);
+  if (!poly)
+    for (const mpcekf_electrode *e : els) tabs.insert(tabs.end(), e->Uocp1, e->Uocp1 + nth);
   for (int j = 0; j < MAXTT; ++j) tabs.push_back(j < nte ? R->tab_T_K[j] : 0.0);
   X->tabT.assign(R->tab_T_K, R->tab_T_K + nte);
   for (int e = 0; e < 2; ++e)
@@ -344,15 +356,36 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       X->soc_end[e][one].assign(src, src + nte);
       for (int j = 0; j < MAXTT; ++j) tabs.push_back(j < nte ? src[j] : 0.0);
     }
+  std::vector<double> ptab;  // v3: [fn][side][nte][nth-1][KPOLY], then Uocp1 [side][nth-1][KPOLY]
+  const int np = R->tab_npoly;
+  auto add_poly = [&](const double *src, size_t rows) {
+    for (size_t k = 0; k < rows * (size_t)(nth - 1); ++k)
+      for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[k * np + c] : 0.0);  // cubic: c4 = c5 = 0
+  };
   for (int fn = 0; fn < 5; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
     for (const mpcekf_electrode *e : els) {
+      if (poly) {
+        add_poly(fn == 0 ? e->Uocp_p : fn == 1 ? e->dUocp_p : fn == 2 ? e->k0_p : fn == 3 ? e->Rf_p : e->Cdleff_p,
+                 (size_t)nte);
+        continue;
+      }
       const double *t = fn == 0 ? e->Uocp : fn == 1 ? e->dUocp : fn == 2 ? e->k0 : fn == 3 ? e->Rf : e->Cdleff;
       tabs.insert(tabs.end(), t, t + (size_t)nte * nth);
+    }
+  if (poly)
+    for (const mpcekf_electrode *e : els) add_poly(e->Uocp1_p, 1);
+  r.npoly = poly ? KPOLY : 0;
+  r.arr = 0;
+  for (int f = 0; f < 5; ++f)
+    for (int sd = 0; sd < 2; ++sd) {
+      const double ea = els[sd]->Ea[f];
+      r.ear[f][sd] = ea != 0.0 ? ea / R->R : 0.0;  // oracle: (Ea / R) * (1/Tref - 1/T)
+      r.arr |= ea != 0.0;
     }
   // k_cell / k_bounds need no Cdleff table, unless k_cell also runs the plant (cell_plant)
   const char *cpe = getenv("MPCEKF_CELL_PLANT");
   bool cell_plant = !(cpe && atoi(cpe) == 0);
-  auto cell_tablen_of = [&](bool cp) { return tabs.size() - (cp ? 0 : (size_t)2 * nte * nth); };
+  auto cell_tablen_of = [&](bool cp) { return tabs.size() - (cp || poly ? 0 : (size_t)2 * nte * nth); };
   std::vector<double> pts(MAXT + MAXZ, 0.0);
   for (int t = 0; t < nT; ++t) pts[t] = R->T_degC[t] + 273.15;  // ROMmdls(t,z).T (initKF.m:58)
   for (int z = 0; z < nZ; ++z) pts[MAXT + z] = R->SOC_pct[z] / 100;  // ROMmdls(t,z).SOC
@@ -430,6 +463,11 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   if (lds_need() > 160 * 1024)
     return fail(MPCEKF_E_UNSUPPORTED, "rom: %d bytes of electrode tables exceed the 160 KiB LDS", lds_need());
   int rc;
+  if (poly) {
+    if ((rc = dalloc(&X->d_poly, ptab.size()))) return rc;
+    HIPCHK(hipMemcpy(X->d_poly, ptab.data(), ptab.size() * 8, hipMemcpyHostToDevice));
+    r.poly = X->d_poly;
+  }
   if ((rc = dalloc(&X->d_cell_blob, cb.size()))) return rc;
   if ((rc = dalloc(&X->d_plant_blob, pb.size()))) return rc;
   if ((rc = dalloc(&X->d_bulk, bt.size()))) return rc;
@@ -596,7 +634,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.R, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
-                  X->w.q, X->w.list, X->w.hist};
+                  X->w.q, X->w.list, X->w.hist, X->d_poly};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);

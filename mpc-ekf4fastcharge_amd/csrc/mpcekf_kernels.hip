@@ -165,36 +165,100 @@ __device__ __forceinline__ double tabi(const double *t, int n, double x) {
   double f = tt - (double)i;
   return t[i] + f * (t[i + 1] - t[i]);
 }
-// Electrode tables in LDS (include/mpcekf.h mpcekf_electrode; host: build_rom): a
+// ABI v3 polynomial row (include/mpcekf.h tab_npoly): theta's interval i and s = t - i as
+// in tabi, then Horner over the interval's 6 coefficients (a cubic's upper two are 0),
+// read from the global table (L2-resident) as three 16-byte loads.  oracle: tab_poly.
+__device__ __forceinline__ double tabp(const double *c, int n, double x) {
+  if (x != x) return __builtin_nan("");
+  double xc = fmin(fmax(x, 0.0), 1.0);
+  double tt = xc * (double)(n - 1);
+  int i = (int)floor(tt);
+  if (i > n - 2) i = n - 2;
+  const double s = tt - (double)i;
+  const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * KPOLY);
+  const double2 c01 = p[0], c23 = p[1], c45 = p[2];
+  double v = c45.y;
+  v = c45.x + s * v;
+  v = c23.y + s * v;
+  v = c23.x + s * v;
+  v = c01.y + s * v;
+  return c01.x + s * v;
+}
+// Defined exp of the v3 Arrhenius factor (oracle/mpcekf_oracle.c orc_exp, rom.py dexp):
+// x = k ln2 + r, k = floor(x / ln2 + 1/2), fdlibm's rational form for exp(r); only
+// +, -, *, /, floor and ldexp, exact or correctly rounded on both sides.
+__device__ __forceinline__ double dexp(double x) {
+  if (x != x) return x;
+  if (x > 709.782712893384) return __builtin_inf();
+  if (x < -745.1332191019412) return 0.0;
+  const double k = floor(x * 1.44269504088896338700e+00 + 0.5);
+  const double hi = x - k * dm::LN2_HI;
+  const double lo = k * dm::LN2_LO;
+  const double r = hi - lo;
+  const double t = r * r;
+  const double c = r - t * (1.66666666666666019037e-01 +
+                            t * (-2.77777777770155933842e-03 +
+                                 t * (6.61375632143793436117e-05 +
+                                      t * (-1.65339022054652515390e-06 + t * 4.13813679705723846039e-08))));
+  const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+  return ldexp(y, (int)k);
+}
+
+// Electrode tables (include/mpcekf.h mpcekf_electrode; host: build_rom).  In LDS: a
 // header [Uocp1 [side][nth] | TK [MAXTT] | soc(0,T), soc(1,T) [side][2][MAXTT]], then
 // the 2-D tables [EF_*][side][nte][nth].  EF_CDL is last and only the plant blob
 // carries it (k_cell / k_bounds never read Cdleff).  A cell's temperature bracket
 // (j, g) is found once per step (bracket); a lookup is then the theta interpolation of
 // rows j and j + 1 and a + g (b - a), the sequence of oracle/mpcekf_oracle.c tab2/tidx.
+// ABI v3 tables (KRom::npoly): the LDS header holds no Uocp1 and no 2-D tables follow;
+// the rows are polynomials in KRom::poly ([EF_*][side][nte][nth-1][KPOLY], then Uocp1
+// [side][nth-1][KPOLY]), and a function with KRom::ear != 0 is multiplied by its
+// Arrhenius factor dexp(Ea/R (1/Tref - 1/T)).
 enum { EF_U = 0, EF_DU, EF_K0, EF_RF, EF_CDL, NEF };
 __host__ __device__ constexpr int etab_header(int nth) { return 2 * nth + 5 * MAXTT; }
 struct ETab {
   const double *b;  // LDS base of the tables
+  const KRom *r;    // v3: the polynomial table and the Arrhenius energies
   int nth, nte;
+  int hn;           // Uocp1 points in the LDS header: nth (v2), 0 (v3)
   int j;            // temperature bracket of this cell-step
   double g;
+  double xa;        // v3: 1/Tref - 1/T of this cell-step (T unclamped)
+  __device__ __forceinline__ double prow(int row, double th) const {
+    return tabp(r->poly + (size_t)row * (nth - 1) * KPOLY, nth, th);
+  }
   __device__ __forceinline__ double f(int side, int fn, double th) const {
+    if (r->npoly) {
+      const int row = (fn * 2 + side) * nte + j;
+      double a = prow(row, th);
+      if (nte > 1) {
+        const double c = prow(row + 1, th);
+        a = a + g * (c - a);
+      }
+      const double ear = r->ear[fn][side];
+      if (ear != 0.0) a = a * dexp(ear * xa);
+      return a;
+    }
     const double *t = b + etab_header(nth) + ((fn * 2 + side) * nte + j) * nth;
     const double a = tabi(t, nth, th);
     if (nte == 1) return a;
     const double c = tabi(t + nth, nth, th);
     return a + g * (c - a);
   }
-  __device__ __forceinline__ double u1(int side, double th) const { return tabi(b + side * nth, nth, th); }
-  __device__ __forceinline__ double tk(int i) const { return b[2 * nth + i]; }
+  __device__ __forceinline__ double u1(int side, double th) const {
+    if (r->npoly) return prow(NEF * 2 * nte + side, th);
+    return tabi(b + side * nth, nth, th);
+  }
+  __device__ __forceinline__ double tk(int i) const { return b[2 * hn + i]; }
   __device__ __forceinline__ double send(int side, int one) const {  // soc(one, T) at the bracket
-    const double *t = b + 2 * nth + MAXTT + (side * 2 + one) * MAXTT;
+    const double *t = b + 2 * hn + MAXTT + (side * 2 + one) * MAXTT;
     if (nte == 1) return t[0];
     return t[j] + g * (t[j + 1] - t[j]);
   }
   __device__ __forceinline__ void bracket(double T) {
     j = 0;
     g = 0.0;
+    xa = r->arr ? 1.0 / r->Tref - 1.0 / T : 0.0;
     if (nte == 1) return;
     const double Tc = fmin(fmax(T, tk(0)), tk(nte - 1));
     int k = 0;
@@ -211,8 +275,10 @@ struct ETab {
 __device__ __forceinline__ ETab etab(const KRom &r, const double *base, double T) {
   ETab e;
   e.b = base;
+  e.r = &r;
   e.nth = r.nth;
   e.nte = r.nte;
+  e.hn = r.npoly ? 0 : r.nth;
   e.bracket(T);
   return e;
 }

@@ -58,7 +58,14 @@ struct KRom {
   // coefficients) and the Cdleff tables, and the fused step runs OB_step's simStep at the
   // start of k_cell (no k_plant launch)
   int cell_plant;
+  // ABI v3 electrode tables (mpcekf_kernels.hip ETab): npoly = KPOLY when the rows are
+  // theta polynomials in `poly` (global, L2-resident), 0 for the v2 linear tables in LDS;
+  // ear = Ea/R of each function's Arrhenius factor [EF_*][side], arr = any of them != 0
+  int npoly, arr;
+  const double *poly;
+  double ear[5][2];
 };
+constexpr int KPOLY = 6;  // coefficients per theta interval the kernels evaluate (quintic; cubics padded)
 
 struct KCfg {
   double SigmaV, SigmaW, ref, u_max, u_min, du_min, du_max, v_max, phise_min, zmax, hild_tol;

@@ -23,7 +23,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import LIN_SIZE, MpcekfError, check, dptr, iptr
-from .rom import ROM, TF_CODE
+from .rom import EL_TABLES, ROM, TF_CODE
 
 __all__ = ["Context", "DeviceBuffer", "hip_runtimes", "tc_grid", "make_config", "predMat", "constraintsMPC", "hildreth", "runMPC", "MpcekfError",
            "LIN_SIZE"]
@@ -88,6 +88,11 @@ class _PackedRom:
             s.theta0, s.theta100 = e.theta0, e.theta100
             for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
                 setattr(s, k, dptr(arr(getattr(e, k))))
+            for k in EL_TABLES + ("Uocp1",):    # ABI v3 theta polynomials (NULL: v2 linear tables)
+                setattr(s, k + "_p", dptr(arr(e.poly[k])) if e.poly else _lib._dp())
+            for i, k in enumerate(EL_TABLES):  # ABI v3 Arrhenius energies (0: none)
+                s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
+        r.tab_npoly = rom.npoly
         self.s = r
 
 

@@ -67,7 +67,14 @@ EL_TABLES = ("Uocp", "dUocp", "k0", "Rf", "Cdleff")   # [ntemp, ntheta] each (in
 @dataclass
 class Electrode:
     """One electrode's ``cellData.function.{neg,pos}`` handles, tabulated on the ROM's
-    (T, theta) grid (:attr:`ROM.tab_T_K` x uniform theta over [0, 1])."""
+    (T, theta) grid (:attr:`ROM.tab_T_K` x uniform theta over [0, 1]).
+
+    ABI v3 (optional): ``poly`` holds, per table, the coefficients of a piecewise
+    polynomial in theta ([ntemp, ntheta - 1, npoly], ``Uocp1``: [ntheta - 1, npoly];
+    npoly 4: cubic, 6: quintic Hermite); when present the lookups use them instead of
+    the linear interpolation of the node values.  ``Ea``
+    gives a function an Arrhenius factor exp(Ea/R (1/Tref - 1/T)) applied after the
+    temperature interpolation of its rows (0: none).  See :func:`eval_fn`."""
     theta0: float              # theta0(): the plant's zero-argument call (OB_step.m:207-210)
     theta100: float            # theta100()
     soc0: np.ndarray           # [ntemp] soc(0, T)
@@ -78,6 +85,8 @@ class Electrode:
     k0: np.ndarray             # [ntemp, ntheta] k0(theta, T)
     Rf: np.ndarray             # [ntemp, ntheta] Rf(theta, T)
     Cdleff: np.ndarray         # [ntemp, ntheta] Cdl^(2-nDL) wDL^(nDL-1) (OB_step.m:212-219)
+    poly: dict = None          # ABI v3: {"Uocp": [ntemp, ntheta-1, npoly], ..., "Uocp1": [ntheta-1, npoly]}
+    Ea: dict = None            # ABI v3: {"k0": J/mol, ...}; missing / 0: no Arrhenius factor
 
 
 def interp_tab(tab: np.ndarray, x: float) -> float:
@@ -99,6 +108,60 @@ def interp_tab(tab: np.ndarray, x: float) -> float:
     return float(tab[i] + f * (tab[i + 1] - tab[i]))
 
 
+def interp_poly(coef: np.ndarray, x: float) -> float:
+    """ABI v3 piecewise-polynomial lookup: coef [ntheta - 1, npoly] over the uniform theta
+    grid of ntheta nodes.  The interval i and its local s = t - i are found as in
+    :func:`interp_tab`; the value is Horner's c0 + s (c1 + s (... + s c_last)) (no
+    contraction).  The library evaluates 6 coefficients, a cubic's two upper ones zero,
+    which gives the same value.  Same sequence in the C oracle (tab_poly) and the kernels
+    (tabp)."""
+    if x != x:
+        return float("nan")
+    n = coef.shape[0] + 1
+    xc = min(max(x, 0.0), 1.0)
+    t = xc * (n - 1)
+    i = int(math.floor(t))
+    if i > n - 2:
+        i = n - 2
+    s = t - i
+    c = coef[i]
+    v = float(c[-1])                     # Horner: c0 + s (c1 + s (... + s c_last))
+    for k in range(len(c) - 2, -1, -1):
+        v = float(c[k] + s * v)
+    return v
+
+
+# Defined exp (the Arrhenius factor of the v3 lookup): fdlibm's reduction x = k ln2 + r and
+# its rational remez form, with only correctly rounded operations, so the kernels (dexp),
+# the C oracle (orc_exp) and this function give the same bits.
+_EXP_P = (1.66666666666666019037e-01, -2.77777777770155933842e-03, 6.61375632143793436117e-05,
+          -1.65339022054652515390e-06, 4.13813679705723846039e-08)
+_LN2_HI, _LN2_LO, _INVLN2 = 6.93147180369123816490e-01, 1.90821492927058770002e-10, 1.44269504088896338700e+00
+
+
+def dexp(x: float) -> float:
+    if x != x:
+        return x
+    if x > 709.782712893384:
+        return math.inf
+    if x < -745.1332191019412:
+        return 0.0
+    k = math.floor(x * _INVLN2 + 0.5)
+    hi = x - k * _LN2_HI
+    lo = k * _LN2_LO
+    r = hi - lo
+    t = r * r
+    P1, P2, P3, P4, P5 = _EXP_P
+    c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))))
+    y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi)
+    return math.ldexp(y, int(k))
+
+
+def arrhenius(Ea_over_R: float, Tref: float, T: float) -> float:
+    """The v3 Arrhenius factor exp(Ea/R (1/Tref - 1/T)), spelled as the kernels do."""
+    return dexp(Ea_over_R * (1.0 / Tref - 1.0 / T))
+
+
 def temp_index(T_K: np.ndarray, T: float):
     """(j, g) of T on the table temperature grid: T clamped to the grid ends, j the
     last grid index with T_K[j] <= T (at most ntemp - 2), g = (T - T_K[j]) / (T_K[j+1] - T_K[j]).
@@ -113,15 +176,28 @@ def temp_index(T_K: np.ndarray, T: float):
     return j, float((Tc - T_K[j]) / (T_K[j + 1] - T_K[j]))
 
 
-def eval_tab2(tab2: np.ndarray, theta: float, jg) -> float:
+def eval_tab2(tab2: np.ndarray, theta: float, jg, coef=None) -> float:
     """Defined bilinear lookup of a [ntemp, ntheta] table: the theta interpolation of rows
-    j and j+1, then a + g (b - a)."""
+    j and j+1, then a + g (b - a).  coef [ntemp, ntheta-1, 4] (ABI v3): the rows are the
+    piecewise polynomials instead of the linear interpolation of tab2."""
     j, g = jg
-    a = interp_tab(tab2[j], theta)
+    row = (lambda k: interp_tab(tab2[k], theta)) if coef is None else (lambda k: interp_poly(coef[k], theta))
+    a = row(j)
     if tab2.shape[0] == 1:
         return a
-    b = interp_tab(tab2[j + 1], theta)
+    b = row(j + 1)
     return float(a + g * (b - a))
+
+
+def eval_fn(e: Electrode, name: str, theta: float, jg, T: float, R: float, Tref: float) -> float:
+    """The v3 lookup of one cellData.function handle (include/mpcekf.h): the rows of
+    ``name`` at theta (polynomial when ``e.poly`` has them, else linear), linear in T between
+    the bracketing rows, times the Arrhenius factor when ``e.Ea[name]`` is non-zero."""
+    v = eval_tab2(getattr(e, name), theta, jg, None if not e.poly else e.poly.get(name))
+    ea = 0.0 if not e.Ea else float(e.Ea.get(name, 0.0))
+    if ea != 0.0:
+        v = v * arrhenius(ea / R, Tref, T)
+    return v
 
 
 def eval_tab1(tab1: np.ndarray, jg) -> float:
@@ -135,31 +211,37 @@ def eval_tab1(tab1: np.ndarray, jg) -> float:
 class CellFunctions:
     """The tabulated ``cellData.function.{neg,pos}`` handles of one electrode."""
 
-    def __init__(self, e: Electrode, T_K: np.ndarray):
+    def __init__(self, e: Electrode, T_K: np.ndarray, R: float = 8.3144621, Tref: float = 298.15):
         self.e = e
         self.T_K = np.asarray(T_K, dtype=float)
+        self.R, self.Tref = R, Tref
 
     def soc(self, z, T):                      # cellData.function.neg.soc(z,T)
         jg = temp_index(self.T_K, T)
         s0, s1 = eval_tab1(self.e.soc0, jg), eval_tab1(self.e.soc100, jg)
         return s0 + z * (s1 - s0)
 
+    def _f(self, name, theta, T):
+        return eval_fn(self.e, name, theta, temp_index(self.T_K, T), T, self.R, self.Tref)
+
     def Uocp(self, theta, T=None):            # 1-arg call: its own table (EKFmatsHandler.m:96)
         if T is None:
+            if self.e.poly:
+                return interp_poly(self.e.poly["Uocp1"], theta)
             return interp_tab(self.e.Uocp1, theta)
-        return eval_tab2(self.e.Uocp, theta, temp_index(self.T_K, T))
+        return self._f("Uocp", theta, T)
 
     def dUocp(self, theta, T):
-        return eval_tab2(self.e.dUocp, theta, temp_index(self.T_K, T))
+        return self._f("dUocp", theta, T)
 
     def k0(self, theta, T):
-        return eval_tab2(self.e.k0, theta, temp_index(self.T_K, T))
+        return self._f("k0", theta, T)
 
     def Rf(self, theta, T):
-        return eval_tab2(self.e.Rf, theta, temp_index(self.T_K, T))
+        return self._f("Rf", theta, T)
 
     def Cdleff(self, theta, T):
-        return eval_tab2(self.e.Cdleff, theta, temp_index(self.T_K, T))
+        return self._f("Cdleff", theta, T)
 
     def theta0(self):
         return self.e.theta0
@@ -211,7 +293,13 @@ class ROM:
         return self.nT * self.nZ
 
     def fn(self, which):
-        return CellFunctions(self.neg if which == "neg" else self.pos, self.tab_T_K)
+        return CellFunctions(self.neg if which == "neg" else self.pos, self.tab_T_K, self.R, self.Tref)
+
+    @property
+    def npoly(self):
+        """ABI v3: coefficients per theta interval of the electrode tables (4 cubic, 6
+        quintic), 0 for v2 linear tables."""
+        return int(np.asarray(self.neg.poly["Uocp1"]).shape[-1]) if self.neg.poly else 0
 
     @property
     def ntheta(self):
@@ -304,6 +392,21 @@ class ROM:
                     raise ValueError(f"electrode table {k}: shape {t.shape}, expected ({tk.size}, ntheta >= 2)")
             if e.Uocp1.shape != (self.ntheta,) or e.soc0.shape != (tk.size,) or e.soc100.shape != (tk.size,):
                 raise ValueError("electrode tables Uocp1 / soc0 / soc100 have the wrong length")
+            if e.poly:
+                if set(e.poly) != set(EL_TABLES) | {"Uocp1"}:
+                    raise ValueError(f"poly tables: need all of {EL_TABLES + ('Uocp1',)}, got {sorted(e.poly)}")
+                npoly = np.asarray(e.poly["Uocp1"]).shape[-1]
+                if npoly not in (4, 6):
+                    raise ValueError(f"poly tables: {npoly} coefficients per interval (4: cubic, 6: quintic)")
+                for k, c in e.poly.items():
+                    want = (self.ntheta - 1, npoly) if k == "Uocp1" else (tk.size, self.ntheta - 1, npoly)
+                    if np.asarray(c).shape != want:
+                        raise ValueError(f"poly table {k}: shape {np.asarray(c).shape}, expected {want}")
+            for k in (e.Ea or {}):
+                if k not in EL_TABLES:
+                    raise ValueError(f"Ea: {k!r} is not one of {EL_TABLES}")
+        if bool(self.neg.poly) != bool(self.pos.poly):
+            raise ValueError("poly tables must be given for both electrodes or neither")
         if not np.all(self.A[..., -1] == 1):
             raise ValueError("A does not have integrator state (initKF.m:74)")
         self.resolve_indices()
@@ -358,8 +461,13 @@ class ROM:
                  names=np.array(self.names), xloc=self.xloc, F=self.F, R=self.R, Q=self.Q, Rc=self.Rc,
                  Tref=self.Tref, tab_T_K=self.tab_T_K)
         for side, e in (("neg", self.neg), ("pos", self.pos)):
-            for k, v in e.__dict__.items():
-                d[f"{side}_{k}"] = v
+            for k in _EL_SCALARS + _EL_ARRAYS:
+                d[f"{side}_{k}"] = getattr(e, k)
+            # ABI v3 fields only when present (a v2 ROM's dict, and so its hash, is unchanged)
+            for k, v in (e.poly or {}).items():
+                d[f"{side}_poly_{k}"] = np.asarray(v, dtype=float)
+            for k, v in (e.Ea or {}).items():
+                d[f"{side}_Ea_{k}"] = float(v)
         return d
 
     def save_npz(self, path):
@@ -373,7 +481,10 @@ class ROM:
             kw = {k: float(z[f"{side}_{k}"]) for k in _EL_SCALARS}
             for k in _EL_ARRAYS:
                 kw[k] = np.array(z[f"{side}_{k}"], dtype=float)
-            return Electrode(**kw)
+            cub = {k[len(side) + 6:]: np.array(z[k], dtype=float) for k in z.files
+                   if k.startswith(f"{side}_poly_")}
+            ea = {k[len(side) + 4:]: float(z[k]) for k in z.files if k.startswith(f"{side}_Ea_")}
+            return Electrode(**kw, poly=cub or None, Ea=ea or None)
 
         return ROM(T_degC=np.array(z["T_degC"], float), SOC_pct=np.array(z["SOC_pct"], float),
                    Ts=float(z["Ts"]), A=np.array(z["A"], float), C=np.array(z["C"], float),
@@ -385,6 +496,7 @@ class ROM:
 
     # ---- JSON exchange format (matlab/mpcekf_export_rom.m) ------------------
     JSON_FORMAT = "mpcekf-rom-v2"
+    JSON_FORMAT_V3 = "mpcekf-rom-v3"   # + per-table theta polynomials and Arrhenius energies
 
     def to_json_dict(self):
         """The dict ``matlab/mpcekf_export_rom.m`` writes: every array as
@@ -397,9 +509,13 @@ class ROM:
         def el(e):
             d = {k: float(getattr(e, k)) for k in _EL_SCALARS}
             d.update({k: arr(getattr(e, k)) for k in _EL_ARRAYS})
+            if e.poly:   # v3: [ntemp, ntheta-1, 4] (Uocp1: [ntheta-1, 4]) column-major like the rest
+                d["poly"] = {k: arr(v) for k, v in e.poly.items()}
+            if e.Ea:
+                d["Ea"] = {k: float(v) for k, v in e.Ea.items()}
             return d
 
-        return {"format": self.JSON_FORMAT, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
+        return {"format": self.JSON_FORMAT_V3 if self.npoly or self.neg.Ea or self.pos.Ea else self.JSON_FORMAT, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
                 "Ts": float(self.Ts), "A": arr(self.A), "C": arr(self.C), "D": arr(self.D),
                 "names": list(self.names), "xloc": arr(self.xloc), "F": float(self.F), "R": float(self.R),
                 "Q": float(self.Q), "Rc": float(self.Rc), "Tref": float(self.Tref),
@@ -415,8 +531,9 @@ class ROM:
         """Inverse of :meth:`to_json_dict`; accepts what MATLAB's ``jsonencode`` makes of
         the exporter's struct (1-element arrays as bare numbers, NaN as null, a lone
         name as a string).  Raises ValueError on a wrong format tag or shape."""
-        if d.get("format") != ROM.JSON_FORMAT:
-            raise ValueError(f"ROM json: format {d.get('format')!r}, expected {ROM.JSON_FORMAT!r}")
+        if d.get("format") not in (ROM.JSON_FORMAT, ROM.JSON_FORMAT_V3):
+            raise ValueError(f"ROM json: format {d.get('format')!r}, expected {ROM.JSON_FORMAT!r} "
+                             f"or {ROM.JSON_FORMAT_V3!r}")
 
         def arr(a, ndim):
             if a.get("order", "F") != "F":
@@ -445,7 +562,26 @@ class ROM:
                     kw[k] = x.reshape(ntemp, -1)
                 else:
                     kw[k] = arr(e[k], 1)
-            return Electrode(**kw)
+            nth = kw["Uocp1"].size
+            cub = {}
+            pj = e.get("poly") or {}
+            # coefficients per interval (4 cubic, 6 quintic) from Uocp1's (ntheta-1) x npoly shape
+            npoly = int(np.atleast_1d(pj["Uocp1"]["shape"])[-1]) if "Uocp1" in pj else 0
+            for k, a in pj.items():
+                if k not in EL_TABLES + ("Uocp1",):
+                    raise ValueError(f"ROM json: unknown poly table {k!r}")
+                # F order with the leading ntemp (absent for Uocp1 or when MATLAB dropped a 1)
+                x = np.array([np.nan if v is None else v for v in np.atleast_1d(a["data"])], dtype=float)
+                shape = [int(v) for v in np.atleast_1d(a["shape"])]
+                if int(np.prod(shape)) != x.size:
+                    raise ValueError(f"ROM json: poly {k}: shape {shape} does not hold {x.size} values")
+                x = x.reshape(shape, order="F")
+                want = (nth - 1, npoly) if k == "Uocp1" else (ntemp, nth - 1, npoly)
+                if x.size != int(np.prod(want)):
+                    raise ValueError(f"ROM json: poly {k}: {x.size} values, expected {want}")
+                cub[k] = x.reshape(want, order="F") if x.shape != want else x
+            ea = {k: float(v) for k, v in (e.get("Ea") or {}).items()}
+            return Electrode(**kw, poly=cub or None, Ea=ea or None)
 
         names = d["names"]
         names = [names] if isinstance(names, str) else [str(s) for s in names]
@@ -557,15 +693,204 @@ def _synth_electrode(T_K, th, Tref, R, *, theta0, theta100, u, dudt, k0ref, Ea_k
                      Cdleff=(cdl ** (2 - nDL)) * (wDL ** (nDL - 1)) * ones * np.ones_like(th)[None, :])
 
 
+def _du_neg(th):
+    return (-0.8 * np.exp(-8 * th) - 0.25 / np.cosh((th - 0.55) / 0.12) ** 2 - 24.0 * np.exp(-60 * th))
+
+
+def _d2u_neg(th):
+    x = (th - 0.55) / 0.12
+    return (6.4 * np.exp(-8 * th) + (2 * 0.03 / 0.12 ** 2) * np.tanh(x) / np.cosh(x) ** 2
+            + 1440.0 * np.exp(-60 * th))
+
+
+def _d3u_neg(th):
+    x = (th - 0.55) / 0.12
+    sc2 = 1.0 / np.cosh(x) ** 2
+    return (-51.2 * np.exp(-8 * th) + (2 * 0.03 / 0.12 ** 3) * sc2 * (sc2 - 2 * np.tanh(x) ** 2)
+            - 86400.0 * np.exp(-60 * th))
+
+
+def _du_pos(th):
+    return -1.31 + 1.8 * (th - 0.4965) - 12.0 * np.exp(40 * (th - 1.0)) - 8.0 * np.exp(-40 * (th - 0.35))
+
+
+def _d2u_pos(th):
+    return 1.8 - 480.0 * np.exp(40 * (th - 1.0)) + 320.0 * np.exp(-40 * (th - 0.35))
+
+
+def _d3u_pos(th):
+    return -19200.0 * np.exp(40 * (th - 1.0)) - 12800.0 * np.exp(-40 * (th - 0.35))
+
+
+class SynthHandles:
+    """The synthetic electrodes' ``cellData.function.{neg,pos}`` as closed-form handles:
+    what a MATLAB ROM's function handles are to its exported tables.  ``make_synth_rom``
+    tabulates exactly these functions (the v2 tables sample them; the v3 tables fit them
+    by piecewise cubics with an exact Arrhenius factor), and ``oracle_np``'s handle mode
+    (``Cell(rom, handles=True)``) calls them at every reference call site, as MATLAB
+    would (OB_step.m:212-215,231-232,313-314,329-340; iterEKF.m:282-283,362-363,392-407,
+    463-464,495-500,577-580; EKFmatsHandler.m:57-69,84-85,96).
+
+    Families (Plett's parameter conventions): OCP with an entropic term,
+    U(th, T) = U0(th) + (T - Tref) dU/dT(th); Arrhenius kinetics and film resistance,
+    k0(th, T) = k0ref g(th) exp(Ea/R (1/Tref - 1/T)); the double-layer Cdleff of
+    OB_step.m:212-219 with a linear temperature coefficient of Cdl."""
+
+    def __init__(self, *, theta0, theta100, u, du, d2u, d3u, dudt, ddudt, d2dudt, d3dudt, k0ref, Ea_k0, Rf, Ea_rf,
+                 wDL, Cdl, nDL, R, Tref):
+        self.th0, self.th100 = theta0, theta100
+        self.u, self.du, self.d2u, self.d3u = u, du, d2u, d3u
+        self.dudt, self.ddudt, self.d2dudt, self.d3dudt = dudt, ddudt, d2dudt, d3dudt
+        self.k0ref, self.Ea_k0, self.Rf0, self.Ea_rf = k0ref, Ea_k0, Rf, Ea_rf
+        self.wDL, self.Cdl, self.nDL = wDL, Cdl, nDL
+        self.R, self.Tref = R, Tref
+
+    # zero-argument calls (OB_step.m:207-210)
+    def theta0(self):
+        return self.th0
+
+    def theta100(self):
+        return self.th100
+
+    def soc(self, z, T):
+        return self.th0 + z * (self.th100 - self.th0)
+
+    def Uocp(self, th, T=None):
+        if T is None:                      # one argument (EKFmatsHandler.m:96): the Tref curve
+            return float(self.u(th))
+        return float(self.u(th) + (T - self.Tref) * self.dudt(th))
+
+    def dUocp(self, th, T):
+        return float(self.du(th) + (T - self.Tref) * self.ddudt(th))
+
+    def _arr(self, Ea, T):
+        return math.exp(Ea / self.R * (1.0 / self.Tref - 1.0 / T))
+
+    def k0(self, th, T):
+        return float(self.k0ref * self._arr(self.Ea_k0, T) * (0.9 + 0.4 * th * (1 - th)))
+
+    def Rf(self, th, T):
+        return float(self.Rf0 * self._arr(-self.Ea_rf, T) * (0.8 + 0.4 * th))
+
+    def Cdleff(self, th, T):
+        cdl = self.Cdl * (1.0 + 2e-3 * (T - self.Tref))
+        return float((cdl ** (2 - self.nDL)) * (self.wDL ** (self.nDL - 1)))
+
+    # ---- tabulation: values and theta-slopes on arrays, per function --------------------
+    def rows(self, name, th, T):
+        """(value, d/dtheta, d2/dtheta2) of ``name`` at the theta array and temperature T
+        (K), with the Arrhenius factor divided out for the functions :meth:`energies` names."""
+        one = np.ones_like(th)
+        dT = T - self.Tref
+        if name == "Uocp":
+            return (self.u(th) + dT * self.dudt(th), self.du(th) + dT * self.ddudt(th),
+                    self.d2u(th) + dT * self.d2dudt(th))
+        if name == "dUocp":
+            return (self.du(th) + dT * self.ddudt(th), self.d2u(th) + dT * self.d2dudt(th),
+                    self.d3u(th) + dT * self.d3dudt(th))
+        if name == "k0":
+            return self.k0ref * (0.9 + 0.4 * th * (1 - th)), self.k0ref * 0.4 * (1 - 2 * th), -0.8 * self.k0ref * one
+        if name == "Rf":
+            return self.Rf0 * (0.8 + 0.4 * th), self.Rf0 * 0.4 * one, 0.0 * one
+        if name == "Cdleff":
+            return self.Cdleff(0.0, T) * one, 0.0 * one, 0.0 * one
+        if name == "Uocp1":
+            return self.u(th), self.du(th), self.d2u(th)
+        raise KeyError(name)
+
+    def energies(self):
+        """Ea (J/mol) of the v3 Arrhenius factor per function (Rf falls with T: -Ea)."""
+        return {"k0": self.Ea_k0, "Rf": -self.Ea_rf}
+
+
+def hermite_coefs(y, m, h, k=None):
+    """Piecewise-polynomial coefficients in s = (th - th_i) / h from node values y and
+    theta-derivatives: cubic Hermite [n-1, 4] from the slopes m; with the second
+    derivatives k, quintic Hermite [n-1, 6] (value, slope and curvature matched at both
+    nodes).  D = y_i+1 - y_i, a = h m, b = h^2 k:
+      cubic   c = [y_i, a_i, 3D - 2a_i - a_i+1, a_i + a_i+1 - 2D]
+      quintic c = [y_i, a_i, b_i/2, 10D - 6a_i - 4a_i+1 - (3b_i - b_i+1)/2,
+                   -15D + 8a_i + 7a_i+1 + (3b_i - 2b_i+1)/2, 6D - 3(a_i + a_i+1) - (b_i - b_i+1)/2]"""
+    y = np.asarray(y, dtype=float)
+    a = h * np.asarray(m, dtype=float)
+    d = y[1:] - y[:-1]
+    a0, a1 = a[:-1], a[1:]
+    if k is None:
+        return np.stack([y[:-1], a0, 3 * d - 2 * a0 - a1, a0 + a1 - 2 * d], axis=-1)
+    b = h * h * np.asarray(k, dtype=float)
+    b0, b1 = b[:-1], b[1:]
+    return np.stack([y[:-1], a0, b0 / 2, 10 * d - 6 * a0 - 4 * a1 - (3 * b0 - b1) / 2,
+                     -15 * d + 8 * a0 + 7 * a1 + (3 * b0 - 2 * b1) / 2, 6 * d - 3 * (a0 + a1) - (b0 - b1) / 2],
+                    axis=-1)
+
+
+def tabulate_electrode(hd: SynthHandles, th, T_K, order=1):
+    """An Electrode from closed-form handles: v2 node tables (the handle values at the
+    (T, theta) nodes), and with ``order`` 3 / 5 the v3 cubic / quintic Hermite
+    coefficients of each row, with the Arrhenius factor of ``hd.energies()`` divided out
+    of the rows."""
+    th = np.asarray(th, dtype=float)
+    T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
+    h = 1.0 / (th.size - 1)
+    cubic = order > 1
+    ea = hd.energies() if cubic else {}
+    tabs, coefs = {}, {}
+    for name in EL_TABLES:
+        vals, cs = [], []
+        for T in T_K:
+            y, m, k = hd.rows(name, th, T)
+            if not cubic and name in ("k0", "Rf"):    # v2: the handle's values, factor included
+                f = hd._arr(hd.Ea_k0 if name == "k0" else -hd.Ea_rf, T)
+                y = y * f
+            vals.append(y)
+            cs.append(hermite_coefs(y, m, h, k if order == 5 else None))
+        tabs[name] = np.array(vals)
+        coefs[name] = np.array(cs)
+    u1, m1, k1 = hd.rows("Uocp1", th, hd.Tref)
+    coefs["Uocp1"] = hermite_coefs(u1, m1, h, k1 if order == 5 else None)
+    return Electrode(theta0=hd.th0, theta100=hd.th100, soc0=np.full(T_K.size, hd.th0),
+                     soc100=np.full(T_K.size, hd.th100), Uocp=tabs["Uocp"], Uocp1=u1, dUocp=tabs["dUocp"],
+                     k0=tabs["k0"], Rf=tabs["Rf"], Cdleff=tabs["Cdleff"],
+                     poly=coefs if cubic else None, Ea=ea or None)
+
+
+def synth_handles(R=8.3144621, Tref=298.15):
+    """(neg, pos) closed-form handles of the synthetic NMC30-like cell."""
+    neg = SynthHandles(theta0=0.01, theta100=0.80, u=_u_neg, du=_du_neg, d2u=_d2u_neg, d3u=_d3u_neg,
+                       dudt=lambda x: -1.0e-4 * np.exp(-5 * x), ddudt=lambda x: 5.0e-4 * np.exp(-5 * x),
+                       d2dudt=lambda x: -2.5e-3 * np.exp(-5 * x), d3dudt=lambda x: 1.25e-2 * np.exp(-5 * x), k0ref=2.0, Ea_k0=3.0e4, Rf=2.0e-3,
+                       Ea_rf=1.0e4, wDL=5.0, Cdl=150.0, nDL=0.95, R=R, Tref=Tref)
+    pos = SynthHandles(theta0=0.93, theta100=0.40, u=_u_pos, du=_du_pos, d2u=_d2u_pos, d3u=_d3u_pos,
+                       dudt=lambda x: -0.5e-4 * (1 - x), ddudt=lambda x: 0.5e-4 + 0.0 * x,
+                       d2dudt=lambda x: 0.0 * x, d3dudt=lambda x: 0.0 * x, k0ref=4.0, Ea_k0=4.0e4, Rf=3.0e-3, Ea_rf=1.0e4, wDL=5.0,
+                       Cdl=120.0, nDL=0.93, R=R, Tref=Tref)
+    return neg, pos
+
+
 def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), Ts=1.0,
-                   ntab=201, tab_T_degC=(5.0, 25.0, 45.0)) -> ROM:
+                   ntab=None, tab_T_degC=None, lookup="linear") -> ROM:
     """Deterministic synthetic NMC30-like xRA ROM.
 
     Every number is fixed here; nothing random.  Local models differ smoothly with
     temperature (Arrhenius) and SOC so the bilinear blends of OB_step.m:281-285 and
-    iterEKF.m:312-313 exercise real interpolation.  The electrode handles are tabulated
-    on ``tab_T_degC`` x ``ntab`` theta points (include/mpcekf.h mpcekf_electrode).
+    iterEKF.m:312-313 exercise real interpolation.  The electrode handles
+    (:func:`synth_handles`, attached as ``rom.handles``) are tabulated on ``tab_T_degC``
+    x ``ntab`` theta points (include/mpcekf.h mpcekf_electrode):
+
+    * ``lookup="linear"`` (ABI v2, the default of the round-1..4 fixtures): node values,
+      linear in theta and T; ``ntab`` default 201;
+    * ``lookup="cubic"`` / ``"quintic"`` (ABI v3): Hermite cubics / quintics in theta
+      from the handles' values and theta-derivatives, k0 / Rf with their exact Arrhenius
+      factor; ``ntab`` default 1025 / 513 (the quintic follows the handles
+      to the ulp level on the outputs, the cubic to ~1e-10).
     """
+    order = {"linear": 1, "cubic": 3, "quintic": 5}.get(lookup)
+    if order is None:
+        raise ValueError(f"lookup {lookup!r}: 'linear', 'cubic' or 'quintic'")
+    if tab_T_degC is None:   # v3: rows past the operating range (an affine OCP is exact between rows, not beyond)
+        tab_T_degC = (5.0, 25.0, 45.0) if lookup == "linear" else (-10.0, 25.0, 60.0)
+    if ntab is None:   # DESIGN.md §3 (tools/handle_gap.py): the quintic at 513 points follows the handles to ulps
+        ntab = {"linear": 201, "cubic": 1025, "quintic": 513}[lookup]
     T_degC = np.asarray(T_degC, dtype=float)
     SOC_pct = np.asarray(SOC_pct, dtype=float)
     R = 8.3144621
@@ -577,12 +902,17 @@ def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), T
 
     th = np.linspace(0.0, 1.0, ntab)
     T_K = np.asarray(tab_T_degC, dtype=float) + 273.15
-    neg = _synth_electrode(T_K, th, Tref, R, theta0=0.01, theta100=0.80, u=_u_neg,
-                           dudt=lambda x: -1.0e-4 * np.exp(-5 * x), k0ref=2.0, Ea_k0=3.0e4, Rf=2.0e-3,
-                           Ea_rf=1.0e4, wDL=5.0, Cdl=150.0, nDL=0.95)
-    pos = _synth_electrode(T_K, th, Tref, R, theta0=0.93, theta100=0.40, u=_u_pos,
-                           dudt=lambda x: -0.5e-4 * (1 - x), k0ref=4.0, Ea_k0=4.0e4, Rf=3.0e-3,
-                           Ea_rf=1.0e4, wDL=5.0, Cdl=120.0, nDL=0.93)
+    hn, hp = synth_handles(R, Tref)
+    if lookup == "linear":   # the round-1..4 tables, bit for bit (their fixtures are keyed by this ROM's hash)
+        neg = _synth_electrode(T_K, th, Tref, R, theta0=0.01, theta100=0.80, u=_u_neg,
+                               dudt=lambda x: -1.0e-4 * np.exp(-5 * x), k0ref=2.0, Ea_k0=3.0e4, Rf=2.0e-3,
+                               Ea_rf=1.0e4, wDL=5.0, Cdl=150.0, nDL=0.95)
+        pos = _synth_electrode(T_K, th, Tref, R, theta0=0.93, theta100=0.40, u=_u_pos,
+                               dudt=lambda x: -0.5e-4 * (1 - x), k0ref=4.0, Ea_k0=4.0e4, Rf=3.0e-3,
+                               Ea_rf=1.0e4, wDL=5.0, Cdl=120.0, nDL=0.93)
+    else:
+        neg = tabulate_electrode(hn, th, T_K, order=order)
+        pos = tabulate_electrode(hp, th, T_K, order=order)
     res0n = -Ts * (neg.theta100 - neg.theta0) / (3600 * Q)
     res0p = -Ts * (pos.theta100 - pos.theta0) / (3600 * Q)
 
@@ -613,6 +943,8 @@ def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), T
     rom = ROM(T_degC=T_degC, SOC_pct=SOC_pct, Ts=float(Ts), A=A, C=C, D=D,
               names=[o[0] for o in _OUTPUTS], xloc=np.array([o[1] for o in _OUTPUTS]),
               F=F, R=R, Q=Q, Rc=8.0e-4, Tref=Tref, tab_T_K=T_K, neg=neg, pos=pos,
-              meta={"kind": "synthetic-NMC30-like", "version": 2})
+              meta={"kind": "synthetic-NMC30-like", "version": 2 if lookup == "linear" else 3,
+                    "lookup": lookup})
+    rom.handles = {"neg": hn, "pos": hp}
     rom.validate()
     return rom

@@ -101,6 +101,10 @@ typedef struct {
   const double *soc0, *soc100;                   /* [ntemp] */
   const double *Uocp, *dUocp, *k0, *Rf, *Cdleff; /* [ntemp][ntheta] */
   const double *Uocp1;                           /* [ntheta] one-argument Uocp (EKFmatsHandler.m:96) */
+  /* ABI v3 (include/mpcekf.h): theta polynomials [ntemp][ntheta-1][6] ([ntheta-1][6] for
+   * Uocp1), all NULL for linear tables; Arrhenius energies of Uocp, dUocp, k0, Rf, Cdleff */
+  const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p, *Uocp1_p;
+  double Ea[5];
 } orc_electrode;
 
 typedef struct {
@@ -117,6 +121,8 @@ typedef struct {
   const double *TK; /* [ntemp] table temperatures (K, ascending) */
   orc_electrode neg, pos;
 } orc_rom;
+enum { EF_U = 0, EF_DU, EF_K0, EF_RF, EF_CDL };
+#define NPOLY 6 /* coefficients per theta interval of the v3 tables (a cubic's upper two are 0) */
 
 typedef struct {
   int Np, Nc;
@@ -199,14 +205,58 @@ static void tidx(const orc_rom *r, double T, int *j, double *g) {
   *j = k;
   *g = (Tc - r->TK[k]) / (r->TK[k + 1] - r->TK[k]);
 }
-static double tab2(const orc_rom *r, const double *t, double th, double T) {
+/* ABI v3 row: the polynomial of theta's interval, Horner over 6 coefficients in
+ * s = t - i (rom.py interp_poly, mpcekf_kernels.hip tabp) */
+static double tab_poly(const double *c, int n, double x) {
+  if (x != x) return NAN;
+  double xc = fmin(fmax(x, 0.0), 1.0);
+  double t = xc * (double)(n - 1);
+  int i = (int)floor(t);
+  if (i > n - 2) i = n - 2;
+  double s = t - (double)i;
+  const double *p = c + (size_t)i * NPOLY;
+  double v = p[5];
+  v = p[4] + s * v;
+  v = p[3] + s * v;
+  v = p[2] + s * v;
+  v = p[1] + s * v;
+  return p[0] + s * v;
+}
+/* Defined exp (the v3 Arrhenius factor; rom.py dexp, mpcekf_kernels.hip dexp): fdlibm's
+ * reduction x = k ln2 + r (k = floor(x / ln2 + 1/2)) and its rational form for exp(r);
+ * +, -, *, /, floor and ldexp only, each exact or correctly rounded on both sides. */
+static const double EXP_P1 = 1.66666666666666019037e-01, EXP_P2 = -2.77777777770155933842e-03,
+                    EXP_P3 = 6.61375632143793436117e-05, EXP_P4 = -1.65339022054652515390e-06,
+                    EXP_P5 = 4.13813679705723846039e-08, EXP_INVLN2 = 1.44269504088896338700e+00;
+double orc_exp(double x) {
+  if (x != x) return x;
+  if (x > 709.782712893384) return INFINITY;
+  if (x < -745.1332191019412) return 0.0;
+  double k = floor(x * EXP_INVLN2 + 0.5);
+  double hi = x - k * DM_LN2_HI;
+  double lo = k * DM_LN2_LO;
+  double r = hi - lo;
+  double t = r * r;
+  double c = r - t * (EXP_P1 + t * (EXP_P2 + t * (EXP_P3 + t * (EXP_P4 + t * EXP_P5))));
+  double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+  return ldexp(y, (int)k);
+}
+/* One handle lookup (include/mpcekf.h): the rows j, j+1 of the T bracket at
+ * theta (linear in the node values, or the v3 polynomials), a + g (b - a), then the
+ * Arrhenius factor exp(Ea/R (1/Tref - 1/T)) when Ea != 0 (T unclamped). */
+static double tab2(const orc_rom *r, const double *t, const double *tp, double Ea, double th, double T) {
   int j;
   double g;
   tidx(r, T, &j, &g);
-  double a = tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
-  if (r->ntemp == 1) return a;
-  double b = tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
-  return a + g * (b - a);
+  const size_t rp = (size_t)(r->ntheta - 1) * NPOLY;
+  double a = tp ? tab_poly(tp + j * rp, r->ntheta, th) : tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
+  if (r->ntemp > 1) {
+    double b = tp ? tab_poly(tp + (j + 1) * rp, r->ntheta, th)
+                  : tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
+    a = a + g * (b - a);
+  }
+  if (Ea != 0.0) a = a * orc_exp((Ea / r->R) * (1.0 / r->Tref - 1.0 / T));
+  return a;
 }
 static double tab1T(const orc_rom *r, const double *t, double T) {
   int j;
@@ -220,12 +270,24 @@ static double fsoc(const orc_rom *r, const orc_electrode *e, double z, double T)
   double s0 = tab1T(r, e->soc0, T), s1 = tab1T(r, e->soc100, T);
   return s0 + z * (s1 - s0);
 }
-static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Uocp, th, T); }
-static double fUocp1(const orc_rom *r, const orc_electrode *e, double th) { return tab_interp(e->Uocp1, r->ntheta, th); }
-static double fdUocp(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->dUocp, th, T); }
-static double fk0(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->k0, th, T); }
-static double fRf(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Rf, th, T); }
-static double fCdl(const orc_rom *r, const orc_electrode *e, double th, double T) { return tab2(r, e->Cdleff, th, T); }
+static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
+  return tab2(r, e->Uocp, e->Uocp_p, e->Ea[EF_U], th, T);
+}
+static double fUocp1(const orc_rom *r, const orc_electrode *e, double th) {
+  return e->Uocp1_p ? tab_poly(e->Uocp1_p, r->ntheta, th) : tab_interp(e->Uocp1, r->ntheta, th);
+}
+static double fdUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
+  return tab2(r, e->dUocp, e->dUocp_p, e->Ea[EF_DU], th, T);
+}
+static double fk0(const orc_rom *r, const orc_electrode *e, double th, double T) {
+  return tab2(r, e->k0, e->k0_p, e->Ea[EF_K0], th, T);
+}
+static double fRf(const orc_rom *r, const orc_electrode *e, double th, double T) {
+  return tab2(r, e->Rf, e->Rf_p, e->Ea[EF_RF], th, T);
+}
+static double fCdl(const orc_rom *r, const orc_electrode *e, double th, double T) {
+  return tab2(r, e->Cdleff, e->Cdleff_p, e->Ea[EF_CDL], th, T);
+}
 static double msqrt(double x) { return x >= 0 ? sqrt(x) : NAN; }
 
 /* ----------------------------------------------------------------------- */
@@ -1539,4 +1601,4 @@ int orc_run(const orc_rom *r, const orc_cfg *c, int ncells, const double *soc0, 
   return orc_run_traj(r, c, ncells, soc0, tc, nsteps, u, v, soc, phise, nexec, status, zk, zbk, NULL, nthreads);
 }
 
-int orc_version(void) { return 2; }
+int orc_version(void) { return 3; }

@@ -26,7 +26,22 @@ _ip = C.POINTER(C.c_int32)
 
 class _Electrode(C.Structure):
     _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
-                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp)]
+                ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp),
+                ("Uocp_p", _dp), ("dUocp_p", _dp), ("k0_p", _dp), ("Rf_p", _dp), ("Cdleff_p", _dp),
+                ("Uocp1_p", _dp), ("Ea", C.c_double * 5)]
+
+
+EL_FNS = ("Uocp", "dUocp", "k0", "Rf", "Cdleff")   # orc_electrode.Ea order (EF_*)
+
+
+def poly6(c):
+    """v3 theta polynomials padded to the 6 coefficients the C oracle and the library
+    evaluate (a cubic's c4 = c5 = 0)."""
+    c = np.asarray(c, dtype=np.float64)
+    if c.shape[-1] == 6:
+        return c
+    pad = np.zeros(c.shape[:-1] + (6 - c.shape[-1],))
+    return np.concatenate([c, pad], axis=-1)
 
 
 class _Rom(C.Structure):
@@ -89,6 +104,8 @@ def lib():
         L.orc_sigma_min.argtypes = [C.c_int, _dp]
         L.orc_meas_cov.argtypes = [_dp, _dp, C.c_double, C.c_int]
         L.orc_jacobi.argtypes = [C.c_int, _dp, _dp, _dp]
+        L.orc_exp.restype = C.c_double      # the v3 Arrhenius factor's defined exp
+        L.orc_exp.argtypes = [C.c_double]
         _lib = L
     return _lib
 
@@ -127,6 +144,10 @@ class PackedRom:
             s.theta0, s.theta100 = e.theta0, e.theta100
             for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
                 setattr(s, k, _p(arr(getattr(e, k))))
+            for k in EL_FNS + ("Uocp1",):   # ABI v3 polynomials (NULL: linear tables)
+                setattr(s, k + "_p", _p(arr(poly6(e.poly[k]))) if e.poly else _dp())
+            for i, k in enumerate(EL_FNS):
+                s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
         self.s = r
 
 

@@ -163,9 +163,14 @@ def stable_two_nearest(d):
 class Cell:
     """Reads the ROM *data*; re-implements the tabulated handle semantics itself
     (include/mpcekf.h mpcekf_electrode): [ntemp, ntheta] tables, theta interpolated
-    on a uniform [0, 1] grid, then T linearly between the two bracketing grid rows."""
+    on a uniform [0, 1] grid (linearly, or by the v3 piecewise polynomials), then T linearly
+    between the two bracketing grid rows, then the v3 Arrhenius factor.
 
-    def __init__(self, rom):
+    ``handles=True``: calls the ROM's closed-form ``cellData.function`` handles
+    (``rom.handles``, rom.py SynthHandles) instead, at every call site, as MATLAB does --
+    the reference semantics the tables approximate."""
+
+    def __init__(self, rom, handles=False):
         self.rom = rom
         self.F = rom.F
         self.R = rom.R
@@ -174,6 +179,11 @@ class Cell:
         self.Tref = rom.Tref
         self.TK = [float(t) for t in np.atleast_1d(rom.tab_T_K)]
         self.e = {"neg": rom.neg, "pos": rom.pos}
+        self.h = None
+        if handles:
+            self.h = getattr(rom, "handles", None)
+            if self.h is None:
+                raise ValueError("handle mode needs a ROM with closed-form handles (rom.handles)")
 
     @staticmethod
     def _interp(tab, x):
@@ -188,6 +198,40 @@ class Cell:
         f = t - i
         return float(tab[i] + f * (tab[i + 1] - tab[i]))
 
+    @staticmethod
+    def _poly(coef, x):
+        """v3 row: Horner c0 + s (c1 + s (... + s c_last)) on interval i of the uniform grid."""
+        if x != x:
+            return NAN
+        n = len(coef) + 1
+        xc = min(max(x, 0.0), 1.0)
+        t = xc * (n - 1)
+        i = int(math.floor(t))
+        if i > n - 2:
+            i = n - 2
+        s = t - i
+        c = coef[i]
+        v = float(c[-1])                     # Horner: c0 + s (c1 + s (... + s c_last))
+        for k in range(len(c) - 2, -1, -1):
+            v = float(c[k] + s * v)
+        return v
+
+    def _fn(self, s, name, th, T):
+        """One v3 lookup: rows (polynomial or linear) bilinear in T, times the Arrhenius factor."""
+        e = self.e[s]
+        coef = e.poly.get(name) if e.poly else None
+        tab = getattr(e, name)
+        j, g = self._tj(T)
+        row = (lambda k: self._interp(tab[k], th)) if coef is None else (lambda k: self._poly(coef[k], th))
+        v = row(j)
+        if len(self.TK) > 1:
+            b = row(j + 1)
+            v = v + g * (b - v)
+        ea = float(e.Ea.get(name, 0.0)) if e.Ea else 0.0
+        if ea != 0.0:
+            v = v * _dexp((ea / self.R) * (1.0 / self.Tref - 1.0 / T))
+        return v
+
     def _tj(self, T):
         TK = self.TK
         if len(TK) == 1:
@@ -198,15 +242,9 @@ class Cell:
             j += 1
         return j, (Tc - TK[j]) / (TK[j + 1] - TK[j])
 
-    def _tab2(self, tab, th, T):
-        j, g = self._tj(T)
-        a = self._interp(tab[j], th)
-        if len(self.TK) == 1:
-            return a
-        b = self._interp(tab[j + 1], th)
-        return a + g * (b - a)
-
     def soc(self, s, z, T):
+        if self.h is not None:
+            return self.h[s].soc(z, T)
         e = self.e[s]
         j, g = self._tj(T)
         if len(self.TK) == 1:
@@ -217,22 +255,48 @@ class Cell:
         return s0 + z * (s1 - s0)
 
     def Uocp(self, s, th, T=None):
+        if self.h is not None:
+            return self.h[s].Uocp(th, T)
         if T is None:                                  # one-argument call (EKFmatsHandler.m:96)
-            return self._interp(self.e[s].Uocp1, th)
-        return self._tab2(self.e[s].Uocp, th, T)
+            e = self.e[s]
+            return self._poly(e.poly["Uocp1"], th) if e.poly else self._interp(e.Uocp1, th)
+        return self._fn(s, "Uocp", th, T)
 
     def dUocp(self, s, th, T):
-        return self._tab2(self.e[s].dUocp, th, T)
+        return self.h[s].dUocp(th, T) if self.h is not None else self._fn(s, "dUocp", th, T)
 
     def k0(self, s, th, T):
-        return self._tab2(self.e[s].k0, th, T)
+        return self.h[s].k0(th, T) if self.h is not None else self._fn(s, "k0", th, T)
 
     def Rf(self, s, th, T):
-        return self._tab2(self.e[s].Rf, th, T)
+        return self.h[s].Rf(th, T) if self.h is not None else self._fn(s, "Rf", th, T)
 
     def Cdleff(self, s, th, T):
         """Cdl(th,T)^(2-nDL) * wDL(th,T)^(nDL-1) (OB_step.m:212-219), tabulated by the exporter."""
-        return self._tab2(self.e[s].Cdleff, th, T)
+        return self.h[s].Cdleff(th, T) if self.h is not None else self._fn(s, "Cdleff", th, T)
+
+
+# the defined exp of the v3 Arrhenius factor (rom.py dexp; kernels dexp; C oracle orc_exp)
+_EXP_P = (1.66666666666666019037e-01, -2.77777777770155933842e-03, 6.61375632143793436117e-05,
+          -1.65339022054652515390e-06, 4.13813679705723846039e-08)
+
+
+def _dexp(x):
+    if x != x:
+        return x
+    if x > 709.782712893384:
+        return math.inf
+    if x < -745.1332191019412:
+        return 0.0
+    k = math.floor(x * 1.44269504088896338700e+00 + 0.5)
+    hi = x - k * 6.93147180369123816490e-01
+    lo = k * 1.90821492927058770002e-10
+    r = hi - lo
+    t = r * r
+    P1, P2, P3, P4, P5 = _EXP_P
+    c = r - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))))
+    y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi)
+    return math.ldexp(y, int(k))
 
 
 # ---------------------------------------------------------------------------
@@ -272,9 +336,9 @@ def setup_inds(rom):
 # ---------------------------------------------------------------------------
 # OB_step (plant), OB_step.m:1-357
 # ---------------------------------------------------------------------------
-def ob_step_init(rom, SOC0_pct, Tc):
+def ob_step_init(rom, SOC0_pct, Tc, handles=False):
     """First call of OB_step (OB_step.m:39-72): returns cellState."""
-    cell = Cell(rom)
+    cell = Cell(rom, handles)
     ind = setup_inds(rom)
     NM = rom.NM
     bigA = np.zeros((rom.n + 1, NM))
@@ -388,7 +452,7 @@ def ob_step(Iapp, Tc, cs):
 # ---------------------------------------------------------------------------
 # initKF (initKF.m:30-136) and iterEKF 'OB' (iterEKF.m:30-210)
 # ---------------------------------------------------------------------------
-def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW, method="OB"):
+def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW, method="OB", handles=False):
     """initKF.m:30-136.  method 'OB' (output blend) or 'MB' (model blend, initKF.m:44-49)."""
     n = rom.n
     method = {"OUTB": "OB", "OB": "OB", "MDLB": "MB", "MB": "MB"}[method.upper()]
@@ -404,7 +468,7 @@ def init_kf(rom, SOC0, T0, SigmaX0, SigmaV, SigmaW, method="OB"):
             M[(t, z)] = dict(A=rom.A[t, z, :n].copy(), C=rom.C[t, z, :, :n].copy(),
                              D=rom.D[t, z].copy(), xhat=np.zeros(n),
                              SigmaX=np.array(SigmaX0[:n, :n], dtype=float))
-    return dict(rom=rom, cell=Cell(rom), ind=setup_inds(rom), M=M, n=n, nz=rom.nz,
+    return dict(rom=rom, cell=Cell(rom, handles), ind=setup_inds(rom), M=M, n=n, nz=rom.nz,
                 x0=0.0, SigmaX0=float(SigmaX0[n, n]), xhat=np.zeros(n + 1),
                 SigmaV=SigmaV, SigmaW=SigmaW, priorI=0.0, Ts=rom.Ts, SOC0=SOC0 / 100,
                 Q=rom.Q, Tpts=np.unique(TK), Zpts=np.unique(ZS), warnCount=0, status=0,
@@ -1012,9 +1076,10 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
     if cfg:
         c.update(cfg)
     SigmaX0 = np.diag([1.0] * rom.n + [2e6])
-    ekf = init_kf(rom, SOC0, TC, SigmaX0, c["SigmaV"], c["SigmaW"], c.get("method", "OB"))
+    hm = bool(c.get("handles", False))   # cellData.function handles called directly (Cell)
+    ekf = init_kf(rom, SOC0, TC, SigmaX0, c["SigmaV"], c["SigmaW"], c.get("method", "OB"), hm)
     mpc = init_mpc(rom, SOC0, c["Np"], c["Nc"], c["targetSOC"], c)
-    cs = ob_step_init(rom, SOC0, TC)
+    cs = ob_step_init(rom, SOC0, TC, hm)
     uk = 0.0
     ob_step(uk, TC, cs)                                         # runMPC.m:74 (state no-op)
     nz = rom.nz

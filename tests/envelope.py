@@ -62,3 +62,22 @@ def check_near(out, e, window=NEAR_TAIL):
     end = np.asarray(out["soc"])[-1]
     bad = outside(end, e["soc_end"].min(1), e["soc_end"].max(1))
     assert not bad.any(), f"final SOC of cells {np.nonzero(bad)[0].tolist()} outside the members' range"
+
+
+def check_tail_stats(out, e):
+    """One cell's trajectories [steps] (or [steps, 1]) over its chaotic tail [tail0, end)
+    against the members of a ulp ensemble (tests/golden/handles_runmpc_3001): the window
+    mean, 10th and 90th percentile of u, v, soc and phise each inside the range the
+    members' own statistics span (widened by 1e-6 relative), and the step to 90 % SOC
+    one of the members' (check_near's rule for a single cell)."""
+    a = int(e["tail0"])
+    stats = {"wmean": lambda x: x.mean(), "wlo": lambda x: np.percentile(x, 10), "whi": lambda x: np.percentile(x, 90)}
+    for k in KEYS:
+        x = np.asarray(out[k]).reshape(-1)[a:]
+        for nm, f in stats.items():
+            m = e[f"{k}_{nm}"]
+            assert not outside(np.array([f(x)]), m.min(), m.max()).any(), \
+                f"{k} {nm} over steps {a}-: {f(x)!r} outside the members' [{m.min()!r}, {m.max()!r}]"
+    soc = np.asarray(out["soc"]).reshape(-1)
+    t90 = int(np.argmax(soc >= 0.90)) if (soc >= 0.90).any() else -1
+    assert e["t90"].min() <= t90 <= e["t90"].max(), (t90, e["t90"].min(), e["t90"].max())

@@ -162,8 +162,17 @@ def rom_struct(rom):
                     soc100=np.asarray(e.soc100, float), Uocp=np.asarray(e.Uocp, float),
                     dUocp=np.asarray(e.dUocp, float), k0=np.asarray(e.k0, float), Rf=np.asarray(e.Rf, float),
                     Cdleff=np.asarray(e.Cdleff, float), Uocp1=np.asarray(e.Uocp1, float))
+
+    def el3(e):   # ABI v3: theta polynomials and Arrhenius energies (mpcekf_rom_struct.m's poly / Ea)
+        d = el(e)
+        if e.poly:
+            d["poly"] = {k: np.asarray(v, float) for k, v in e.poly.items()}
+        if e.Ea:
+            d["Ea"] = np.array([float(e.Ea.get(k, 0.0)) for k in ("Uocp", "dUocp", "k0", "Rf", "Cdleff")])
+        return d
+    el_ = el3
     return dict(T_degC=np.asarray(rom.T_degC, float), SOC_pct=np.asarray(rom.SOC_pct, float), Ts=float(rom.Ts),
                 A=np.asarray(rom.A, float), C=np.asarray(rom.C, float), D=np.asarray(rom.D, float),
                 tf_code=np.array([codes[nm] for nm in rom.names], np.int32), xloc=np.asarray(rom.xloc, float),
                 F=float(rom.F), R=float(rom.R), Q=float(rom.Q), Rc=float(rom.Rc), Tref=float(rom.Tref),
-                tab_T_K=np.atleast_1d(np.asarray(rom.tab_T_K, float)), neg=el(rom.neg), pos=el(rom.pos))
+                tab_T_K=np.atleast_1d(np.asarray(rom.tab_T_K, float)), neg=el_(rom.neg), pos=el_(rom.pos))

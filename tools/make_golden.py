@@ -168,8 +168,91 @@ def make_envelopes(rom, hsh):
                         ulps=ks9, kicked=NK_NEAR, **env)
 
 
+def _handle_cell(args):
+    soc0, tc, steps, cfg, tct = args
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    c = {"handles": True}
+    c.update(cfg or {})
+    o = O.run_cell(P.make_synth_rom(), soc0, tc, steps, c, tc_traj=tct)
+    return {k: o[k] for k in ("u", "v", "soc", "phise", "nexec", "status")}
+
+
+def make_handles():
+    """Handle-mode fixtures (round-4 review item 1): the restatement with the synthetic
+    ROM's closed-form cellData.function handles called at every reference call site
+    (oracle_np Cell(handles=True), rom.py SynthHandles), as MATLAB calls its handles --
+    not the tables.  The library's ABI v3 tables (make_synth_rom(lookup="quintic")) are
+    held to these within 1e-6 where the fixture is well-conditioned:
+      handles_runmpc_3001   the runMPC.m cell (10 %, 25 degC) x 3001 steps, with a
+                            handle-mode ulp ensemble (SOC0 -8..+8 ulps, 32 members with a
+                            1-ulp command kick per step, as make_envelopes): per-step min /
+                            max, so the test knows where one trajectory is followable;
+      handles_batch8_1000   the 8 batch cells (TC ~ U[20, 30] degC, Arrhenius k0 / Rf
+                            between table temperatures) x 1000 steps;
+      handles_tprofile4_300 the 4-cell temperature profile (per-step T) x 300 steps;
+      handles_mb4_200       the MB EKF, 4 cells x 200 steps."""
+    from multiprocessing import Pool
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    base = P.make_synth_rom()
+    hsh, qhsh = rom_hash(base), rom_hash(P.make_synth_rom(lookup="quintic"))
+    rng = np.random.Generator(np.random.PCG64(0x5EED))
+    soc0, tc = rng.uniform(5, 30, 8), rng.uniform(20, 30, 8)
+    rng4 = np.random.Generator(np.random.PCG64(0x5EED))
+    soc4, tc4 = rng4.uniform(5, 30, 4), rng4.uniform(20, 30, 4)
+    tsoc = np.array([10.0, 35.0, 20.0, 60.0])
+    tct = tprofile(300)
+    ks = list(range(-8, 9))
+    NK = 32
+    jobs = [(s, 25.0, 3001, None, None) for s in _ulp_members(10.0, ks)]
+    jobs += [(10.0, 25.0, 3001, {"ulp_kick": (3000 + i, 1)}, None) for i in range(NK)]
+    jobs += [(s, t, 1000, None, None) for s, t in zip(soc0, tc)]
+    jobs += [(s, float(tct[0, i]), 300, None, tct[:, i]) for i, s in enumerate(tsoc)]
+    jobs += [(s, t, 200, {"method": "MB"}, None) for s, t in zip(soc4, tc4)]
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        outs = pool.map(_handle_cell, jobs)
+    keys = ("u", "v", "soc", "phise", "nexec")
+    run, outs = outs[:len(ks) + NK], outs[len(ks) + NK:]
+    one = run[ks.index(0)]
+    env = {}
+    for k in ("u", "v", "soc", "phise"):
+        a = np.stack([o[k] for o in run], axis=1)
+        env[k + "_min"], env[k + "_max"] = a.min(1), a.max(1)
+    soc = np.stack([o["soc"] for o in run], axis=1)
+    env["t90"] = np.array([int(np.argmax(soc[:, j] >= 0.90)) if (soc[:, j] >= 0.90).any() else -1
+                           for j in range(soc.shape[1])])
+    # the followable window ends where the members part by more than 1e-6 on any output;
+    # beyond it (the chaotic tail) a trajectory is held in distribution: each member's
+    # window mean and 10th / 90th percentile (tests/envelope.py check_tail_stats)
+    wide = np.zeros(3001, dtype=bool)
+    for k in ("u", "v", "soc", "phise"):
+        lo, hi = env[k + "_min"], env[k + "_max"]
+        wide |= (hi - lo) > 1e-6 * np.maximum(np.abs(lo), np.abs(hi))
+    tail0 = int(np.argmax(wide)) if wide.any() else 3001
+    env["tail0"] = tail0
+    for k in ("u", "v", "soc", "phise"):
+        w = np.stack([o[k] for o in run], axis=1)[tail0:]
+        env[k + "_wmean"] = w.mean(0)
+        env[k + "_wlo"], env[k + "_whi"] = np.percentile(w, 10, axis=0), np.percentile(w, 90, axis=0)
+    np.savez_compressed(os.path.join(OUT, "handles_runmpc_3001.npz"), rom_hash=hsh, quintic_hash=qhsh, soc0=[10.0],
+                        tc=[25.0], status=np.array([one["status"][-1]]),
+                        **{k: one[k][:, None] for k in keys}, **env)
+    for name, n, s0, t0, extra in (("handles_batch8_1000", 8, soc0, tc, {}),
+                                   ("handles_tprofile4_300", 4, tsoc, tct[0], {"tc_traj": tct}),
+                                   ("handles_mb4_200", 4, soc4, tc4, {"method": "MB"})):
+        o, outs = outs[:n], outs[n:]
+        r = {k: np.stack([x[k] for x in o], axis=1) for k in keys}
+        r["status"] = np.array([x["status"][-1] for x in o])
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), rom_hash=hsh, quintic_hash=qhsh, soc0=s0, tc=t0,
+                            **extra, **r)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--handles-only" in sys.argv:
+        t0 = time.time()
+        make_handles()
+        print(f"handle-mode fixtures written in {time.time() - t0:.0f} s")
+        return
     if "--envelopes-only" in sys.argv:
         P = importlib.import_module("mpc-ekf4fastcharge_amd")
         rom = P.make_synth_rom()
@@ -228,6 +311,8 @@ def main():
     make_wide(rom, hsh)
     # 5d. ulp-ensemble envelopes of the chaotic tails (runMPC cell, Np = 20 near-limit cells)
     make_envelopes(rom, hsh)
+    # 5e. handle-mode fixtures (closed-form cellData.function handles, not tables)
+    make_handles()
     # 6. per-function vectors: predMat and hildreth (incl. the zero row of G_soc)
     rng = np.random.default_rng(11)
     n = 24
