@@ -39,7 +39,7 @@ METRIC = "MPC+EKF control steps/sec (whole batch), Np=5 Nc=2; 1/2/4/8 MI355X"
 LAZY_H = 64  # the library's input-ring length = flush period (mpcekf_kernels.hpp MPCEKF_LAZY_H)
 
 
-def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, bounds_kernel=False, plant_kernel=False,
+def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, bounds_kernel=True, plant_kernel=False,
                                hild_kernel=True):
     """Algorithmic HBM bytes each kernel moves per cell per launch:
     the state it must read and write once, with nothing re-read.
@@ -50,9 +50,10 @@ def algorithmic_bytes_per_cell(NM, ncon, bounds, lazy_h=LAZY_H, Np=5, Nc=2, boun
     cell : the 4 corner EKF records read + written, their timestamps, the step's
            ring input, per-cell scalars/constants, outputs u/v/soc/phise, zk,
            the QP record (+ the 14-double boundzk hand-off record).
-    bounds: (k_bounds, when launched) the hand-off record and corner 1's packed Sigma
-           read, 4 per-cell constants read, boundzk (28) written; by default k_cell
-           evaluates boundzk itself (corner 1's Sigma read, boundzk written, no record).
+    bounds: (k_bounds, the library default: MPCEKF_CELL_BOUNDS=0) the hand-off record and
+           corner 1's packed Sigma read, 4 per-cell constants read, boundzk (28) written;
+           with bounds_kernel=False k_cell evaluates boundzk itself (corner 1's Sigma
+           read, boundzk written, no record).
     plant: the 4 corner plant states read + written, timestamps, ring writes,
            per-cell scalars (k_cell's own bytes when it runs the plant, the default).
     hild : the QP record read, lambda read + written, outputs.
@@ -144,16 +145,68 @@ def cpu_baseline(rom, soc0, tc, cells, steps, threads, Np=5, Nc=2):
                           "what": "runMPC.m cell (SOC0 10 %, 25 degC), full charge, 1 thread"})
 
 
+def count_gpus(sysfs="/sys/class/kfd/kfd/topology/nodes", dev="/dev/dri", env=None):
+    """GPUs this process could open, counted without any HIP / HSA call and without torch:
+    the KFD topology nodes with SIMDs (GPU agents) whose render node /dev/dri/renderD<minor>
+    is accessible, then limited by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES (the runtime applies them in that order).  The rank launcher's
+    parent uses it so that it never maps a GPU runtime before it spawns the ranks."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        nodes = sorted(os.listdir(sysfs), key=lambda x: int(x) if x.isdigit() else 1 << 30)
+    except OSError:
+        nodes = []
+    for nd in nodes:
+        props = {}
+        try:
+            with open(os.path.join(sysfs, nd, "properties")) as f:
+                for line in f:
+                    kv = line.split()
+                    if len(kv) == 2 and kv[1].lstrip("-").isdigit():
+                        props[kv[0]] = int(kv[1])
+        except OSError:
+            continue
+        if props.get("simd_count", 0) <= 0:
+            continue                                  # a CPU agent
+        minor = props.get("drm_render_minor", -1)
+        node = os.path.join(dev, f"renderD{minor}")
+        if minor >= 0 and os.path.exists(node) and os.access(node, os.R_OK | os.W_OK):
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids))
+    return n
+
+
+def _parent_maps_gpu_runtime():
+    """Lines of /proc/self/maps naming a GPU runtime (HIP, HSA, torch's bundled ones)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return sorted({ln.split()[-1] for ln in f if any(k in ln for k in
+                           ("libamdhip64", "libhsa-runtime64", "libtorch_hip", "libtorch_cuda"))})
+    except OSError:
+        return []
+
+
 def launch_ranks(args):
     """--gpus N without torchrun: N worker processes, one per GPU, started before this
-    process touches the GPU; exits with the first failing rank's code."""
+    process touches the GPU (it counts devices from sysfs, count_gpus, and refuses to
+    spawn if a GPU runtime is mapped here); exits with the first failing rank's code."""
     import socket
     import subprocess
     if not (args.dry_run or args.share_device):
-        import torch
-        have = torch.cuda.device_count()  # does not initialise the GPU on this image
+        have = count_gpus()
         if have < args.gpus:
-            sys.exit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible")
+            sys.exit(f"bench.py: --gpus {args.gpus} but only {have} GPU(s) visible (KFD topology)")
+    mapped = _parent_maps_gpu_runtime()
+    if os.environ.get("MPCEKF_BENCH_PARENT_MAPS"):   # tests/test_multiproc.py
+        with open(os.environ["MPCEKF_BENCH_PARENT_MAPS"], "w") as f:
+            f.write("\n".join(mapped))
+    if mapped:
+        sys.exit(f"bench.py: the rank launcher has a GPU runtime mapped before spawning: {mapped}")
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -263,7 +316,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="default: the cores this process may use")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--timing-every", type=int, default=8,
-                    help="per-kernel HIP-event timing on every N-th step of the timed region (N | 32)")
+                    help="per-kernel HIP-event timing on every N-th step of the timed region (N divides "
+                         "the flush period, 64)")
     ap.add_argument("--pmc", default="",
                     help="PMC traffic JSON (tools/pmc_traffic.py); default profiles/pmc_traffic.json, "
                          "profiles/pmc_traffic_np20.json at Np = 20")
@@ -281,6 +335,11 @@ def main():
     if not args.pmc:
         args.pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json" if args.np == 5 else f"pmc_traffic_np{args.np}.json")
 
+    period = int(os.environ.get("MPCEKF_FLUSH_PERIOD", str(LAZY_H)))
+    if args.timing_every > 1 and period % args.timing_every:
+        # report() counts the timed k_flush launches as the region's flushes: every flush
+        # step must be a sampled step
+        sys.exit(f"bench.py: --timing-every {args.timing_every} must divide the flush period {period}")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         launch_ranks(args)
     rank = int(os.environ.get("RANK", "0"))
@@ -302,14 +361,19 @@ def main():
     runtimes = None
 
     if args.dry_run:
+        # the rank / shard / coordinator path without a GPU (tests/test_multiproc.py): each
+        # rank "works" (rank + 1) x 20 ms on its shard, and the reductions carry its cell
+        # count and a checksum of its SOC0 so the test can see max-over-ranks timing and
+        # shard coverage through the same collectives the GPU run uses
         rom = None
         soc0_all, tc_all = batch_inputs(total)
         if coord:
             coord.barrier()
         t0 = time.perf_counter()
-        _ = soc0_all[lo:hi].sum() + tc_all[lo:hi].sum()
+        time.sleep(0.02 * (rank + 1))
+        shard_sum = float(soc0_all[lo:hi].sum())
         dt = time.perf_counter() - t0
-        tim, nerr, mean_nexec, u_last = {}, 0, 0.0, np.zeros(0)
+        tim, nerr, mean_nexec, u_last = {}, ncell, shard_sum / max(ncell, 1), np.zeros(0)
     else:
         P = importlib.import_module("mpc-ekf4fastcharge_amd")
         M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
@@ -383,6 +447,8 @@ def main():
         if args.dry_run:
             line["dry_run"] = True
             line["value"] = None
+            # reduced over the ranks: the cells they covered and the sum of their SOC0
+            line["dry_run_checks"] = {"cells": nerr, "soc0_sum": mean_nexec * total, "max_dt_s": dt}
             print(json.dumps(line), flush=True)
         else:
             line.update(report(args, rom, tim, K, ncell, value, nerr, mean_nexec, u_last, build_id,

@@ -221,15 +221,25 @@ int mpcekf_cl_eig(int32_t n, const double *a, double *re, double *im, double *sv
  * degC, [ncells]) sets each cell's temperature for this and later calls; NULL keeps it. */
 /* OB_step: applies iapp[c] to the plant state at tc_degC[c], returns vcell[c]. */
 int mpcekf_plant_step(mpcekf_ctx *ctx, const double *iapp, const double *tc_degC, double *vcell);
-/* iterEKF: zk/boundzk [ncells][nz+2] (boundzk may be NULL), xind_model [ncells][4]
- * (model index t*nZ+z of Xind.theT/theZ), xind_gamma [ncells][4]. */
+/* iterEKF: zk/boundzk [ncells][nz+2], xind_model [ncells][4] (model index t*nZ+z of
+ * Xind.theT/theZ), xind_gamma [ncells][4].  Every output may be NULL: zk and Xind also stay
+ * on the device for the next mpcekf_linearize (runMPC.m:91 -> :94 without a host round trip). */
 int mpcekf_ekf_step(mpcekf_ctx *ctx, const double *vk, const double *ik, const double *tk_degC, double *zk,
                     double *boundzk, int32_t *xind_model, double *xind_gamma);
-/* EKFmatsHandler: lin [ncells][MPCEKF_LIN_SIZE]. */
+/* EKFmatsHandler: lin [ncells][MPCEKF_LIN_SIZE], or NULL (the record stays on the device for
+ * mpcekf_mpc_step / mpcekf_mpc_diag with lin = NULL and mpcekf_lin_fields).  zk, xind_model and
+ * xind_gamma are all given, or all NULL for the device copies of the last mpcekf_ekf_step
+ * (MPCEKF_E_STATE if there was none since init / the last fused step / set_state). */
 int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_model, const double *xind_gamma,
                      const double *tk_degC, double *lin);
+/* Selected slots (MPCEKF_LIN_*) of the device-resident linearisation records of the last
+ * mpcekf_linearize: out [ncells][nslots] (may be NULL), and set [ncells][nslots] (may be NULL)
+ * written into those slots first -- e.g. runMPC.m:95-96 reads MPC.Cphi / Dphi / bphi and xhat
+ * (14 doubles of the 35), and an iterMPC caller with another xk writes MPCEKF_LIN_XHAT.. */
+int mpcekf_lin_fields(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, const double *set, double *out);
 /* iterMPC (uses and updates the context's uk_1 and lambda warm start):
- * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec. */
+ * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec.  lin = NULL: the device-resident
+ * record of the last mpcekf_linearize. */
 int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
 /* The same, also returning this call's iterMPC.m:89-95 cost log (mpcData.cost.J_uncon,
  * J_final, norm_DU, viol) per cell; any of the four may be NULL. */
@@ -239,7 +249,8 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *ctx, const double *lin, const double *soc_k1,
  * Kmpc = first row of E\(G_soc'*Phi_soc), CL = Abar - Bbar*Kmpc; poles [ncells][7][2]
  * (eig(CL): re, im, sorted as in mpcekf_traj), sv [ncells][7] (svd(CL)).  uk_1 [ncells]
  * (mpcData.uk_1) or NULL for the context's current one (call before mpcekf_mpc_step).
- * Reads nothing else of the context's state and changes none of it. */
+ * Reads nothing else of the context's state and changes none of it.  lin = NULL: the
+ * device-resident record of the last mpcekf_linearize. */
 int mpcekf_mpc_diag(mpcekf_ctx *ctx, const double *lin, const double *uk_1, double *poles, double *sv);
 
 /* Context-free batched kernels (device chosen by `device`).
@@ -298,8 +309,10 @@ int mpcekf_get_timing(mpcekf_ctx *ctx, double *ms_sum, int64_t *launches);
 int mpcekf_get_hild_problems(mpcekf_ctx *ctx, double *prob, int32_t *hflag);
 /* Profiling builds only (-DMPCEKF_STAMPS, tools/stamps.py): shader-clock stamps at the
  * section boundaries of the EKF/MPC kernel (rows 0..11) and the plant kernel (rows
- * 12..19) for the last fused step, [MPCEKF_NSTAMPS][ncells].  *nstamps = 0 (and nothing
- * written) in normal builds. */
+ * 12..19) for the last fused step, [MPCEKF_NSTAMPS][ncells].  Rows 12..19 are written
+ * only when the plant runs as its own kernel (k_plant4: MPCEKF_CELL_PLANT=0 or the
+ * lane-quad path); when it runs inside k_cell (the default) they read 0.  *nstamps = 0
+ * (and nothing written) in normal builds.  ABI v3: 20 rows (v2 had 12). */
 #define MPCEKF_NSTAMPS 20
 int mpcekf_get_stamps(mpcekf_ctx *ctx, int64_t *stamps, int32_t *nstamps);
 

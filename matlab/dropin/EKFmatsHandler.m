@@ -1,15 +1,22 @@
 function [MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)
-% Drop-in for EKFmatsHandler.m:1 over the MI355X library (mpcekf_linearize).  MPC holds
-% the first cell's matrices in the reference's shapes plus MPC.lin, the 35 x ncells
-% linearisation records (include/mpcekf.h MPCEKF_LIN_*) iterMPC hands back to the
-% library; xhat is 6 x ncells.
+% Drop-in for EKFmatsHandler.m:1 over the MI355X library (mpcekf_linearize).  The 35 x
+% ncells linearisation records (include/mpcekf.h MPCEKF_LIN_*) stay on the device for
+% iterMPC (MPC.lin = [], MPC.tick names them); MPC carries what runMPC.m:95-96 reads,
+% Cphi / Dphi / bphi (one row / value per cell), and xhat is 6 x ncells: 14 doubles per
+% cell cross PCIe (mpcekf_lin_fields).  When Xind or zk are not the last iterEKF's as it
+% returned them, they are passed to the library (the reference's semantics either way).
   S = mpcekf_session('get');
   n = size(zk, 2);
-  lin = mpcekf_mex('linearize', S.h, zk, Xind.model, Xind.gamma, reshape(Tk .* ones(1, n), 1, n));
-  MPC = struct('A', diag(lin(1:6, 1)), 'B', ones(6, 1), 'Csoc', lin(7:12, 1)', 'Dsoc', lin(13, 1), ...
-               'Cv', lin(14:19, 1)', 'Dv', lin(20, 1), 'Cphi', lin(21:26, 1)', 'Dphi', lin(27, 1), ...
-               'bv', lin(28, 1), 'bphi', lin(29, 1), 'lin', lin);
+  tk = reshape(Tk .* ones(1, n), 1, n);
+  if isfield(Xind, 'tick') && Xind.tick == S.ekf_tick && isequal(zk, S.zk_last)
+    mpcekf_mex('linearize', S.h, [], [], [], tk);            % the device copies of zk and Xind
+  else
+    mpcekf_mex('linearize', S.h, zk, Xind.model, Xind.gamma, tk);
+  end
+  f = mpcekf_mex('linfields', S.h, [21:27, 29, 30:35]);      % Cphi (6), Dphi, bphi, xhat (6)
+  MPC = struct('Cphi', f(1:6, :)', 'Dphi', f(7, :), 'bphi', f(8, :), 'lin', [], 'tick', Xind.tick);
   [~, imax] = max(Xind.gamma(:, 1));
   MPC.iT = Xind.theT(imax, 1);  MPC.iZ = Xind.theZ(imax, 1);  MPC.pickWeight = Xind.gamma(imax, 1);
-  xhat = lin(30:35, :);
+  xhat = f(9:14, :);
+  MPC.xhat = xhat;
 end

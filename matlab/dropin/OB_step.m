@@ -16,9 +16,10 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
     cfg.SigmaV = S.kf.SigmaV;  cfg.SigmaW = S.kf.SigmaW;  cfg.SigmaX0 = S.kf.SigmaX0;
     cfg.flags = 1;                                         % MPCEKF_CF_BOUNDS: boundzk too
     if strcmp(S.kf.method, 'MB'), cfg.method = 1; end
-    % the electrode tables hold the ROM set-points and the span of Tc (a per-cell Tc of
-    % thousands of distinct values must not each become a table temperature)
-    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], [min(Tc(:)), max(Tc(:))]), cfg, S.device, n);
+    % the electrode tables hold the ROM set-points and the distinct Tc (mpcekf_rom_struct
+    % keeps only their span when they do not fit its 8 table temperatures, e.g. a per-cell
+    % Tc of thousands of distinct values)
+    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], unique(Tc(:)')), cfg, S.device, n);
     mpcekf_session('set', 'h', h);
     mpcekf_mex('init', h, reshape(initCfg.SOC0, 1, n), Tc .* ones(1, n));
     fn = ROM.cellData.function.neg;

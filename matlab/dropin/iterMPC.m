@@ -1,15 +1,27 @@
 function [uk, mpcData] = iterMPC(xk, cellState, mpcData)
 % Drop-in for iterMPC.m:1 over the MI355X library (mpcekf_mpc_step_ex): the linearisation
-% is cellState.MPC.lin (EKFmatsHandler's records), with its xhat rows replaced by the
-% caller's xk (6 x ncells, the state iterMPC.m:29 augments); uk_1 and the Hildreth warm
-% start live in the context.  When runMPC.m has set mpcData.k, row k of mpcData.cost
-% (iterMPC.m:89-95: t, J_uncon, J_final, norm_DU, viol, nexec) is filled, one column
-% per cell.
+% is EKFmatsHandler's device-resident records (cellState.MPC.lin empty) or, when a caller
+% built cellState.MPC.lin itself, those 35 x ncells records; their xhat rows are the
+% caller's xk (6 x ncells, the state iterMPC.m:29 augments) -- written to the device only
+% when xk is not the xhat EKFmatsHandler returned.  uk_1 and the Hildreth warm start live
+% in the context.  When runMPC.m has set mpcData.k, row k of mpcData.cost
+% (iterMPC.m:89-95: t, J_uncon, J_final, norm_DU, viol, nexec) is filled, one column per
+% cell.
   S = mpcekf_session('get');
   lin = cellState.MPC.lin;
-  n = size(lin, 2);
-  if ~isempty(xk)
-    lin(30:35, :) = reshape(xk, 6, []) .* ones(1, n);        % MPCEKF_LIN_XHAT
+  if isempty(lin)
+    n = size(cellState.MPC.xhat, 2);
+    if ~isempty(xk)
+      xk = reshape(xk, 6, []) .* ones(1, n);
+      if ~isequal(xk, cellState.MPC.xhat)
+        mpcekf_mex('linfields', S.h, 30:35, xk);              % MPCEKF_LIN_XHAT
+      end
+    end
+  else
+    n = size(lin, 2);
+    if ~isempty(xk)
+      lin(30:35, :) = reshape(xk, 6, []) .* ones(1, n);      % MPCEKF_LIN_XHAT
+    end
   end
   % iterMPC.m:53-60 stability analysis (before the solve: it uses this step's uk_1)
   [mpcData.poles, mpcData.sv] = mpcekf_mex('mpcdiag', S.h, lin, []);

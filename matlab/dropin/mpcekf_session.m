@@ -5,7 +5,9 @@ function S = mpcekf_session(op, name, value)
 % the context is created from on the first OB_step call.
 %   S = mpcekf_session('get');  mpcekf_session('set', name, value);  mpcekf_session('reset')
   persistent P
-  if isempty(P), P = struct('h', [], 'kf', [], 'mpc', [], 'device', 0); end
+  % zk_last / ekf_tick: the zk the last iterEKF returned and a counter of iterEKF calls, so
+  % EKFmatsHandler knows when the library's device copies of zk and Xind are the caller's
+  if isempty(P), P = struct('h', [], 'kf', [], 'mpc', [], 'device', 0, 'zk_last', [], 'ekf_tick', 0); end
   switch op
     case 'set'
       P.(name) = value;

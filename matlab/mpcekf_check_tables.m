@@ -1,34 +1,72 @@
-function err = mpcekf_check_tables(f, e, th, TK)
-% MPCEKF_CHECK_TABLES  Max abs error of the library's bilinear (theta, T) tables against
-% the original cellData.function handles, at 997 interior theta points and at every
-% table temperature and the midpoints between them, plus the deviation of soc(z,T) from
-% the linear-in-z form the library assumes.  The library reproduces the tables
-% bit-for-bit; this is the tabulation part of any real-MATLAB parity gap.
-  x = linspace(0.001, 0.999, 997);
+function [err, ok] = mpcekf_check_tables(f, e, th, TK, Tref, R, thlim)
+% MPCEKF_CHECK_TABLES  Largest difference of the library's lookups (include/mpcekf.h: v2
+% bilinear tables, or the ABI v3 theta polynomials with the Arrhenius factor when e has
+% a poly field) from the original cellData.function handles, at 997 theta points in
+% thlim (default [0.001, 0.999]) and at every table temperature and the midpoints
+% between them, plus the deviation of soc(z,T) from the linear-in-z form the library
+% assumes.  The library reproduces the lookups bit-for-bit, so this is the tabulation
+% part of any real-MATLAB parity gap.  ok: every error within the budget (rom.py
+% TABLE_BUDGET; a tenth of north_star's 1e-6 relative on phise ~ 0.08 V, into which
+% Uocp_n enters directly, EKFmatsHandler.m:96).  The same measure as rom.py table_errors.
+  if nargin < 5 || isempty(Tref), Tref = 298.15; end
+  if nargin < 6 || isempty(R), R = 8.3144621; end
+  if nargin < 7 || isempty(thlim), thlim = [0.001, 0.999]; end
+  x = linspace(thlim(1), thlim(2), 997);
   Ts = sort([TK, (TK(1:end-1) + TK(2:end)) / 2]);
-  tab = @(t2, xx, T) bilin(reshape(t2.data, t2.shape), th, TK, xx, T);
-  err = struct('Uocp', 0, 'dUocp', 0, 'k0_rel', 0, 'Rf_rel', 0, 'Cdleff_rel', 0, 'soc_lin', 0);
+  budget = struct('Uocp', 8e-9, 'dUocp_rel', 1e-7, 'k0_rel', 1e-9, 'Rf_rel', 1e-9, 'Cdleff_rel', 1e-3, 'soc_lin', 1e-12);
+  err = struct('Uocp', 0, 'dUocp_rel', 0, 'k0_rel', 0, 'Rf_rel', 0, 'Cdleff_rel', 0, 'soc_lin', 0);
   nDL = f.nDL();
   for T = Ts
-    err.Uocp = max(err.Uocp, max(abs(arrayfun(@(t) f.Uocp(t, T), x) - tab(e.Uocp, x, T))));
-    err.dUocp = max(err.dUocp, max(abs(arrayfun(@(t) f.dUocp(t, T), x) - tab(e.dUocp, x, T))));
+    err.Uocp = max(err.Uocp, max(abs(arrayfun(@(t) f.Uocp(t, T), x) - look(e, 'Uocp', 1, th, TK, x, T, Tref, R))));
+    d = arrayfun(@(t) f.dUocp(t, T), x);
+    err.dUocp_rel = max(err.dUocp_rel, max(abs(d - look(e, 'dUocp', 2, th, TK, x, T, Tref, R)) ./ max(abs(d), eps)));
     k = arrayfun(@(t) f.k0(t, T), x);
-    err.k0_rel = max(err.k0_rel, max(abs(k - tab(e.k0, x, T)) ./ abs(k)));
+    err.k0_rel = max(err.k0_rel, max(abs(k - look(e, 'k0', 3, th, TK, x, T, Tref, R)) ./ abs(k)));
     r = arrayfun(@(t) f.Rf(t, T), x);
-    err.Rf_rel = max(err.Rf_rel, max(abs(r - tab(e.Rf, x, T)) ./ max(abs(r), eps)));
+    err.Rf_rel = max(err.Rf_rel, max(abs(r - look(e, 'Rf', 4, th, TK, x, T, Tref, R)) ./ max(abs(r), eps)));
     c = arrayfun(@(t) f.Cdl(t, T)^(2 - nDL) * f.wDL(t, T)^(nDL - 1), x);
-    err.Cdleff_rel = max(err.Cdleff_rel, max(abs(c - tab(e.Cdleff, x, T)) ./ abs(c)));
+    err.Cdleff_rel = max(err.Cdleff_rel, max(abs(c - look(e, 'Cdleff', 5, th, TK, x, T, Tref, R)) ./ abs(c)));
     s0 = f.soc(0, T);  s1 = f.soc(1, T);
     err.soc_lin = max(err.soc_lin, max(abs(arrayfun(@(z) f.soc(z, T), x) - (s0 + x * (s1 - s0)))));
   end
+  ok = true;
+  for k = fieldnames(budget)'
+    ok = ok && err.(k{1}) <= budget.(k{1});
+  end
 end
 
-function v = bilin(t2, th, TK, x, T)
-  % the library's evaluation order (include/mpcekf.h): theta rows first, then T
-  rows = interp1(th, t2.', min(max(x, 0), 1), 'linear').';   % [ntemp, numel(x)]
-  if numel(TK) == 1, v = rows; return; end
-  Tc = min(max(T, TK(1)), TK(end));
-  j = find(TK <= Tc, 1, 'last');  j = min(j, numel(TK) - 1);
-  g = (Tc - TK(j)) / (TK(j + 1) - TK(j));
-  v = rows(j, :) + g * (rows(j + 1, :) - rows(j, :));
+function v = look(e, name, fk, th, TK, x, T, Tref, R)
+  % the library's evaluation (include/mpcekf.h): theta rows, then T (clamped), then the
+  % Arrhenius factor with the unclamped T
+  t2 = e.(name);
+  if isfield(t2, 'shape'), t2 = reshape(t2.data, t2.shape); end
+  nth = numel(th);
+  if isfield(e, 'poly') && ~isempty(e.poly)
+    P = e.poly.(name);
+    if isfield(P, 'shape'), P = reshape(P.data, P.shape); end
+    xc = min(max(x, 0), 1);
+    tt = xc * (nth - 1);
+    i = min(floor(tt), nth - 2);
+    s = tt - i;
+    rows = zeros(numel(TK), numel(x));
+    for j = 1:numel(TK)
+      c = reshape(P(j, i + 1, :), numel(x), []).';   % (order+1) x numel(x)
+      acc = c(end, :);
+      for q = size(c, 1) - 1:-1:1, acc = c(q, :) + s .* acc; end
+      rows(j, :) = acc;
+    end
+  else
+    rows = interp1(th, t2.', min(max(x, 0), 1), 'linear').';   % [ntemp, numel(x)]
+  end
+  if numel(TK) == 1
+    v = rows;
+  else
+    Tc = min(max(T, TK(1)), TK(end));
+    j = find(TK <= Tc, 1, 'last');  j = min(j, numel(TK) - 1);
+    g = (Tc - TK(j)) / (TK(j + 1) - TK(j));
+    v = rows(j, :) + g * (rows(j + 1, :) - rows(j, :));
+  end
+  if isfield(e, 'Ea') && ~isempty(e.Ea) && e.Ea(fk) ~= 0
+    v = v * exp((e.Ea(fk) / R) * (1 / Tref - 1 / T));
+  end
 end

@@ -1,9 +1,18 @@
-function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
+function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC, order)
 % MPCEKF_EXPORT_ROM  Tabulate a reference ROM (.mat) into the JSON file the MI355X
-% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py, format v2).
+% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py, format v3; v2 with
+% order = 1).
 %
-%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json')          % 101 x 6 tables
-%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json', 201, [15 25 35])
+%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json')          % quintics, ntheta by budget
+%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json', 1025, [15 25 35])
+%   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30_v2.json', 101, [], 1)   % v2 linear
+%
+% ABI v3 (order 5, the default; include/mpcekf.h tab_npoly): every row is also a
+% piecewise Hermite quintic in theta fitted to the handle's values and derivatives, and a
+% handle of Arrhenius form gets its exact factor (mpcekf_tabulate_electrode).  Without an
+% explicit ntheta the exporter starts at 257 theta points and doubles them until
+% mpcekf_check_tables' budget holds (a tenth of north_star's 1e-6 on phise and V); it
+% refuses to write a file whose tables miss the budget at 4097 points.
 %
 % Runs on a machine with MATLAB and the reference's ROM file (runMPC.m:4-5; the file
 % is listed in .MISSING_LARGE_BLOBS:1 and is not in this repository).  Every
@@ -22,22 +31,38 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
 % The library evaluates the tables with a defined bilinear interpolation (theta, then
 % T; both clamped to the grid).  mpcekf_check_tables reports how far that is from the
 % handles between the grid points: the part of a real-MATLAB parity gap that comes from
-% tabulation rather than the kernels.  LDS budget: the kernels stage 4 (plant: 5) of
-% the tables per electrode next to the ROM models, so ntheta x ntemp is bounded
-% (mpcekf_ctx_create fails with MPCEKF_E_UNSUPPORTED when they do not fit 160 KiB).
+% tabulation rather than the kernels.  LDS budget (v2 only): the kernels stage 4
+% (plant: 5) of the tables per electrode next to the ROM models, so ntheta x ntemp is
+% bounded (mpcekf_ctx_create fails with MPCEKF_E_UNSUPPORTED when they do not fit
+% 160 KiB); the v3 polynomials are read from a global (L2-resident) table of any size.
 %
 % Every array is written as {"shape": size(X), "order": "F", "data": X(:)'} so the
 % loader needs no knowledge of MATLAB's N-D jsonencode nesting.
   if nargin < 3, ntheta = []; end
   if nargin < 4, TdegC = []; end
+  if nargin < 5 || isempty(order), order = 5; end
   S = load(matFile);
   if isfield(S, 'ROM'), ROM = S.ROM; else, f = fieldnames(S); ROM = S.(f{1}); end
-  R = mpcekf_rom_struct(ROM, ntheta, TdegC);
   fn = ROM.cellData.function;
+  if order > 1 && isempty(ntheta)
+    % the operating theta range of each electrode (0-100 % SOC, widened by 0.04)
+    lim = @(g) [max(0, min(g.soc(0, 298.15), g.soc(1, 298.15)) - 0.04), min(1, max(g.soc(0, 298.15), g.soc(1, 298.15)) + 0.04)];
+    for ntheta = [257, 513, 1025, 2049, 4097]
+      R = mpcekf_rom_struct(ROM, ntheta, TdegC, [], order);
+      th = linspace(0, 1, ntheta);
+      [en, okn] = mpcekf_check_tables(fn.neg, R.neg, th, R.tab_T_K, R.Tref, R.R, lim(fn.neg));
+      [ep, okp] = mpcekf_check_tables(fn.pos, R.pos, th, R.tab_T_K, R.Tref, R.R, lim(fn.pos));
+      if okn && okp, break; end
+    end
+    assert(okn && okp, 'mpcekf_export_rom: the tables miss the error budget at %d theta points', ntheta);
+  else
+    R = mpcekf_rom_struct(ROM, ntheta, TdegC, [], order);
+  end
   th = linspace(0, 1, size(R.neg.Uocp, 2));
 
   out = struct();
   out.format = 'mpcekf-rom-v2';
+  if order > 1, out.format = 'mpcekf-rom-v3'; end
   out.source = matFile;
   out.T_degC = arr(R.T_degC);
   out.SOC_pct = arr(R.SOC_pct);
@@ -49,8 +74,8 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC)
   out.tab_T_K = arr(R.tab_T_K);
   out.neg = jsonify(R.neg);
   out.pos = jsonify(R.pos);
-  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, out.neg, th, R.tab_T_K), ...
-                         'pos', mpcekf_check_tables(fn.pos, out.pos, th, R.tab_T_K));
+  out.tab_error = struct('neg', mpcekf_check_tables(fn.neg, R.neg, th, R.tab_T_K, R.Tref, R.R), ...
+                         'pos', mpcekf_check_tables(fn.pos, R.pos, th, R.tab_T_K, R.Tref, R.R));
 
   fid = fopen(jsonFile, 'w');
   assert(fid > 0, 'mpcekf_export_rom: cannot open %s', jsonFile);
@@ -64,6 +89,17 @@ function e = jsonify(t)
   e.soc0 = arr(t.soc0);  e.soc100 = arr(t.soc100);
   e.Uocp = arr(t.Uocp);  e.dUocp = arr(t.dUocp);  e.k0 = arr(t.k0);  e.Rf = arr(t.Rf);
   e.Cdleff = arr(t.Cdleff);  e.Uocp1 = arr(t.Uocp1);
+  if isfield(t, 'poly')   % v3: {"poly": {"Uocp": {shape, order, data}, ...}, "Ea": {"k0": J/mol, ...}}
+    e.poly = struct();
+    for k = fieldnames(t.poly)'
+      e.poly.(k{1}) = arr(t.poly.(k{1}));
+    end
+    names = {'Uocp', 'dUocp', 'k0', 'Rf', 'Cdleff'};
+    e.Ea = struct();
+    for k = 1:5
+      if t.Ea(k) ~= 0, e.Ea.(names{k}) = t.Ea(k); end
+    end
+  end
 end
 
 function a = arr(X)

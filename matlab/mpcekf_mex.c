@@ -250,6 +250,7 @@ static void need(int nrhs, int k, const char *usage) {
   if (nrhs < k) mexErrMsgIdAndTxt("mpcekf:arg", "usage: mpcekf_mex(%s)", usage);
 }
 
+static int g_nlhs = 1; /* the caller's nargout: 'ekf' copies Xind back only when it is asked for */
 static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   char cmd[32];
   if (nrhs < 1 || mxGetString(prhs[0], cmd, sizeof cmd)) mexErrMsgIdAndTxt("mpcekf:arg", "first argument: command");
@@ -303,7 +304,7 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     return;
   }
   static const char *const with_handle[] = {"destroy", "init", "step", "plant", "ekf", "linearize", "mpc",
-                                            "graph", "mpcdiag", "get_state", "set_state", "scalars"};
+                                            "graph", "mpcdiag", "get_state", "set_state", "scalars", "linfields"};
   int known = 0;
   for (size_t i = 0; i < sizeof with_handle / sizeof *with_handle; ++i) known = known || !strcmp(cmd, with_handle[i]);
   if (!known) mexErrMsgIdAndTxt("mpcekf:arg", "unknown command %s", cmd);
@@ -337,25 +338,35 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
                           mxGetDoubles(plhs[0])));
   } else if (!strcmp(cmd, "ekf")) {
     need(nrhs, 4, "'ekf', h, vk, ik[, tk]");
+    /* [zk, zbk, xm, xg]: Xind crosses back only when asked for (nargout > 2); it stays on
+       the device for 'linearize' with empty zk / xm / xg either way */
+    const int want_x = g_nlhs > 2;
     plhs[0] = dmat(nzz, nc);
     plhs[1] = dmat(nzz, nc);
-    plhs[2] = imat(4, nc);
-    plhs[3] = dmat(4, nc);
+    plhs[2] = want_x ? imat(4, nc) : mxCreateDoubleMatrix(0, 0, mxREAL);
+    plhs[3] = want_x ? dmat(4, nc) : mxCreateDoubleMatrix(0, 0, mxREAL);
     chk(mpcekf_ekf_step(h, dvec(prhs[2], nc, "vk"), dvec(prhs[3], nc, "ik"),
                         nrhs > 4 ? opt_vec(prhs[4], nc, "tk") : NULL, mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]),
-                        (int32_t *)mxGetData(plhs[2]), mxGetDoubles(plhs[3])));
+                        want_x ? (int32_t *)mxGetData(plhs[2]) : NULL, want_x ? mxGetDoubles(plhs[3]) : NULL));
   } else if (!strcmp(cmd, "linearize")) {
     need(nrhs, 5, "'linearize', h, zk, xm, xg[, tk]");
-    plhs[0] = dmat(MPCEKF_LIN_SIZE, nc);
-    chk(mpcekf_linearize(h, dvec(prhs[2], nzz * nc, "zk"), ivec(prhs[3], 4 * nc, "xm (4 x ncells)"),
-                         dvec(prhs[4], 4 * nc, "xg"), nrhs > 5 ? opt_vec(prhs[5], nc, "tk") : NULL,
-                         mxGetDoubles(plhs[0])));
+    /* empty zk, xm, xg: the device copies of the last 'ekf'; the records stay on the device
+       (plhs[0] empty) for 'mpc' / 'mpcdiag' with an empty lin and for 'linfields' */
+    const double *tk = nrhs > 5 ? opt_vec(prhs[5], nc, "tk") : NULL;
+    if (mxIsEmpty(prhs[2]) && mxIsEmpty(prhs[3]) && mxIsEmpty(prhs[4])) {
+      plhs[0] = mxCreateDoubleMatrix(0, 0, mxREAL);
+      chk(mpcekf_linearize(h, NULL, NULL, NULL, tk, NULL));
+    } else {
+      plhs[0] = dmat(MPCEKF_LIN_SIZE, nc);
+      chk(mpcekf_linearize(h, dvec(prhs[2], nzz * nc, "zk"), ivec(prhs[3], 4 * nc, "xm (4 x ncells)"),
+                           dvec(prhs[4], 4 * nc, "xg"), tk, mxGetDoubles(plhs[0])));
+    }
   } else if (!strcmp(cmd, "mpc")) {
     need(nrhs, 4, "'mpc', h, lin, soc_k1");
     /* [uk, nexec, J_uncon, J_final, norm_DU, viol]: iterMPC.m's command and its
        mpcData.cost row (iterMPC.m:89-95), 1 x ncells each */
     for (int i = 0; i < 6; ++i) plhs[i] = (i == 1 || i == 5) ? imat(1, nc) : dmat(1, nc);
-    chk(mpcekf_mpc_step_ex(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
+    chk(mpcekf_mpc_step_ex(h, opt_vec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), dvec(prhs[3], nc, "soc_k1"),
                            mxGetDoubles(plhs[0]), (int32_t *)mxGetData(plhs[1]), mxGetDoubles(plhs[2]),
                            mxGetDoubles(plhs[3]), mxGetDoubles(plhs[4]), (int32_t *)mxGetData(plhs[5])));
   } else if (!strcmp(cmd, "graph")) {
@@ -365,7 +376,7 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
     need(nrhs, 3, "'mpcdiag', h, lin[, uk_1]");
     plhs[0] = mxCreateDoubleMatrix(7, (mwSize)nc, mxCOMPLEX);  /* interleaved (re, im): [ncells][7][2] */
     plhs[1] = dmat(7, nc);
-    chk(mpcekf_mpc_diag(h, dvec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), nrhs > 3 ? opt_vec(prhs[3], nc, "uk_1") : NULL,
+    chk(mpcekf_mpc_diag(h, opt_vec(prhs[2], MPCEKF_LIN_SIZE * nc, "lin"), nrhs > 3 ? opt_vec(prhs[3], nc, "uk_1") : NULL,
                         (double *)mxGetComplexDoubles(plhs[0]), mxGetDoubles(plhs[1])));
   } else if (!strcmp(cmd, "get_state") || !strcmp(cmd, "set_state")) {
     /* the model-blend EKF state (xhat, SigmaX 6 x 6) is part of an MB context's checkpoint */
@@ -401,6 +412,23 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
       if (nf == 7 && mxGetField(s, 0, "mb")) st.mb = (double *)dvec(mxGetField(s, 0, "mb"), rows[6] * nc, "mb (MB context)");
       chk(mpcekf_set_state(h, &st));
     }
+  } else if (!strcmp(cmd, "linfields")) {
+    /* out = mpcekf_mex('linfields', h, idx[, set]): rows idx (1-based MPCEKF_LIN_* + 1) of
+       the device-resident records of the last 'linearize' with empty zk, k x ncells; set
+       (k x ncells) is written into them first */
+    need(nrhs, 3, "'linfields', h, idx[, set]");
+    const size_t k = mxGetNumberOfElements(prhs[2]);
+    if (k < 1 || k > MPCEKF_LIN_SIZE) mexErrMsgIdAndTxt("mpcekf:arg", "linfields: 1..%d slot indices", MPCEKF_LIN_SIZE);
+    const double *idx = dvec(prhs[2], k, "idx");
+    int32_t slots[MPCEKF_LIN_SIZE];
+    for (size_t j = 0; j < k; ++j) {
+      if (!(idx[j] >= 1 && idx[j] <= MPCEKF_LIN_SIZE) || idx[j] != (double)(int)idx[j])
+        mexErrMsgIdAndTxt("mpcekf:arg", "linfields: idx(%zu) = %g is not a slot 1..%d", j + 1, idx[j], MPCEKF_LIN_SIZE);
+      slots[j] = (int32_t)idx[j] - 1;
+    }
+    plhs[0] = dmat(k, nc);
+    chk(mpcekf_lin_fields(h, slots, (int32_t)k, nrhs > 3 ? opt_vec(prhs[3], k * nc, "set (k x ncells)") : NULL,
+                          mxGetDoubles(plhs[0])));
   } else if (!strcmp(cmd, "scalars")) {
     need(nrhs, 3, "'scalars', h, idx");
     const size_t k = mxGetNumberOfElements(prhs[2]);
@@ -424,6 +452,7 @@ static void gateway(mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
 
 void mexFunction(int nlhs, mxArray *plhs[], int nrhs, const mxArray *prhs[]) {
   mxArray *out[MAXOUT] = {0};
+  g_nlhs = nlhs;
   gateway(out, nrhs, prhs);
   const int keep = nlhs < 1 ? 1 : nlhs;
   if (keep > MAXOUT) mexErrMsgIdAndTxt("mpcekf:arg", "too many outputs");

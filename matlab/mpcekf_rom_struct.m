@@ -1,4 +1,4 @@
-function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC)
+function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC, order)
 % MPCEKF_ROM_STRUCT  The reference ROM struct (runMPC.m:5) as the plain arrays of the
 % library's mpcekf_rom (include/mpcekf.h): what mpcekf_mex('create', R, ...) takes and
 % what mpcekf_export_rom writes to JSON.
@@ -8,9 +8,15 @@ function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC)
 % the simulation temperatures TC (default 25 degC, runMPC.m:8) and guard points 10 degC
 % beyond the coldest / warmest (T is clamped to the table range); spare slots up to 8
 % split the widest intervals.
-% Between table points an Arrhenius k0 interpolated linearly is off by about
-% h^2/8 (Ea/(R T^2))^2 (DESIGN.md 3: ~1.4 % at h = 5 K, Ea = 50 kJ/mol).
-  if nargin < 2 || isempty(ntheta), ntheta = 101; end
+% order (ABI v3, default 5): the rows are also fitted by Hermite quintics (3: cubics) in
+% theta and Arrhenius handles get their exact factor (mpcekf_tabulate_electrode): an OCP
+% U0(th) + (T - Tref) dU/dT(th) is then exact between table temperatures and k0 / Rf at
+% any T; default ntheta 513 (mpcekf_export_rom raises it until mpcekf_check_tables'
+% budget holds).  order 1: the v2 linear tables (default ntheta 101), where an Arrhenius
+% k0 interpolated linearly in T is off by about h^2/8 (Ea/(R T^2))^2 between table
+% points (DESIGN.md 3: ~1.4 % at h = 5 K, Ea = 50 kJ/mol).
+  if nargin < 5 || isempty(order), order = 5; end
+  if nargin < 2 || isempty(ntheta), ntheta = 101 + 412 * (order > 1); end
   if nargin < 4 || isempty(TC), TC = 25; end
   if nargin < 3 || isempty(TdegC)
     Ts = ROM.xraData.T(:)';
@@ -46,6 +52,6 @@ function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC)
   R.names = names;  R.tf_code = int32(code - 1);  R.xloc = xloc(:)';
   R.F = cd.const.F;  R.R = cd.const.R;  R.Q = fn.const.Q();  R.Rc = fn.const.Rc();  R.Tref = 298.15;
   R.tab_T_K = TK;
-  R.neg = mpcekf_tabulate_electrode(fn.neg, th, TK);
-  R.pos = mpcekf_tabulate_electrode(fn.pos, th, TK);
+  R.neg = mpcekf_tabulate_electrode(fn.neg, th, TK, order, R.Tref, R.R);
+  R.pos = mpcekf_tabulate_electrode(fn.pos, th, TK, order, R.Tref, R.R);
 end

@@ -79,7 +79,7 @@ EXPORTS = [
     "mpcekf_set_timing", "mpcekf_get_timing", "mpcekf_get_hild_problems", "mpcekf_get_stamps", "mpcekf_hildreth_structured",
     "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag", "mpcekf_set_graph",
     "mpcekf_dev_alloc", "mpcekf_dev_free", "mpcekf_dev_copy", "mpcekf_dev_copy2d", "mpcekf_sync",
-    "mpcekf_get_scalars",
+    "mpcekf_get_scalars", "mpcekf_lin_fields",
 ]
 
 COPY_H2D, COPY_D2H, COPY_D2D = 0, 1, 2
@@ -137,6 +137,7 @@ def load():
     L.mpcekf_dev_copy2d.argtypes = [vp, C.c_int64, vp, C.c_int64, C.c_int64, C.c_int64, C.c_int32]
     L.mpcekf_sync.argtypes = [vp]
     L.mpcekf_get_scalars.argtypes = [vp, _ip, C.c_int32, _dp, _ip, _ip]
+    L.mpcekf_lin_fields.argtypes = [vp, _ip, C.c_int32, _dp, _dp]
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_build_id"):
             getattr(L, nm).restype = C.c_int

@@ -31,7 +31,12 @@ def _mtime(p):
 
 
 def _stale(obj, src):
-    deps = DEPS + (SOURCES if os.path.basename(src) == "mpcekf_host.cpp" else [])  # it embeds the source hash
+    # the host embeds the source hash and includes the public header; the kernel files
+    # include only the csrc headers
+    if os.path.basename(src) == "mpcekf_host.cpp":
+        deps = DEPS + SOURCES
+    else:
+        deps = [d for d in DEPS if not d.endswith("mpcekf.h")]
     newest = max([_mtime(src)] + [_mtime(os.path.join(SRC, d)) for d in deps])
     return _mtime(obj) < newest
 

@@ -148,6 +148,21 @@ struct mpcekf_ctx {
     HIPCHK(hipGraphLaunch(ex, stream));
     return MPCEKF_OK;
   }
+  // the stage route's device-resident hand-offs (runMPC.m:88-103 as the drop-ins call it):
+  // the last mpcekf_ekf_step's zk and Xind, the last mpcekf_linearize's records, so the next
+  // stage call can take NULL for them instead of a host round trip (valid until a fused step,
+  // set_state or init_cells; stage_zk / stage_lin say which are current)
+  double *d_szk = nullptr, *d_sxg = nullptr, *d_slin = nullptr;
+  int *d_sxm = nullptr;
+  bool stage_zk = false, stage_lin = false;
+  int stage_bufs() {
+    const size_t nzz = (size_t)nz + 2;
+    if (!d_szk) HIPCHK(hipMalloc((void **)&d_szk, (size_t)n * nzz * sizeof(double)));
+    if (!d_sxg) HIPCHK(hipMalloc((void **)&d_sxg, (size_t)n * 4 * sizeof(double)));
+    if (!d_sxm) HIPCHK(hipMalloc((void **)&d_sxm, (size_t)n * 4 * sizeof(int)));
+    if (!d_slin) HIPCHK(hipMalloc((void **)&d_slin, (size_t)n * MPCEKF_LIN_SIZE * sizeof(double)));
+    return MPCEKF_OK;
+  }
   int diag_bufs() {  // the linearisation records and uk_1 copy of the poles / sv diagnostics
     if (!d_lin) HIPCHK(hipMalloc((void **)&d_lin, (size_t)n * MPCEKF_LIN_SIZE * sizeof(double)));
     if (!d_uk1p) HIPCHK(hipMalloc((void **)&d_uk1p, (size_t)n * sizeof(double)));
@@ -356,24 +371,41 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       X->soc_end[e][one].assign(src, src + nte);
       for (int j = 0; j < MAXTT; ++j) tabs.push_back(j < nte ? src[j] : 0.0);
     }
-  std::vector<double> ptab;  // v3: [fn][side][nte][nth-1][KPOLY], then Uocp1 [side][nth-1][KPOLY]
+  // v3 device layout (mpcekf_kernels.hip ETab::f): per function and electrode the nte rows of
+  // each theta interval adjacent, [nth-1][nte][KPOLY] (cubics padded with c4 = c5 = 0), or
+  // [nth-1][1][KPOLY] when every row is equal (tconst: no T blend, the same value); Uocp1 last
+  std::vector<double> ptab;
   const int np = R->tab_npoly;
-  auto add_poly = [&](const double *src, size_t rows) {
-    for (size_t k = 0; k < rows * (size_t)(nth - 1); ++k)
-      for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[k * np + c] : 0.0);  // cubic: c4 = c5 = 0
+  const size_t nint = (size_t)(nth - 1);
+  r.tconst = 0;
+  auto add_poly = [&](const double *src, int rows) {  // src [rows][nth-1][np] (ABI order)
+    for (size_t i = 0; i < nint; ++i)
+      for (int j = 0; j < rows; ++j)
+        for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[((size_t)j * nint + i) * np + c] : 0.0);
   };
-  for (int fn = 0; fn < 5; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
-    for (const mpcekf_electrode *e : els) {
-      if (poly) {
-        add_poly(fn == 0 ? e->Uocp_p : fn == 1 ? e->dUocp_p : fn == 2 ? e->k0_p : fn == 3 ? e->Rf_p : e->Cdleff_p,
-                 (size_t)nte);
-        continue;
-      }
-      const double *t = fn == 0 ? e->Uocp : fn == 1 ? e->dUocp : fn == 2 ? e->k0 : fn == 3 ? e->Rf : e->Cdleff;
-      tabs.insert(tabs.end(), t, t + (size_t)nte * nth);
+  for (int fn = 0; fn < 5 && poly; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
+    for (int sd = 0; sd < 2; ++sd) {
+      const mpcekf_electrode *e = els[sd];
+      const double *src =
+          fn == 0 ? e->Uocp_p : fn == 1 ? e->dUocp_p : fn == 2 ? e->k0_p : fn == 3 ? e->Rf_p : e->Cdleff_p;
+      bool same = nte > 1;
+      for (int j = 1; j < nte && same; ++j)
+        same = std::memcmp(src, src + (size_t)j * nint * np, nint * np * sizeof(double)) == 0;
+      if (same) r.tconst |= 1 << (fn * 2 + sd);
+      r.poff[fn][sd] = (long long)ptab.size();
+      add_poly(src, same ? 1 : nte);
     }
+  if (!poly)  // v2: [fn][side][nte][nth] in the LDS blob
+    for (int fn = 0; fn < 5; ++fn)
+      for (const mpcekf_electrode *e : els) {
+        const double *t = fn == 0 ? e->Uocp : fn == 1 ? e->dUocp : fn == 2 ? e->k0 : fn == 3 ? e->Rf : e->Cdleff;
+        tabs.insert(tabs.end(), t, t + (size_t)nte * nth);
+      }
   if (poly)
-    for (const mpcekf_electrode *e : els) add_poly(e->Uocp1_p, 1);
+    for (int sd = 0; sd < 2; ++sd) {
+      r.poff1[sd] = (long long)ptab.size();
+      add_poly(els[sd]->Uocp1_p, 1);
+    }
   r.npoly = poly ? KPOLY : 0;
   r.arr = 0;
   for (int f = 0; f < 5; ++f)
@@ -545,7 +577,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   // size (0.080 vs 0.075 ms at 1,024 cells, 0.098 vs 0.090 at 16,384, 0.20 vs 0.11 at 65,536;
   // profiles/r02g_*): the per-cell scalar work is replicated four times and the 512-thread
   // blocks run two rounds per CU.  MPCEKF_QUAD=1 turns it on (results identical).
-  const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide;
+  const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide && !rom->tab_npoly;
   X->quad = false;
   if (const char *e = std::getenv("MPCEKF_QUAD")) X->quad = quad_ok && std::atoi(e) != 0;
   if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) X->ekf4_block = std::atoi(e) == 1024 ? 1024 : 512;
@@ -595,6 +627,9 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   s.hist_p = X->d_hist; s.hist_u = X->d_hist + n * LAZY_H;
   s.mb = X->d_mb;
   s.stamps = X->d_stamps;
+  // rows the current launch sequence does not write (k_plant's 12..19 when the plant runs
+  // inside k_cell) read back as zero, never as stale allocation contents
+  if (X->d_stamps) HIPCHK(hipMemset(X->d_stamps, 0, (size_t)n * NSTAMPS * sizeof(long long)));
   double *cs = X->d_const;
   s.Tc = cs; s.SOC0 = cs + n; s.SOC0n = cs + 2 * n; s.SOC0p = cs + 3 * n;
   if (X->wide) {
@@ -634,7 +669,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.R, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
-                  X->w.q, X->w.list, X->w.hist, X->d_poly};
+                  X->w.q, X->w.list, X->w.hist, X->d_poly, X->d_szk, X->d_sxg, X->d_sxm, X->d_slin};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -692,6 +727,7 @@ static int set_tc(mpcekf_ctx *X, const double *tc) {
 
 // initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.
 int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_degC) {
+  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
   if (!X || ((!soc0_pct || !tc_degC) && X->n)) return fail(MPCEKF_E_ARG, "init_cells: null argument");
   HIPCHK(hipSetDevice(X->device));
   const size_t n = (size_t)X->n;
@@ -745,6 +781,7 @@ static int lerr(int rc, const char *what) {
 // update) -> iterEKF measurement update -> EKFmatsHandler -> iterMPC.
 int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const mpcekf_traj *tr,
                    int32_t outputs_on_device) {
+  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
   int rc = need_init(X);
   if (rc) return rc;
   if (nsteps < 0) return fail(MPCEKF_E_ARG, "nsteps < 0");
@@ -1138,14 +1175,17 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
                     double *boundzk, int32_t *xind_model, double *xind_gamma) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!vk || !ik || !zk || !xind_model || !xind_gamma) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
+  if (!vk || !ik) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
   if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
-  if ((rc = X->tmp((2 * n + 2 * n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048))) return rc;
+  if ((rc = X->tmp((2 * n + n * nzz) * 8 + 2048)) || (rc = X->stage_bufs())) return rc;
   Slab sl{(char *)X->d_tmp};
-  double *dvk = sl.take<double>(n), *dik = sl.take<double>(n), *dzk = sl.take<double>(n * nzz);
-  double *dzb = sl.take<double>(n * nzz), *dxg = sl.take<double>(4 * n);
-  int *dxm = sl.take<int>(4 * n);
+  double *dvk = sl.take<double>(n), *dik = sl.take<double>(n), *dzb = sl.take<double>(n * nzz);
+  // zk and Xind stay on the device for the next mpcekf_linearize (NULL there); each host
+  // output is copied only when given
+  double *dzk = X->d_szk, *dxg = X->d_sxg;
+  int *dxm = X->d_sxm;
+  X->stage_zk = X->stage_lin = false;
   HIPCHK(hipMemcpyAsync(dvk, vk, n * 8, hipMemcpyHostToDevice, X->stream));
   HIPCHK(hipMemcpyAsync(dik, ik, n * 8, hipMemcpyHostToDevice, X->stream));
   // iterEKF.m:55 lock-out must see the state before the time update: the bulk
@@ -1164,11 +1204,12 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   io.xg_out = dxg;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
   if (bnd_kernel && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
-  HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
+  if (zk) HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
   if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipMemcpyAsync(xind_gamma, dxg, 4 * n * 8, hipMemcpyDeviceToHost, X->stream));
+  if (xind_model) HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));
+  if (xind_gamma) HIPCHK(hipMemcpyAsync(xind_gamma, dxg, 4 * n * 8, hipMemcpyDeviceToHost, X->stream));
   HIPCHK(hipStreamSynchronize(X->stream));
+  X->stage_zk = true;
   return MPCEKF_OK;
 }
 
@@ -1176,24 +1217,51 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
                      const double *tk_degC, double *lin) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!zk || !xind_model || !xind_gamma || !lin) return fail(MPCEKF_E_ARG, "linearize: null argument");
+  if (!zk != !xind_model || !xind_model != !xind_gamma)
+    return fail(MPCEKF_E_ARG, "linearize: zk, xind_model and xind_gamma are all given or all NULL");
+  if (!zk && !X->stage_zk) return fail(MPCEKF_E_STATE, "linearize: NULL zk / Xind but no mpcekf_ekf_step before it");
   if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
-  if ((rc = X->tmp((n * nzz + 4 * n + n * MPCEKF_LIN_SIZE) * 8 + 4 * n * 4 + 2048))) return rc;
+  if ((rc = X->tmp((n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048)) || (rc = X->stage_bufs())) return rc;
   Slab sl{(char *)X->d_tmp};
-  double *dzk = sl.take<double>(n * nzz), *dxg = sl.take<double>(4 * n), *dl = sl.take<double>(n * MPCEKF_LIN_SIZE);
-  int *dxm = sl.take<int>(4 * n);
-  HIPCHK(hipMemcpyAsync(dzk, zk, n * nzz * 8, hipMemcpyHostToDevice, X->stream));
-  HIPCHK(hipMemcpyAsync(dxm, xind_model, 4 * n * 4, hipMemcpyHostToDevice, X->stream));
-  HIPCHK(hipMemcpyAsync(dxg, xind_gamma, 4 * n * 8, hipMemcpyHostToDevice, X->stream));
+  double *dzk = X->d_szk, *dxg = X->d_sxg, *dl = X->d_slin;
+  int *dxm = X->d_sxm;
+  if (zk) {  // the caller's zk / Xind (a host that changed them after iterEKF)
+    dzk = sl.take<double>(n * nzz);
+    dxg = sl.take<double>(4 * n);
+    dxm = sl.take<int>(4 * n);
+    HIPCHK(hipMemcpyAsync(dzk, zk, n * nzz * 8, hipMemcpyHostToDevice, X->stream));
+    HIPCHK(hipMemcpyAsync(dxm, xind_model, 4 * n * 4, hipMemcpyHostToDevice, X->stream));
+    HIPCHK(hipMemcpyAsync(dxg, xind_gamma, 4 * n * 8, hipMemcpyHostToDevice, X->stream));
+  }
   KIO io{};
   io.mode = MODE_LIN;
   io.zk_in = dzk;
   io.xm_in = dxm;
   io.xg_in = dxg;
   io.lin_out = dl;
+  X->stage_lin = false;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-  HIPCHK(hipMemcpyAsync(lin, dl, n * MPCEKF_LIN_SIZE * 8, hipMemcpyDeviceToHost, X->stream));
+  if (lin) HIPCHK(hipMemcpyAsync(lin, dl, n * MPCEKF_LIN_SIZE * 8, hipMemcpyDeviceToHost, X->stream));
+  HIPCHK(hipStreamSynchronize(X->stream));
+  X->stage_lin = true;
+  return MPCEKF_OK;
+}
+
+int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const double *set, double *out) {
+  int rc = need_init(X);
+  if (rc) return rc;
+  if (!X->stage_lin) return fail(MPCEKF_E_STATE, "lin_fields: no mpcekf_linearize record on the device");
+  if (nslots < 0 || nslots > MPCEKF_LIN_SIZE || (nslots && !slots)) return fail(MPCEKF_E_ARG, "lin_fields: bad slots");
+  for (int i = 0; i < nslots; ++i)
+    if (slots[i] < 0 || slots[i] >= MPCEKF_LIN_SIZE) return fail(MPCEKF_E_ARG, "lin_fields: slot %d", slots[i]);
+  const size_t n = (size_t)X->n, rec = MPCEKF_LIN_SIZE * 8;
+  // one pitched copy per slot: only the named doubles cross PCIe ([ncells][nslots] on the host)
+  for (int i = 0; i < nslots; ++i) {
+    double *col = X->d_slin + slots[i];
+    if (set) HIPCHK(hipMemcpy2DAsync(col, rec, set + i, (size_t)nslots * 8, 8, n, hipMemcpyHostToDevice, X->stream));
+    if (out) HIPCHK(hipMemcpy2DAsync(out + i, (size_t)nslots * 8, col, rec, 8, n, hipMemcpyDeviceToHost, X->stream));
+  }
   HIPCHK(hipStreamSynchronize(X->stream));
   return MPCEKF_OK;
 }
@@ -1206,14 +1274,16 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
                        double *J_unc, double *J_fin, double *norm_du, int32_t *nviol) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!lin || !soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
+  if (!soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
+  if (!lin && !X->stage_lin) return fail(MPCEKF_E_STATE, "mpc_step: NULL lin but no mpcekf_linearize record");
   size_t n = (size_t)X->n;
   if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + 5 * n) * 8 + 2 * n * 4 + 4096))) return rc;
   Slab sl{(char *)X->d_tmp};
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *ds = sl.take<double>(n), *du = sl.take<double>(n);
   double *dju = sl.take<double>(n), *djf = sl.take<double>(n), *dnd = sl.take<double>(n);
   int *dn = sl.take<int>(n), *dv = sl.take<int>(n);
-  HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  if (lin) HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  else dl = X->d_slin;  // the device-resident record of the last mpcekf_linearize
   HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, X->stream));
   KIO io{};
   io.mode = MODE_MPC;
@@ -1246,14 +1316,15 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
 int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!lin) return fail(MPCEKF_E_ARG, "mpc_diag: null lin");
+  if (!lin && !X->stage_lin) return fail(MPCEKF_E_STATE, "mpc_diag: NULL lin but no mpcekf_linearize record");
   if (!poles && !sv) return MPCEKF_OK;
   size_t n = (size_t)X->n;
   if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + n + n * 3 * NA) * 8 + 2048))) return rc;
   Slab sl{(char *)X->d_tmp};
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *du = sl.take<double>(n), *dp = sl.take<double>(n * 2 * NA),
          *ds = sl.take<double>(n * NA);
-  HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  if (lin) HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  else dl = X->d_slin;
   if (uk_1) HIPCHK(hipMemcpyAsync(du, uk_1, n * 8, hipMemcpyHostToDevice, X->stream));
   else HIPCHK(hipMemcpyAsync(du, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
   rc = X->wide ? launch_cl_diag_wide(X->k, X->n, dl, du, poles ? dp : nullptr, sv ? ds : nullptr, X->stream)
@@ -1477,6 +1548,7 @@ int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, doub
 }
 
 int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
+  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
   int rc = need_init(X);
   if (rc) return rc;
   if (!st) return fail(MPCEKF_E_ARG, "set_state: null");

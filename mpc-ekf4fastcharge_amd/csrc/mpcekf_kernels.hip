@@ -168,21 +168,42 @@ __device__ __forceinline__ double tabi(const double *t, int n, double x) {
 // ABI v3 polynomial row (include/mpcekf.h tab_npoly): theta's interval i and s = t - i as
 // in tabi, then Horner over the interval's 6 coefficients (a cubic's upper two are 0),
 // read from the global table (L2-resident) as three 16-byte loads.  oracle: tab_poly.
-__device__ __forceinline__ double tabp(const double *c, int n, double x) {
-  if (x != x) return __builtin_nan("");
-  double xc = fmin(fmax(x, 0.0), 1.0);
-  double tt = xc * (double)(n - 1);
-  int i = (int)floor(tt);
-  if (i > n - 2) i = n - 2;
-  const double s = tt - (double)i;
-  const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * KPOLY);
-  const double2 c01 = p[0], c23 = p[1], c45 = p[2];
+__device__ __forceinline__ double horner6(const double2 c01, const double2 c23, const double2 c45, double s) {
   double v = c45.y;
   v = c45.x + s * v;
   v = c23.y + s * v;
   v = c23.x + s * v;
   v = c01.y + s * v;
   return c01.x + s * v;
+}
+__device__ __forceinline__ int tab_interval(int n, double x, double &s) {
+  double xc = fmin(fmax(x, 0.0), 1.0);
+  double tt = xc * (double)(n - 1);
+  int i = (int)floor(tt);
+  if (i > n - 2) i = n - 2;
+  s = tt - (double)i;
+  return i;
+}
+// one row: interval i's coefficients at c + i * istride
+__device__ __forceinline__ double tabp(const double *c, int n, double x, int istride) {
+  if (x != x) return __builtin_nan("");
+  double s;
+  const int i = tab_interval(n, x, s);
+  const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
+  return horner6(p[0], p[1], p[2], s);
+}
+// two adjacent rows of interval i (the T bracket): a from c + i * istride, b KPOLY after
+__device__ __forceinline__ void tabp2(const double *c, int n, double x, int istride, double &a, double &b) {
+  if (x != x) {
+    a = b = __builtin_nan("");
+    return;
+  }
+  double s;
+  const int i = tab_interval(n, x, s);
+  const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
+  const double2 a01 = p[0], a23 = p[1], a45 = p[2], b01 = p[3], b23 = p[4], b45 = p[5];
+  a = horner6(a01, a23, a45, s);
+  b = horner6(b01, b23, b45, s);
 }
 // Defined exp of the v3 Arrhenius factor (oracle/mpcekf_oracle.c orc_exp, rom.py dexp):
 // x = k ln2 + r, k = floor(x / ln2 + 1/2), fdlibm's rational form for exp(r); only
@@ -219,20 +240,27 @@ __host__ __device__ constexpr int etab_header(int nth) { return 2 * nth + 5 * MA
 struct ETab {
   const double *b;  // LDS base of the tables
   const KRom *r;    // v3: the polynomial table and the Arrhenius energies
+  bool pl;          // v3 tables: a constant of the instantiation (etab<PL>), so each kernel
+                    // compiles one lookup (the linear kernels are the round-4 code)
   int nth, nte;
   int hn;           // Uocp1 points in the LDS header: nth (v2), 0 (v3)
   int j;            // temperature bracket of this cell-step
   double g;
   double xa;        // v3: 1/Tref - 1/T of this cell-step (T unclamped)
-  __device__ __forceinline__ double prow(int row, double th) const {
-    return tabp(r->poly + (size_t)row * (nth - 1) * KPOLY, nth, th);
-  }
+  // v3 device layout (host build_rom): per function and electrode, interval-major with the
+  // nte temperature rows of an interval adjacent, [fn][side][nth-1][nte][KPOLY], so the two
+  // rows of a bracket are one 96-byte span; a T-invariant function (KRom::tconst: all rows
+  // equal, e.g. an exact Arrhenius one) keeps one row, [nth-1][1][KPOLY]; Uocp1 last.
   __device__ __forceinline__ double f(int side, int fn, double th) const {
-    if (r->npoly) {
-      const int row = (fn * 2 + side) * nte + j;
-      double a = prow(row, th);
-      if (nte > 1) {
-        const double c = prow(row + 1, th);
+    if (pl) {
+      const bool one = (r->tconst >> (fn * 2 + side)) & 1;
+      const double *base = r->poly + r->poff[fn][side];
+      double a;
+      if (one || nte == 1) {
+        a = tabp(base, nth, th, KPOLY);
+      } else {
+        double c;
+        tabp2(base + j * KPOLY, nth, th, nte * KPOLY, a, c);
         a = a + g * (c - a);
       }
       const double ear = r->ear[fn][side];
@@ -246,7 +274,7 @@ struct ETab {
     return a + g * (c - a);
   }
   __device__ __forceinline__ double u1(int side, double th) const {
-    if (r->npoly) return prow(NEF * 2 * nte + side, th);
+    if (pl) return tabp(r->poly + r->poff1[side], nth, th, KPOLY);
     return tabi(b + side * nth, nth, th);
   }
   __device__ __forceinline__ double tk(int i) const { return b[2 * hn + i]; }
@@ -258,7 +286,7 @@ struct ETab {
   __device__ __forceinline__ void bracket(double T) {
     j = 0;
     g = 0.0;
-    xa = r->arr ? 1.0 / r->Tref - 1.0 / T : 0.0;
+    xa = pl && r->arr ? 1.0 / r->Tref - 1.0 / T : 0.0;
     if (nte == 1) return;
     const double Tc = fmin(fmax(T, tk(0)), tk(nte - 1));
     int k = 0;
@@ -272,13 +300,15 @@ struct ETab {
     return s0 + z * (s1 - s0);
   }
 };
+template <bool PL>
 __device__ __forceinline__ ETab etab(const KRom &r, const double *base, double T) {
   ETab e;
   e.b = base;
   e.r = &r;
+  e.pl = PL;
   e.nth = r.nth;
   e.nte = r.nte;
-  e.hn = r.npoly ? 0 : r.nth;
+  e.hn = PL ? 0 : r.nth;
   e.bracket(T);
   return e;
 }
@@ -1454,7 +1484,7 @@ __device__ __forceinline__ void ring_chunk(const double *ring, const KState &s, 
 // ---------------------------------------------------------------------------
 // k_plant: OB_step simStep outputs for every cell (lane per cell)
 // ---------------------------------------------------------------------------
-template <bool GR>
+template <bool GR, bool PL>
 __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, const double *iapp, double *vout,
                                                const int lazy_t, const double *tc_in) {
   extern __shared__ double lds[];
@@ -1481,7 +1511,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
   }
   double Iapp = iapp[c];
   double T = (tc_in ? tc_in[c] : s.Tc[c]) + 273.15;  // OB_step.m:75
-  const ETab et = etab(r, tb + r.plant_tab, T);
+  const ETab et = etab<PL>(r, tb + r.plant_tab, T);
   double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
   const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
   double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
@@ -1603,7 +1633,7 @@ __global__ void __launch_bounds__(256) k_plant(const KRom r, const KState s, con
 #define MPCEKF_PLANT_QUAD 1
 #endif
 constexpr int PLANT4_BLOCK = 1024;
-template <bool GR>
+template <bool GR, bool PL>
 __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KState s, const double *iapp,
                                                          double *vout, const int lazy_t, const double *tc_in) {
   extern __shared__ double lds[];
@@ -1642,7 +1672,7 @@ __global__ void __launch_bounds__(PLANT4_BLOCK) k_plant4(const KRom r, const KSt
     return;
   }
   const double T = tcs + 273.15;  // OB_step.m:75
-  const ETab et = etab(r, tb + r.plant_tab, T);
+  const ETab et = etab<PL>(r, tb + r.plant_tab, T);
   const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
   double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
   int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
@@ -2265,7 +2295,7 @@ __device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]
 // first C rows, D at nzp*5, diag(A) after them -- the integrator's a = 1 exactly, checked
 // by build_rom -- and the res0 column after the Sigma coefficients).  Returns Vcell; the
 // plant state, averages, ring inputs and timestamps are stored as k_plant stores them.
-template <int NZ>
+template <int NZ, bool PL>
 __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, const double *L, const double *tb,
                                              const double *Tp, const double *Zp, int64_t c, int lazy_t, double Iapp,
                                              double tcs, int st) {
@@ -2278,7 +2308,7 @@ __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, con
   }
   if (st & ST_ERROR) return __builtin_nan("");
   const double T = tcs + 273.15;  // OB_step.m:75
-  const ETab et = etab(r, tb + r.cell_tab, T);
+  const ETab et = etab<PL>(r, tb + r.cell_tab, T);
   double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
   const double SOC0n = s.SOC0n[c], SOC0p = s.SOC0p[c];
   const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
@@ -2474,7 +2504,7 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
 // (with its slow lanes finished in the same kernel: MPCEKF_HILD_INLINE_SLOW)
 bool cell_runs_hild() { return MPCEKF_CELL_HILD != 0 && MPCEKF_HILD_INLINE_SLOW != 0; }
 __device__ __forceinline__ void hild_cell(const KCfg &cf, const KState &s, const KIO &io, int64_t c);
-template <int NZ, int PARTS, bool MB = false, bool GR = false>
+template <int NZ, int PARTS, bool MB = false, bool GR = false, bool PL = false>
 __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
   const int lo = GR ? r.cell_tab : 0;  // GR: model rows from the global blob (k_plant)
@@ -2500,7 +2530,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   const double Tc = fplant && io.tc_in ? io.tc_in[c] : s.Tc[c];
   if (fplant && io.tc_in) s.Tc[c] = Tc;  // this step's TC (runMPC.m:85-92), read by every later kernel
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.et = etab(r, tb + r.cell_tab, cc.T);
+  cc.et = etab<PL>(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
   const bool fused = io.mode & MODE_FUSED;
   if (io.mode & (MODE_MPC | MODE_FUSED)) s.hflag[c] = 0;  // set again only if hildreth.m must run
@@ -2545,7 +2575,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     if constexpr ((PARTS & P_EKF) && !MB) {
       if (fplant && !planted) {
         if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
-        vplant = cell_plant<NZ>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
+        vplant = cell_plant<NZ, PL>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
         s.vk[c] = vplant;
         planted = true;
       }
@@ -3034,7 +3064,7 @@ __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, con
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.et = etab(r, tb + r.cell_tab, cc.T);
+  cc.et = etab<false>(r, tb + r.cell_tab, cc.T);  // linear tables only (the host keeps v3 ROMs on k_cell)
   int st = s.status[c];
   const int t = io.lazy_t;
   if (live && j == 0) s.hflag[c] = 0;
@@ -3856,22 +3886,27 @@ bool cell_kernel_supported(int nzp) { return nzp == 26 || nzp == 32; }
 int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vout, int lazy_t, const double *tc_in,
                  void *stream) {
   if (s.n == 0) return 0;
+  const hipStream_t st = (hipStream_t)stream;
+  const int lds = plant_lds_bytes(r);
   if (MPCEKF_PLANT_QUAD) {
     const dim3 g(grid_for(4 * s.n, PLANT4_BLOCK)), b(PLANT4_BLOCK);
-    if (r.rom_global)
-      hipLaunchKernelGGL(k_plant4<true>, g, b, plant_lds_bytes(r), (hipStream_t)stream, r, s, iapp, vout, lazy_t,
-                         tc_in);
-    else
-      hipLaunchKernelGGL(k_plant4<false>, g, b, plant_lds_bytes(r), (hipStream_t)stream, r, s, iapp, vout, lazy_t,
-                         tc_in);
+    if (r.npoly) {
+      if (r.rom_global) hipLaunchKernelGGL((k_plant4<true, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+      else hipLaunchKernelGGL((k_plant4<false, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+    } else {
+      if (r.rom_global) hipLaunchKernelGGL((k_plant4<true, false>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+      else hipLaunchKernelGGL((k_plant4<false, false>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+    }
     return (int)hipGetLastError();
   }
-  if (r.rom_global)
-    hipLaunchKernelGGL(k_plant<true>, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r,
-                       s, iapp, vout, lazy_t, tc_in);
-  else
-    hipLaunchKernelGGL(k_plant<false>, dim3(grid_for(s.n, 256)), dim3(256), plant_lds_bytes(r), (hipStream_t)stream, r,
-                       s, iapp, vout, lazy_t, tc_in);
+  const dim3 g(grid_for(s.n, 256)), b(256);
+  if (r.npoly) {
+    if (r.rom_global) hipLaunchKernelGGL((k_plant<true, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+    else hipLaunchKernelGGL((k_plant<false, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+  } else {
+    if (r.rom_global) hipLaunchKernelGGL((k_plant<true, false>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+    else hipLaunchKernelGGL((k_plant<false, false>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
+  }
   return (int)hipGetLastError();
 }
 
@@ -3903,25 +3938,32 @@ int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iap
   return (int)hipGetLastError();
 }
 
-template <int NZ, int PARTS, bool MB, bool GR>
+template <int NZ, int PARTS, bool MB, bool GR, bool PL>
 static void launch_cell_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   int lds = cell_lds_bytes(r);
   if (io.hild) lds = lds > (int)(4 * HILD_LDS_PER_WAVE) ? lds : (int)(4 * HILD_LDS_PER_WAVE);  // the Hildreth slots
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB, GR, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB, GR>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB, GR, PL>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
 }
 
 template <int NZ, int PARTS, bool MB>
 static void launch_cell_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  if (r.npoly) {  // ABI v3 tables: the k_cell instantiations with the polynomial lookup
+    if (r.rom_global)
+      launch_cell_g<NZ, PARTS, MB, true, true>(r, c, s, io, st);
+    else
+      launch_cell_g<NZ, PARTS, MB, false, true>(r, c, s, io, st);
+    return;
+  }
   if (r.rom_global)
-    launch_cell_g<NZ, PARTS, MB, true>(r, c, s, io, st);
+    launch_cell_g<NZ, PARTS, MB, true, false>(r, c, s, io, st);
   else
-    launch_cell_g<NZ, PARTS, MB, false>(r, c, s, io, st);
+    launch_cell_g<NZ, PARTS, MB, false, false>(r, c, s, io, st);
 }
 
 template <int NZ>
@@ -3978,6 +4020,7 @@ static void launch_ekf4_t(const KRom &r, const KCfg &c, const KState &s, const K
 // block = 512 (128 cells, 256 VGPRs, 2 waves per SIMD) or 1024 (256 cells, 128 VGPRs, 4 waves per SIMD)
 int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int block) {
   if (s.n == 0) return 0;
+  if (r.npoly) return -1;  // k_ekf4 reads the v2 linear tables only (the host keeps v3 ROMs on k_cell)
   hipStream_t st = (hipStream_t)stream;
   const bool big = block == 1024;
   switch (r.nzp) {

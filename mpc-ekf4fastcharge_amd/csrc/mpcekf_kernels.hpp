@@ -64,6 +64,11 @@ struct KRom {
   int npoly, arr;
   const double *poly;
   double ear[5][2];
+  // v3 device layout of `poly` (mpcekf_kernels.hip ETab::f): offset of each function's
+  // rows [fn][side] and of Uocp1 [side]; tconst bit fn*2+side: the rows are all equal and
+  // the function keeps one (no T blend)
+  long long poff[5][2], poff1[2];
+  int tconst;
 };
 constexpr int KPOLY = 6;  // coefficients per theta interval the kernels evaluate (quintic; cubics padded)
 

@@ -152,6 +152,8 @@ class DeviceBuffer:
     def to_host(self, rows=None):
         """The first ``rows`` leading-axis rows (default all) as a numpy array."""
         rows = self.shape[0] if rows is None else int(rows)
+        if not 0 <= rows <= self.shape[0]:
+            raise ValueError(f"to_host: rows = {rows} outside [0, {self.shape[0]}]")
         out = np.empty((rows,) + self.shape[1:], dtype=self.dtype)
         check(self.L.mpcekf_dev_copy(out.ctypes.data_as(C.c_void_p), C.c_void_p(self.ptr), out.nbytes,
                                      _lib.COPY_D2H))
@@ -160,9 +162,12 @@ class DeviceBuffer:
     def sampled(self, rows, stride):
         """[rows, ncells] buffer -> its every ``stride``-th column of the first ``rows`` rows
         (a pitched device-to-host copy: only the sampled elements cross PCIe)."""
-        n = self.shape[1]
-        if len(self.shape) != 2 or n % stride:
+        if len(self.shape) != 2 or stride < 1 or self.shape[1] % stride:
             raise ValueError("sampled: 2-D buffer with ncells divisible by stride expected")
+        n = self.shape[1]
+        rows = int(rows)
+        if not 0 <= rows <= self.shape[0]:
+            raise ValueError(f"sampled: rows = {rows} outside [0, {self.shape[0]}]")
         it = self.dtype.itemsize
         out = np.empty((rows, n // stride), dtype=self.dtype)
         check(self.L.mpcekf_dev_copy2d(out.ctypes.data_as(C.c_void_p), it, C.c_void_p(self.ptr), stride * it, it,
@@ -332,38 +337,55 @@ class Context:
         check(self.L.mpcekf_plant_step(self.h, dptr(i), dptr(t), dptr(v)))
         return v
 
-    def iterEKF(self, vk, ik, Tk=None, bounds=True):
+    def iterEKF(self, vk, ik, Tk=None, bounds=True, xind=True):
         """[zk, boundzk, ekfData, Xind] = iterEKF(vk, ik, Tk, ekfData)  (iterEKF.m:30).
 
-        Xind is returned as dict(model=[n,4] model index t*nZ+z, theT, theZ, gamma)."""
+        Xind is returned as dict(model=[n,4] model index t*nZ+z, theT, theZ, gamma);
+        xind=False: None (it stays on the device for EKFmatsHandler(None, None))."""
         v = self._vec(vk)
         i = self._vec(ik)
         t = self._tvec(Tk)
         zk = np.empty((self.n, self.nz + 2))
         zb = np.empty((self.n, self.nz + 2)) if bounds else None
-        xm = np.empty((self.n, 4), dtype=np.int32)
-        xg = np.empty((self.n, 4))
+        xm = np.empty((self.n, 4), dtype=np.int32) if xind else None
+        xg = np.empty((self.n, 4)) if xind else None
         check(self.L.mpcekf_ekf_step(self.h, dptr(v), dptr(i), dptr(t), dptr(zk), dptr(zb), iptr(xm), dptr(xg)))
-        xind = dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
-        return zk, zb, xind
+        if not xind:
+            return zk, zb, None
+        return zk, zb, dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
 
-    def EKFmatsHandler(self, zk, Xind, Tk=None):
+    def EKFmatsHandler(self, zk, Xind, Tk=None, keep=False):
         """[MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)  (EKFmatsHandler.m:1).
 
-        Returns the packed linearisation records [n, 35] (fields: LIN_FIELDS)."""
+        Returns the packed linearisation records [n, 35] (fields: LIN_FIELDS).  zk = Xind =
+        None: the device copies of the last iterEKF; keep=True: the records stay on the
+        device only (None is returned; lin_fields reads slots, iterMPC / mpc_diag take
+        lin=None) -- the stage route without host round trips."""
+        t = self._tvec(Tk)
+        lin = None if keep else np.empty((self.n, LIN_SIZE))
+        if zk is None:
+            check(self.L.mpcekf_linearize(self.h, None, None, None, dptr(t), dptr(lin)))
+            return lin
         zk = np.ascontiguousarray(zk, dtype=np.float64)
         xm = np.ascontiguousarray(Xind["model"], dtype=np.int32)
         xg = np.ascontiguousarray(Xind["gamma"], dtype=np.float64)
-        t = self._tvec(Tk)
-        lin = np.empty((self.n, LIN_SIZE))
         check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin)))
         return lin
+
+    def lin_fields(self, slots, set=None):
+        """Slots (MPCEKF_LIN_*) of the device-resident records of the last EKFmatsHandler:
+        [n, len(slots)]; ``set`` [n, len(slots)] is written into them first."""
+        sl = np.ascontiguousarray(slots, dtype=np.int32)
+        out = np.empty((self.n, sl.size))
+        st = None if set is None else np.ascontiguousarray(set, dtype=np.float64)
+        check(self.L.mpcekf_lin_fields(self.h, iptr(sl), int(sl.size), dptr(st), dptr(out)))
+        return out
 
     def iterMPC(self, lin, SOCk_1, cost=False):
         """[uk, mpcData] = iterMPC(xk, cellState, mpcData)  (iterMPC.m:1). Returns uk, nexec;
         with cost=True also this call's mpcData.cost row (iterMPC.m:89-95) as a dict of
         J_uncon, J_final, norm_DU, viol, nexec per cell."""
-        lin = np.ascontiguousarray(lin, dtype=np.float64)
+        lin = None if lin is None else np.ascontiguousarray(lin, dtype=np.float64)   # None: the device record
         s = self._vec(SOCk_1)
         uk = np.empty(self.n)
         ne = np.empty(self.n, dtype=np.int32)
@@ -379,7 +401,7 @@ class Context:
     def mpc_diag(self, lin, uk_1=None):
         """mpcData.poles / mpcData.sv of the iterMPC that iterMPC(lin, ..) would run
         (iterMPC.m:53-60): (poles complex [n, 7], sv [n, 7]).  uk_1 None: the context's."""
-        lin = np.ascontiguousarray(lin, dtype=np.float64)
+        lin = None if lin is None else np.ascontiguousarray(lin, dtype=np.float64)   # None: the device record
         u = None if uk_1 is None else self._vec(uk_1)
         p = np.empty((self.n, 7, 2))
         sv = np.empty((self.n, 7))

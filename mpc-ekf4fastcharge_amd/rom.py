@@ -854,6 +854,120 @@ def tabulate_electrode(hd: SynthHandles, th, T_K, order=1):
                      poly=coefs if cubic else None, Ea=ea or None)
 
 
+# ---------------------------------------------------------------------------------------
+# The exporter's algorithm for arbitrary handles (matlab/mpcekf_tabulate_electrode.m and
+# mpcekf_export_rom.m run the same steps on a MATLAB ROM's cellData.function; this mirror
+# lets the steps be tested here against the closed-form synthetic handles as black boxes)
+# ---------------------------------------------------------------------------------------
+FD_STEP = 1e-4   # finite-difference step of the exporter's theta-derivatives
+
+
+def fd_derivs(f, th, e=FD_STEP):
+    """(f, f', f'') of a scalar function at the nodes th by 5-point stencils of step e:
+    central inside [2e, 1 - 2e], shifted one-sided (forward / backward, 4th / 3rd order)
+    at the ends so no stencil point leaves [0, 1] (a handle need not extrapolate)."""
+    th = np.asarray(th, dtype=float)
+    y = np.array([f(t) for t in th])
+    d1, d2 = np.empty_like(y), np.empty_like(y)
+    for i, t in enumerate(th):
+        if 2 * e <= t <= 1 - 2 * e:
+            fm2, fm1, fp1, fp2 = f(t - 2 * e), f(t - e), f(t + e), f(t + 2 * e)
+            d1[i] = (-fp2 + 8 * fp1 - 8 * fm1 + fm2) / (12 * e)
+            d2[i] = (-fp2 + 16 * fp1 - 30 * y[i] + 16 * fm1 - fm2) / (12 * e * e)
+        else:
+            s = 1.0 if t < 2 * e else -1.0        # stencil into the interval
+            g = [f(t + s * k * e) for k in range(1, 5)]
+            d1[i] = s * (-25 * y[i] + 48 * g[0] - 36 * g[1] + 16 * g[2] - 3 * g[3]) / (12 * e)
+            d2[i] = (35 * y[i] - 104 * g[0] + 114 * g[1] - 56 * g[2] + 11 * g[3]) / (12 * e * e)
+    return y, d1, d2
+
+
+def detect_arrhenius(f, T_K, Tref, R, th=None, tol=1e-10):
+    """Ea (J/mol) when f(th, T) = f(th, Tref) exp(Ea/R (1/Tref - 1/T)) on the sample (the
+    ratio is theta-independent and log-linear in 1/T, both to tol), else 0.0."""
+    th = np.linspace(0.03, 0.97, 13) if th is None else th
+    Ts = [T for T in np.atleast_1d(T_K) if abs(T - Tref) > 1e-6]
+    if not Ts:
+        return 0.0
+    base = np.array([f(t, Tref) for t in th])
+    if not np.all(np.isfinite(base)) or np.any(base == 0):
+        return 0.0
+    eas = []
+    for T in Ts:
+        r = np.array([f(t, T) for t in th]) / base
+        if not np.all(np.isfinite(r)) or np.any(r <= 0) or np.ptp(r) > tol * abs(r[0]):
+            return 0.0
+        eas.append(R * math.log(float(np.mean(r))) / (1.0 / Tref - 1.0 / T))
+    ea = float(np.mean(eas))
+    if ea == 0.0 or max(abs(x - ea) for x in eas) > 1e-8 * abs(ea):
+        return 0.0
+    return ea
+
+
+def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5):
+    """An ABI v3 Electrode from a handle object with the cellData.function interface
+    (Uocp(th, T), Uocp(th), dUocp, k0, Rf, Cdleff, soc(z, T), theta0(), theta100()),
+    using only handle calls -- the exporter's algorithm (matlab/mpcekf_tabulate_electrode.m):
+
+    * per function, an Arrhenius factor when detect_arrhenius finds one; its rows are then
+      the function at Tref at every table temperature (identical rows: the library reads
+      one), else the function at each table temperature;
+    * theta-derivatives by fd_derivs; Hermite cubics (order 3) or quintics (order 5) of
+      every row (hermite_coefs); the v2 node tables alongside (the handle's values)."""
+    th = np.linspace(0.0, 1.0, int(ntheta))
+    T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
+    h = 1.0 / (th.size - 1)
+    fns = {"Uocp": fh.Uocp, "dUocp": fh.dUocp, "k0": fh.k0, "Rf": fh.Rf, "Cdleff": fh.Cdleff}
+    ea, tabs, coefs = {}, {}, {}
+    for name, f in fns.items():
+        e = detect_arrhenius(f, T_K, Tref, R)
+        if e != 0.0:
+            ea[name] = e
+        vals, cs = [], []
+        for T in T_K:
+            Tr = Tref if e != 0.0 else T
+            y, d1, d2 = fd_derivs(lambda t, Tr=Tr: f(t, Tr), th)
+            cs.append(hermite_coefs(y, d1, h, d2 if order == 5 else None))
+            vals.append(np.array([f(t, T) for t in th]))     # v2 node table: the handle itself
+        tabs[name] = np.array(vals)
+        coefs[name] = np.array(cs)
+    y, d1, d2 = fd_derivs(lambda t: fh.Uocp(t), th)
+    coefs["Uocp1"] = hermite_coefs(y, d1, h, d2 if order == 5 else None)
+    return Electrode(theta0=float(fh.theta0()), theta100=float(fh.theta100()),
+                     soc0=np.array([fh.soc(0.0, T) for T in T_K]), soc100=np.array([fh.soc(1.0, T) for T in T_K]),
+                     Uocp=tabs["Uocp"], Uocp1=y, dUocp=tabs["dUocp"], k0=tabs["k0"], Rf=tabs["Rf"],
+                     Cdleff=tabs["Cdleff"], poly=coefs, Ea=ea or None)
+
+
+# error budget of the exported tables (matlab/mpcekf_check_tables.m): north_star's 1e-6
+# relative is 80 nV on phise (~0.08 V), into which Uocp_n enters directly
+# (EKFmatsHandler.m:96); the tables are held to a tenth of it
+TABLE_BUDGET = {"Uocp": 8e-9, "dUocp_rel": 1e-7, "k0_rel": 1e-9, "Rf_rel": 1e-9, "Cdleff_rel": 1e-3, "soc_lin": 1e-12}
+
+
+def table_errors(fh, e: Electrode, T_K, Tref=298.15, R=8.3144621, theta_lo=0.0, theta_hi=1.0, n=997):
+    """Largest differences of the v3 lookups from the handles (matlab/mpcekf_check_tables.m):
+    at n theta points inside [theta_lo, theta_hi] (interval midpoints included) and at
+    every table temperature and the midpoints between them."""
+    T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
+    cf = CellFunctions(e, T_K, R, Tref)
+    xs = np.linspace(theta_lo, theta_hi, n)
+    Ts = np.sort(np.concatenate([T_K, (T_K[1:] + T_K[:-1]) / 2]))
+    err = {k: 0.0 for k in TABLE_BUDGET}
+    for T in Ts:
+        for x in xs:
+            u = fh.Uocp(x, T)
+            err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x, T) - u))
+            for nm in ("dUocp", "k0", "Rf", "Cdleff"):
+                ref = getattr(fh, nm)(x, T)
+                err[nm + "_rel"] = max(err[nm + "_rel"], abs(getattr(cf, nm)(x, T) - ref) / max(abs(ref), 1e-300))
+            s0, s1 = fh.soc(0.0, T), fh.soc(1.0, T)
+            err["soc_lin"] = max(err["soc_lin"], abs(fh.soc(x, T) - (s0 + x * (s1 - s0))))
+    for x in xs:
+        err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x) - fh.Uocp(x)))
+    return err
+
+
 def synth_handles(R=8.3144621, Tref=298.15):
     """(neg, pos) closed-form handles of the synthetic NMC30-like cell."""
     neg = SynthHandles(theta0=0.01, theta100=0.80, u=_u_neg, du=_du_neg, d2u=_d2u_neg, d3u=_d3u_neg,

@@ -105,6 +105,7 @@ typedef struct {
    * Uocp1), all NULL for linear tables; Arrhenius energies of Uocp, dUocp, k0, Rf, Cdleff */
   const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p, *Uocp1_p;
   double Ea[5];
+  int tconst; /* bit f: every row of function f's polynomials is the same (read row 0, no T blend) */
 } orc_electrode;
 
 typedef struct {
@@ -244,13 +245,14 @@ double orc_exp(double x) {
 /* One handle lookup (include/mpcekf.h): the rows j, j+1 of the T bracket at
  * theta (linear in the node values, or the v3 polynomials), a + g (b - a), then the
  * Arrhenius factor exp(Ea/R (1/Tref - 1/T)) when Ea != 0 (T unclamped). */
-static double tab2(const orc_rom *r, const double *t, const double *tp, double Ea, double th, double T) {
+static double tab2(const orc_rom *r, const double *t, const double *tp, double Ea, int one, double th, double T) {
   int j;
   double g;
   tidx(r, T, &j, &g);
   const size_t rp = (size_t)(r->ntheta - 1) * NPOLY;
+  if (tp && one) j = 0; /* T-invariant rows: row 0, no blend (the library's tconst) */
   double a = tp ? tab_poly(tp + j * rp, r->ntheta, th) : tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
-  if (r->ntemp > 1) {
+  if (r->ntemp > 1 && !(tp && one)) {
     double b = tp ? tab_poly(tp + (j + 1) * rp, r->ntheta, th)
                   : tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
     a = a + g * (b - a);
@@ -271,22 +273,22 @@ static double fsoc(const orc_rom *r, const orc_electrode *e, double z, double T)
   return s0 + z * (s1 - s0);
 }
 static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Uocp, e->Uocp_p, e->Ea[EF_U], th, T);
+  return tab2(r, e->Uocp, e->Uocp_p, e->Ea[EF_U], (e->tconst >> EF_U) & 1, th, T);
 }
 static double fUocp1(const orc_rom *r, const orc_electrode *e, double th) {
   return e->Uocp1_p ? tab_poly(e->Uocp1_p, r->ntheta, th) : tab_interp(e->Uocp1, r->ntheta, th);
 }
 static double fdUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->dUocp, e->dUocp_p, e->Ea[EF_DU], th, T);
+  return tab2(r, e->dUocp, e->dUocp_p, e->Ea[EF_DU], (e->tconst >> EF_DU) & 1, th, T);
 }
 static double fk0(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->k0, e->k0_p, e->Ea[EF_K0], th, T);
+  return tab2(r, e->k0, e->k0_p, e->Ea[EF_K0], (e->tconst >> EF_K0) & 1, th, T);
 }
 static double fRf(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Rf, e->Rf_p, e->Ea[EF_RF], th, T);
+  return tab2(r, e->Rf, e->Rf_p, e->Ea[EF_RF], (e->tconst >> EF_RF) & 1, th, T);
 }
 static double fCdl(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Cdleff, e->Cdleff_p, e->Ea[EF_CDL], th, T);
+  return tab2(r, e->Cdleff, e->Cdleff_p, e->Ea[EF_CDL], (e->tconst >> EF_CDL) & 1, th, T);
 }
 static double msqrt(double x) { return x >= 0 ? sqrt(x) : NAN; }
 

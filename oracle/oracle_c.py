@@ -28,7 +28,7 @@ class _Electrode(C.Structure):
     _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
                 ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp),
                 ("Uocp_p", _dp), ("dUocp_p", _dp), ("k0_p", _dp), ("Rf_p", _dp), ("Cdleff_p", _dp),
-                ("Uocp1_p", _dp), ("Ea", C.c_double * 5)]
+                ("Uocp1_p", _dp), ("Ea", C.c_double * 5), ("tconst", C.c_int)]
 
 
 EL_FNS = ("Uocp", "dUocp", "k0", "Rf", "Cdleff")   # orc_electrode.Ea order (EF_*)
@@ -148,6 +148,10 @@ class PackedRom:
                 setattr(s, k + "_p", _p(arr(poly6(e.poly[k]))) if e.poly else _dp())
             for i, k in enumerate(EL_FNS):
                 s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
+                # rows all equal (an exact Arrhenius function): row 0, no T blend (the library's tconst)
+                if e.poly and e.poly[k].shape[0] > 1 and all(np.array_equal(e.poly[k][0], e.poly[k][j])
+                                                             for j in range(1, e.poly[k].shape[0])):
+                    s.tconst |= 1 << i
         self.s = r
 
 

@@ -223,8 +223,9 @@ class Cell:
         tab = getattr(e, name)
         j, g = self._tj(T)
         row = (lambda k: self._interp(tab[k], th)) if coef is None else (lambda k: self._poly(coef[k], th))
-        v = row(j)
-        if len(self.TK) > 1:
+        one = coef is not None and all(np.array_equal(coef[0], coef[k]) for k in range(1, len(coef)))
+        v = row(0 if one else j)               # T-invariant rows: row 0, no blend
+        if len(self.TK) > 1 and not one:
             b = row(j + 1)
             v = v + g * (b - v)
         ea = float(e.Ea.get(name, 0.0)) if e.Ea else 0.0

@@ -176,3 +176,25 @@ def rom_struct(rom):
                 tf_code=np.array([codes[nm] for nm in rom.names], np.int32), xloc=np.asarray(rom.xloc, float),
                 F=float(rom.F), R=float(rom.R), Q=float(rom.Q), Rc=float(rom.Rc), Tref=float(rom.Tref),
                 tab_T_K=np.atleast_1d(np.asarray(rom.tab_T_K, float)), neg=el_(rom.neg), pos=el_(rom.pos))
+
+
+def default_table_temps(T_set, TC, nmax=8):
+    """matlab/mpcekf_rom_struct.m's default TdegC, restated: the ROM set-point temperatures
+    and the distinct simulation temperatures TC (only their span when they would not fit
+    the nmax slots), evenly nmax points when the set-points + span still do not, guard
+    points 10 degC beyond when 2 slots are free, then spare slots halve the widest
+    intervals (the first widest on ties, as MATLAB's max)."""
+    Ts = [float(t) for t in np.ravel(T_set)]
+    TCu = sorted(set(float(t) for t in np.ravel(TC)))
+    if len(set(Ts) | set(TCu)) > nmax:
+        TCu = sorted({min(TCu), max(TCu)})
+    T = sorted(set(Ts) | set(TCu))
+    if len(T) > nmax:
+        T = list(np.linspace(min(T), max(T), nmax))
+    if len(T) + 2 <= nmax:
+        T = sorted(set([T[0] - 10] + T + [T[-1] + 10]))
+    while len(T) < nmax:
+        d = np.diff(T)
+        k = int(np.argmax(d))
+        T = T[:k + 1] + [(T[k] + T[k + 1]) / 2] + T[k + 1:]
+    return np.array(T)

@@ -181,3 +181,46 @@ def test_linear_tables_miss_the_handle_fixtures(rom, oc):
     r = oc.run(rom, g["soc0"], g["tc"], 200, nthreads=4)
     worst = max(rel(r[k], g[k][:200]).max() for k in KEYS)
     assert worst > 1e-4, worst
+
+
+class _BlackBox:
+    """A handle object that exposes only calls (no analytic derivatives): what a MATLAB
+    cellData.function struct gives matlab/mpcekf_tabulate_electrode.m."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def __getattr__(self, nm):
+        if nm in ("Uocp", "dUocp", "k0", "Rf", "Cdleff", "soc", "theta0", "theta100"):
+            return getattr(self._h, nm)
+        raise AttributeError(nm)
+
+
+def test_exporter_algorithm_from_handle_calls_alone(P, oc):
+    """The exporter's steps (rom.py tabulate_handles / table_errors, mirrored by
+    matlab/mpcekf_tabulate_electrode.m and mpcekf_check_tables.m) on the synthetic handles
+    as black boxes: the Arrhenius energies are found, finite-difference Hermite quintics
+    at 513 points meet the error budget (rom.TABLE_BUDGET, a tenth of north_star's 1e-6 on
+    phise), and the exported ROM follows the handle fixture within 1e-6 through the C
+    oracle.  At 129 points the budget check fails: the exporter's ntheta choice is real."""
+    from importlib import import_module
+    R = import_module("mpc-ekf4fastcharge_amd.rom")
+    rom = P.make_synth_rom(lookup="quintic")
+    TK = rom.tab_T_K
+    for side in ("neg", "pos"):
+        h = _BlackBox(rom.handles[side])
+        e = R.tabulate_handles(h, 513, TK, rom.Tref, rom.R)
+        assert set(e.Ea) == {"k0", "Rf"}
+        assert abs(e.Ea["k0"] - rom.handles[side].Ea_k0) <= 1e-9 * rom.handles[side].Ea_k0
+        lo, hi = sorted((h.soc(0.05, 298.15), h.soc(0.95, 298.15)))
+        err = R.table_errors(h, e, TK, rom.Tref, rom.R, lo - 0.04, hi + 0.04, n=201)
+        assert all(err[k] <= R.TABLE_BUDGET[k] for k in err), err
+        coarse = R.table_errors(h, R.tabulate_handles(h, 129, TK, rom.Tref, rom.R), TK, rom.Tref, rom.R,
+                                lo - 0.04, hi + 0.04, n=201)
+        assert side == "pos" or coarse["Uocp"] > R.TABLE_BUDGET["Uocp"], coarse
+        setattr(rom, side, e)
+    rom.validate()
+    g = golden("handles_batch8_1000")
+    r = oc.run(rom, g["soc0"], g["tc"], 400, nthreads=4)
+    for k in KEYS:
+        assert rel(r[k], g[k][:400]).max() <= RTOL, k

@@ -266,3 +266,35 @@ def test_clear_mex_destroys_live_contexts(shim, rom):
         with pytest.raises(shim.MexError, match="not a live mpcekf context"):
             shim.mex("init", h, np.zeros(16) + 20, np.zeros(16) + 25, nargout=0)
     assert not shim.clear_mex()        # nothing registered until the next create
+
+
+def test_dropin_table_temperatures_hold_each_distinct_tc():
+    """matlab/dropin/OB_step.m passes unique(Tc) to mpcekf_rom_struct: three
+    distinct per-cell temperatures are each a table temperature (their lookups exact at
+    weight 0), thousands of distinct ones keep only their span."""
+    g = mexshim.default_table_temps([15.0, 25.0, 35.0], [20.0, 25.0, 30.0, 20.0])
+    assert {20.0, 25.0, 30.0} <= set(g) and {15.0, 35.0} <= set(g) and len(g) == 8
+    assert np.all(np.diff(g) > 0) and g[0] == 5.0 and g[-1] == 45.0
+    many = mexshim.default_table_temps([15.0, 25.0, 35.0], np.linspace(20.0, 30.0, 1000))
+    assert len(many) == 8 and {20.0, 30.0} <= set(many) and 20.0 + 10.0 / 999 not in set(many)
+
+
+@pytest.mark.gpu
+def test_dropin_three_tc_and_v3_rom_through_gateway(shim, P, M, oc):
+    """Three distinct per-cell Tc with the drop-in's table temperatures (v2 tables), and the
+    ABI v3 quintic ROM (poly / Ea fields of mpcekf_rom_struct.m), created through the
+    gateway: the fused step gives the C oracle's bits."""
+    n, steps = 48, 30
+    soc0, _ = batch_inputs(n, seed=79)
+    tc = np.array([20.0, 25.0, 30.0] * (n // 3))
+    grid = mexshim.default_table_temps(P.make_synth_rom().T_degC, np.unique(tc))
+    for rom in (P.make_synth_rom(tab_T_degC=tuple(grid)), P.make_synth_rom(lookup="quintic")):
+        h = _create(shim, rom, n, {})
+        try:
+            shim.mex("init", h, soc0, tc, nargout=0)
+            u, v, soc, ph, ne = shim.mex("step", h, float(steps), nargout=5)
+        finally:
+            shim.mex("destroy", h, nargout=0)
+        ref = oc.run(rom, soc0, tc, steps, nthreads=4)
+        for k, a in (("u", u), ("v", v), ("soc", soc), ("phise", ph), ("nexec", ne)):
+            _same(a, np.asarray(ref[k]).T, k)

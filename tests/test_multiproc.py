@@ -69,10 +69,13 @@ def test_bench_algorithmic_bytes():
     # 416*NM state bytes, + model timestamps and the two input rings
     assert b["flush"] == 416 * 63 + 2 * 2 * 4 * 63 + 2 * 8 * bench.LAZY_H
     assert bench.survey_bytes_per_cell_step(63, 23) == 26736
-    # the plant runs inside k_cell (no "plant" kernel) and boundzk comes from k_bounds' record
-    assert "plant" not in b and set(b) == {"flush", "cell", "hild"}
-    bk = bench.algorithmic_bytes_per_cell(63, 23, True, bounds_kernel=True)
-    assert bk["bounds"] == (14 + 15 + 4 + 28) * 8
+    # the library default: the plant inside k_cell (no "plant" kernel), boundzk in k_bounds
+    # from k_cell's hand-off record
+    assert "plant" not in b and set(b) == {"flush", "cell", "hild", "bounds"}
+    assert b["bounds"] == (14 + 15 + 4 + 28) * 8
+    # boundzk inside k_cell (MPCEKF_CELL_BOUNDS=1): no record, corner 1's Sigma + boundzk in k_cell
+    bc = bench.algorithmic_bytes_per_cell(63, 23, True, bounds_kernel=False)
+    assert set(bc) == {"flush", "cell", "hild"} and bc["cell"] == b["cell"] - 14 * 8 + 15 * 8 + 28 * 8
     # Np = 20 / Nc = 10: k_hild_prep hands k_hild_wide chol(E) (55) and K (100), not X (800 per cell)
     w = bench.algorithmic_bytes_per_cell(63, 100, True, Np=20, Nc=10)
     prob = 10 * 10 + 10 + 4 * 20 + 100 + 2
@@ -123,6 +126,43 @@ def test_bench_spawns_ranks_over_gloo(gpus, extra, total, per):
     assert line["scaling"] == ("strong" if "--total-cells" in extra else "weak")
     for r in range(gpus):
         assert f"rank {r}/{gpus}: cells [" in err
+
+
+def test_bench_rank_path_reduces_over_gloo_and_parent_maps_no_runtime(tmp_path):
+    """bench.py --gpus 2 (no torchrun): the parent counts nothing through HIP or torch and
+    maps no GPU runtime before it spawns the ranks (MPCEKF_BENCH_PARENT_MAPS records its
+    /proc/self/maps runtime lines), and the two ranks' gloo coordinators reduce the timing
+    as max over ranks and the shard coverage as sums: every cell once, the full SOC0
+    checksum (ragged shards of 1,001 cells)."""
+    import bench
+    maps = tmp_path / "parent_maps.txt"
+    line, err = _bench("--gpus", "2", "--dry-run", "--total-cells", "1001", "--steps", "3",
+                       env={"MPCEKF_BENCH_PARENT_MAPS": str(maps)})
+    assert maps.exists() and maps.read_text().strip() == ""
+    chk = line["dry_run_checks"]
+    assert chk["cells"] == 1001 and line["config"]["cells_per_gpu"] == [501, 500]
+    soc0, _ = bench.batch_inputs(1001)
+    assert abs(chk["soc0_sum"] - soc0.sum()) <= 1e-9 * soc0.sum()
+    assert chk["max_dt_s"] >= 0.04          # rank 1's 40 ms, not rank 0's 20 ms
+    assert line["config"]["timing_collectives"] == "gloo"
+
+
+def test_count_gpus_from_kfd_topology(tmp_path):
+    """The launcher's device count (no HIP, no torch): KFD GPU nodes with an accessible
+    render node, limited by the *_VISIBLE_DEVICES lists."""
+    import bench
+    sysfs, dev = tmp_path / "nodes", tmp_path / "dri"
+    dev.mkdir()
+    for i, (simd, minor) in enumerate([(0, 0), (256, 128), (256, 136), (256, 144), (256, 152)]):
+        d = sysfs / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simd}\ndrm_render_minor {minor}\n")
+    for minor in (128, 136, 144):           # renderD152 is not in this container
+        (dev / f"renderD{minor}").write_text("")
+    assert bench.count_gpus(str(sysfs), str(dev), env={}) == 3
+    assert bench.count_gpus(str(sysfs), str(dev), env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert bench.count_gpus(str(sysfs), str(dev), env={"ROCR_VISIBLE_DEVICES": "2"}) == 1
+    assert bench.count_gpus(str(tmp_path / "none"), str(dev), env={}) == 0
 
 
 def test_bench_refuses_world_size_mismatch():

@@ -40,14 +40,22 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-diag", action="store_true", help="skip the mpcdiag call (poles / sv)")
+    ap.add_argument("--route", default="device", choices=("device", "host", "capi"),
+                    help="device: the drop-ins' round-5 sequence (zk / Xind / lin stay on the device, 14 "
+                         "doubles of lin read back); host: the round-4 sequence (every array through the "
+                         "host); capi: the device sequence through ctypes (mpcekf.py) instead of the MEX "
+                         "gateway, so the shim's marshalling is separated out")
+    ap.add_argument("--rom-lookup", default="quintic", choices=("linear", "cubic", "quintic"))
     a = ap.parse_args()
+    if a.route == "capi":
+        return capi(a)
     import importlib
 
     import mexshim
     import bench
     P = importlib.import_module("mpc-ekf4fastcharge_amd")
     M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
-    rom = P.make_synth_rom()
+    rom = P.make_synth_rom(lookup=a.rom_lookup)
     n = a.cells
     soc0, tc = bench.batch_inputs(n)
     nbytes = {"args": 0, "state": 0}
@@ -65,15 +73,26 @@ def main():
         uk = np.zeros((1, n))
         tk = tc[None, :].copy()
 
+        e = np.zeros((0, 0))
+        lin_slots = np.array([list(range(21, 28)) + [29] + list(range(30, 36))], dtype=float)
+
         def step():
             nonlocal uk
             s = mex("state", "scalars", h, np.array([[1.0, 2.0]]))
             v = mex("args", "plant", h, uk, tk)
-            zk, zbk, xm, xg = mex("args", "ekf", h, v, uk, tk, nargout=4)
+            if a.route == "host":
+                zk, zbk, xm, xg = mex("args", "ekf", h, v, uk, tk, nargout=4)
+            else:  # Xind crosses back too (the drop-in keeps MPC.iT / iZ from it), zk / Xind are not sent back
+                zk, zbk, xm, xg = mex("args", "ekf", h, v, uk, tk, nargout=4)
             s, warn, status = mex("state", "scalars", h, np.array([[3.0, 4.0, 5.0]]), nargout=3)
-            lin = mex("args", "linearize", h, zk, xm, xg, tk)
+            if a.route == "host":
+                lin = mex("args", "linearize", h, zk, xm, xg, tk)
+            else:
+                mex("args", "linearize", h, e, e, e, tk)
+                mex("args", "linfields", h, lin_slots)     # Cphi, Dphi, bphi, xhat (runMPC.m:95-96)
+                lin = e
             if not a.no_diag:
-                mex("args", "mpcdiag", h, lin, np.zeros((0, 0)), nargout=2)
+                mex("args", "mpcdiag", h, lin, e, nargout=2)
             out = mex("args", "mpc", h, lin, zk[-1:, :], nargout=6)
             uk = out[0]
             return out
@@ -94,6 +113,7 @@ def main():
     line = {
         "what": "MATLAB drop-in stage route (matlab/dropin/*.m command sequence) through the MEX gateway, "
                 "driven by the MEX API test shim (no MATLAB); host arrays in and out every call",
+        "route": a.route, "rom_lookup": a.rom_lookup,
         "cells": n, "steps": a.steps, "warmup": a.warmup, "mpcdiag": not a.no_diag,
         "cell_steps_per_s": n * a.steps / dt, "ms_per_step": dt / a.steps * 1e3,
         "host_bytes_per_cell_step": {k: v / (n * a.steps) for k, v in nbytes.items()},
@@ -103,6 +123,75 @@ def main():
     print(json.dumps(line), flush=True)
     if not same:
         sys.exit("dropin_bench: the stage route's u differs from the fused step")
+
+
+def capi(a):
+    """The drop-ins' device-route stage sequence through the C-ABI directly (ctypes, host
+    buffers, mpcekf.py), timed per stage, bytes counted from the arrays each call moves."""
+    import importlib
+
+    import bench
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
+    rom = P.make_synth_rom(lookup=a.rom_lookup)
+    n = a.cells
+    soc0, tc = bench.batch_inputs(n)
+    slots = np.array(list(range(20, 27)) + [28] + list(range(29, 35)), dtype=np.int32)
+    tim = {k: 0.0 for k in ("scalars", "plant", "ekf", "linearize", "lin_fields", "mpcdiag", "mpc")}
+    nb = {k: 0 for k in tim}
+    with M.Context(rom, n, M.make_config(bounds=True)) as ctx:
+        ctx.init_cells(soc0, tc)
+        uk = np.zeros(n)
+
+        def timed(k, f, *args, **kw):
+            t0 = time.perf_counter()
+            r = f(*args, **kw)
+            tim[k] += time.perf_counter() - t0
+            return r
+
+        def step(count):
+            nonlocal uk
+            timed("scalars", ctx.get_scalars, ("SOCnAvg", "SOCpAvg"))          # OB_step.m:226-228
+            v = timed("plant", ctx.OB_step, uk, tc)
+            zk, zb, xi = timed("ekf", ctx.iterEKF, v, uk, tc)
+            timed("scalars", ctx.get_scalars, ("x0", "SigmaX0", "priorI"), flags=True)   # ekfData fields
+            timed("linearize", ctx.EKFmatsHandler, None, None, tc, keep=True)
+            f = timed("lin_fields", ctx.lin_fields, slots)
+            if not a.no_diag:
+                timed("mpcdiag", ctx.mpc_diag, None)
+            uk, ne, cost = timed("mpc", ctx.iterMPC, None, zk[:, -1], cost=True)
+            if count:
+                nb["scalars"] += (16 + 24 + 8) * n
+                nb["plant"] += 3 * 8 * n
+                nb["ekf"] += 3 * 8 * n + zk.nbytes + zb.nbytes + xi["model"].nbytes + xi["gamma"].nbytes
+                nb["linearize"] += 8 * n
+                nb["lin_fields"] += f.nbytes
+                nb["mpcdiag"] += 0 if a.no_diag else (14 + 7) * 8 * n
+                nb["mpc"] += 8 * n + uk.nbytes + ne.nbytes + sum(np.asarray(x).nbytes for x in cost.values()
+                                                                  if np.asarray(x).dtype != object)
+            return uk
+
+        for _ in range(a.warmup):
+            step(False)
+        for k in tim:
+            tim[k] = 0.0
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            u_last = step(True)
+        dt = time.perf_counter() - t0
+    ref = M.runMPC(rom, soc0, tc, a.warmup + a.steps)["u"][-1]
+    same = bool(np.array_equal(u_last, ref))
+    line = {"what": "the drop-ins' device-route stage sequence through the C-ABI (ctypes, host buffers): "
+                    "plant -> ekf -> linearize (kept on device) -> lin_fields (14 doubles) -> mpc_diag -> mpc",
+            "route": "capi", "rom_lookup": a.rom_lookup, "cells": n, "steps": a.steps, "warmup": a.warmup,
+            "mpcdiag": not a.no_diag, "cell_steps_per_s": n * a.steps / dt, "ms_per_step": dt / a.steps * 1e3,
+            "ms_per_step_by_stage": {k: v / a.steps * 1e3 for k, v in tim.items()},
+            "host_bytes_per_cell_step": {k: v / (n * a.steps) for k, v in nb.items()},
+            "host_bytes_per_cell_step_total": sum(nb.values()) / (n * a.steps),
+            "u_last_equals_fused": same, "build_id": M._lib.load().mpcekf_build_id().decode()}
+    print(json.dumps(line), flush=True)
+    if not same:
+        sys.exit("dropin_bench: the C-ABI stage route's u differs from the fused step")
 
 
 if __name__ == "__main__":
