@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # fully so the per-lane arrays stay in registers instead of scratch.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
           "-Wno-unused-result", "-mllvm", "-pragma-unroll-threshold=200000"]
-SOURCES = ["mpcekf_kernels.hip", "mpcekf_wide.hip", "mpcekf_host.cpp"]
+SOURCES = ["mpcekf_kernels.hip", "mpcekf_wide.hip", "mpcekf_io.hip", "mpcekf_host.cpp"]
 DEPS = ["mpcekf_kernels.hpp", "mpcekf_mpc.hpp", "mpcekf_eig.hpp", os.path.join("..", "..", "include", "mpcekf.h")]
 
 

@@ -1255,12 +1255,23 @@ int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const
   if (nslots < 0 || nslots > MPCEKF_LIN_SIZE || (nslots && !slots)) return fail(MPCEKF_E_ARG, "lin_fields: bad slots");
   for (int i = 0; i < nslots; ++i)
     if (slots[i] < 0 || slots[i] >= MPCEKF_LIN_SIZE) return fail(MPCEKF_E_ARG, "lin_fields: slot %d", slots[i]);
-  const size_t n = (size_t)X->n, rec = MPCEKF_LIN_SIZE * 8;
-  // one pitched copy per slot: only the named doubles cross PCIe ([ncells][nslots] on the host)
-  for (int i = 0; i < nslots; ++i) {
-    double *col = X->d_slin + slots[i];
-    if (set) HIPCHK(hipMemcpy2DAsync(col, rec, set + i, (size_t)nslots * 8, 8, n, hipMemcpyHostToDevice, X->stream));
-    if (out) HIPCHK(hipMemcpy2DAsync(out + i, (size_t)nslots * 8, col, rec, 8, n, hipMemcpyDeviceToHost, X->stream));
+  if (!nslots || (!set && !out)) return MPCEKF_OK;
+  // the slots gathered into / scattered from a compact [ncells][nslots] device buffer, which
+  // crosses PCIe in one copy: only the named doubles move (per-slot pitched copies of 8-byte
+  // columns cost 3.7 ms for 14 slots at 65,536 cells, profiles/r05b_dropin_capi_65536.json)
+  const size_t n = (size_t)X->n, bytes = n * (size_t)nslots * 8;
+  if ((rc = X->tmp(bytes + 1024))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dc = sl.take<double>(n * (size_t)nslots);
+  int *ds = sl.take<int>((size_t)nslots);
+  HIPCHK(hipMemcpyAsync(ds, slots, (size_t)nslots * sizeof(int), hipMemcpyHostToDevice, X->stream));
+  if (set) {
+    HIPCHK(hipMemcpyAsync(dc, set, bytes, hipMemcpyHostToDevice, X->stream));
+    if ((rc = lerr(launch_cols(X->d_slin, X->n, MPCEKF_LIN_SIZE, ds, nslots, dc, true, X->stream), "cols"))) return rc;
+  }
+  if (out) {
+    if ((rc = lerr(launch_cols(X->d_slin, X->n, MPCEKF_LIN_SIZE, ds, nslots, dc, false, X->stream), "cols"))) return rc;
+    HIPCHK(hipMemcpyAsync(out, dc, bytes, hipMemcpyDeviceToHost, X->stream));
   }
   HIPCHK(hipStreamSynchronize(X->stream));
   return MPCEKF_OK;

@@ -166,15 +166,16 @@ __device__ __forceinline__ double tabi(const double *t, int n, double x) {
   return t[i] + f * (t[i + 1] - t[i]);
 }
 // ABI v3 polynomial row (include/mpcekf.h tab_npoly): theta's interval i and s = t - i as
-// in tabi, then Horner over the interval's 6 coefficients (a cubic's upper two are 0),
+// in tabi, then Horner (fma) over the interval's 6 coefficients (a cubic's upper two are 0),
 // read from the global table (L2-resident) as three 16-byte loads.  oracle: tab_poly.
+// Horner with explicit fma (correctly rounded here and on the host: oracle tab_poly)
 __device__ __forceinline__ double horner6(const double2 c01, const double2 c23, const double2 c45, double s) {
   double v = c45.y;
-  v = c45.x + s * v;
-  v = c23.y + s * v;
-  v = c23.x + s * v;
-  v = c01.y + s * v;
-  return c01.x + s * v;
+  v = __builtin_fma(s, v, c45.x);
+  v = __builtin_fma(s, v, c23.y);
+  v = __builtin_fma(s, v, c23.x);
+  v = __builtin_fma(s, v, c01.y);
+  return __builtin_fma(s, v, c01.x);
 }
 __device__ __forceinline__ int tab_interval(int n, double x, double &s) {
   double xc = fmin(fmax(x, 0.0), 1.0);
@@ -583,10 +584,21 @@ struct CellCtx {
 // getVariables (iterEKF.m:259-417).  Z is the permuted output vector.
 // QUAD: a lane quad per cell (k_ekf4): this lane's corner is qj with state xr[0]; the
 // corner sums Z = fma(z_j, g_j, Z), j = 0..3 in order, take z_j from lane j by DPP.
+// k0 and Rf of one getVariables call at its SOCnAvg / SOCpAvg (after its clamps): getChatV
+// (the same x0), getChatZ's scalars and EKFmatsHandler (the same x0 after the update) read
+// k0 / Rf at the unclamped averages, which are these whenever no clamp fired -- the same
+// lookup, so the same bits; they reuse the values then (fewer table reads, notably of
+// the v3 polynomials) and look up otherwise
+struct KR {
+  double T, thn, thp, k0n, k0p, rfn, rfp;  // T: the lookups' temperature (EKFmatsHandler brackets its own)
+};
+__device__ __forceinline__ bool kr_hit(const KR *kr, double T, double thn, double thp) {
+  return kr && kr->T == T && kr->thn == thn && kr->thp == thp;
+}
 template <int NZ, bool QUAD = false>
 __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, const XI &xi, double ik, double x0,
                                            double SOC0, int &warn, int &st, double Z[NZ], double &Zsoc,
-                                           const double (*xr)[NX] = nullptr, int qj = 0) {
+                                           const double (*xr)[NX] = nullptr, int qj = 0, KR *kr = nullptr) {
   double xSOC = SOC0 - x0 * (r.Ts / (3600 * r.Q));
   double SOCnAvg = cc.et.soc(0, xSOC);
   double SOCpAvg = cc.et.soc(1, xSOC);
@@ -736,6 +748,7 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   double posEta3 = 2 * r.R * cc.T / r.F * dasinh(If3 / (2 * i0p));
   double Uocpn0 = cc.et.f(0, EF_U, Z[R_TH0]), Uocpp3 = cc.et.f(1, EF_U, Z[R_TH3]);
   double Rfn = cc.et.f(0, EF_RF, SOCnAvg), Rfp = cc.et.f(1, EF_RF, SOCpAvg);  // iterEKF.m:406-407
+  if (kr) *kr = KR{cc.T, SOCnAvg, SOCpAvg, k0n, k0p, Rfn, Rfp};
   double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (Rfp * Z[R_IFDL3] - Rfn * Z[R_IFDL0]);
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
@@ -751,13 +764,23 @@ struct ChatK {
 // xSOC = SOC0 - x0 Ts/(3600 Q) with the x0 of the call: Rf and k0 at the unclamped
 // soc(xSOC, Tk) (iterEKF.m:437-442,463-464)
 __device__ __forceinline__ ChatK chat_k(const KRom &r, const CellCtx &cc, double xSOC, double zTE1, double zTH0,
-                                        double zTEE, double zTH3) {
+                                        double zTEE, double zTH3, const KR *kr = nullptr) {
   ChatK k;
   const double SOCnAvg = cc.et.soc(0, xSOC), SOCpAvg = cc.et.soc(1, xSOC);
-  k.Rfn = cc.et.f(0, EF_RF, SOCnAvg);
-  k.Rfp = cc.et.f(1, EF_RF, SOCpAvg);
-  double i0n = cc.et.f(0, EF_K0, SOCnAvg) * sqrt(zTE1 * (1 - zTH0) * zTH0);
-  double i0p = cc.et.f(1, EF_K0, SOCpAvg) * sqrt(zTEE * (1 - zTH3) * zTH3);
+  double k0n, k0p;
+  if (kr_hit(kr, cc.T, SOCnAvg, SOCpAvg)) {
+    k.Rfn = kr->rfn;
+    k.Rfp = kr->rfp;
+    k0n = kr->k0n;
+    k0p = kr->k0p;
+  } else {
+    k.Rfn = cc.et.f(0, EF_RF, SOCnAvg);
+    k.Rfp = cc.et.f(1, EF_RF, SOCpAvg);
+    k0n = cc.et.f(0, EF_K0, SOCnAvg);
+    k0p = cc.et.f(1, EF_K0, SOCpAvg);
+  }
+  double i0n = k0n * sqrt(zTE1 * (1 - zTH0) * zTH0);
+  double i0p = k0p * sqrt(zTEE * (1 - zTH3) * zTH3);
   k.Rctn = r.R * cc.T / (r.F * i0n);
   k.Rctp = r.R * cc.T / (r.F * i0p);
   k.dUn0 = cc.et.f(0, EF_DU, zTH0);
@@ -785,8 +808,9 @@ __device__ __forceinline__ double chat0(const KRom &r, const ChatK &K) {
 // Voltage Jacobian rows of the 4 corners.
 template <int NZ>
 __device__ __forceinline__ void get_chatv(const KRom &r, const CellCtx &cc, const XI &xi, double xSOC, double zTE1,
-                                          double zTH0, double zTEE, double zTH3, double Chat[4][NX], double &Chat0) {
-  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
+                                          double zTH0, double zTEE, double zTH3, double Chat[4][NX], double &Chat0,
+                                          const KR *kr = nullptr) {
+  const ChatK K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3, kr);
 #pragma unroll
   for (int j = 0; j < 4; ++j) chat_row(r, K, cc.L + xi.m[j] * cc.stride, xi.g[j], Chat[j]);
   Chat0 = chat0(r, K);
@@ -798,9 +822,9 @@ struct BoundK {
   double C0, r0n, r0p, dUn, dUp;
 };
 __device__ __forceinline__ BoundK bound_k(const KRom &r, const CellCtx &cc, double xSOC, double zTE1, double zTH0,
-                                          double zTEE, double zTH3) {
+                                          double zTEE, double zTH3, const KR *kr = nullptr) {
   BoundK b;
-  b.K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3);
+  b.K = chat_k(r, cc, xSOC, zTE1, zTH0, zTEE, zTH3, kr);
   b.C0 = chat0(r, b.K);
   b.r0n = -r.Ts * b.K.dn / (3600 * r.Q);  // iterEKF.m:562-565
   b.r0p = -r.Ts * b.K.dp / (3600 * r.Q);
@@ -857,7 +881,7 @@ __device__ __forceinline__ int corner_max(const XI &xi, int *mmax = nullptr) {
 template <int NZ>
 __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, const XI &xi, const double *zr,
                                              double Zsoc, double TK, Lin &L, double xend, const double (&xm)[NX],
-                                             bool use_xm) {
+                                             bool use_xm, const KR *kr = nullptr) {
   int m;
   (void)corner_max(xi, &m);
   const double *Cm = cc.L + m * cc.stride;
@@ -882,9 +906,20 @@ __device__ __forceinline__ void mats_handler(const KRom &r, const CellCtx &cc, c
   ETab et = cc.et;
   et.bracket(TK);  // EKFmatsHandler.m:53: TK = Tk + 273.15
   double SOCnAvg = et.soc(0, Zsoc), SOCpAvg = et.soc(1, Zsoc);  // EKFmatsHandler.m:57-58
-  double i0n = et.f(0, EF_K0, SOCnAvg) * sqrt(zr[R_TE1] * (1 - zr[R_TH0]) * zr[R_TH0]);
-  double i0p = et.f(1, EF_K0, SOCpAvg) * sqrt(zr[R_TEE] * (1 - zr[R_TH3]) * zr[R_TH3]);
-  const double Rfn = et.f(0, EF_RF, SOCnAvg), Rfp = et.f(1, EF_RF, SOCpAvg);  // EKFmatsHandler.m:68-69
+  double k0n, k0p, Rfn, Rfp;  // EKFmatsHandler.m:60-61,68-69 (the second getVariables' when its averages)
+  if (kr_hit(kr, TK, SOCnAvg, SOCpAvg)) {
+    k0n = kr->k0n;
+    k0p = kr->k0p;
+    Rfn = kr->rfn;
+    Rfp = kr->rfp;
+  } else {
+    k0n = et.f(0, EF_K0, SOCnAvg);
+    k0p = et.f(1, EF_K0, SOCpAvg);
+    Rfn = et.f(0, EF_RF, SOCnAvg);
+    Rfp = et.f(1, EF_RF, SOCpAvg);
+  }
+  double i0n = k0n * sqrt(zr[R_TE1] * (1 - zr[R_TH0]) * zr[R_TH0]);
+  double i0p = k0p * sqrt(zr[R_TEE] * (1 - zr[R_TH3]) * zr[R_TH3]);
 #pragma unroll
   for (int k = 0; k < NX; ++k)
     L.Cv[k] = Rfp * Cm[R_IFDL3 * NX + k] - Rfn * Cm[R_IFDL0 * NX + k] + Cm[R_PHIE * NX + k];
@@ -2563,6 +2598,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   double Z[NZ];
   double xmax[NX];         // fused step: EKFmatsHandler's corner xhat, from the EKF's registers
   bool have_xmax = false;
+  KR kr2{};               // the second getVariables' k0 / Rf (EKFmatsHandler reuses them)
+  bool have_kr2 = false;
   double vhat = 0.0, Zsoc = 0.0;
   XI xi;
   double ik = 0.0, vk = 0.0;
@@ -2781,7 +2818,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
             for (int k = 0; k < NX; ++k) xr[j][k] = xr[i][k];
     }
     STAMP(3);
-    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr);
+    KR kr1;
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xr, 0, &kr1);
     STAMP(4);
     if (st & ST_ERROR) {
       s.status[c] = st;
@@ -2792,7 +2830,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     }
     __builtin_amdgcn_sched_barrier(0);
     double ChatV[4][NX], C0;
-    get_chatv<NZ>(r, cc, xi, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0);
+    get_chatv<NZ>(r, cc, xi, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], ChatV, C0,
+                  &kr1);
     if (t) replay_S(Sr[0], cc.L + xi.m[0] * cc.stride + NZ * NX + NZ, tsj[0], t, cf.SigmaW);
     double St[4], Lg[4][NX];
 #pragma unroll
@@ -2866,7 +2905,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int j = 0; j < 4; ++j) load_x(cc.erec + (size_t)xi.m[j] * REC, xu[j]);
     }
     STAMP(7);
-    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xu);
+    vhat = get_vars<NZ>(r, cc, xi, ik, x0, SOC0, warn, st, Z, Zsoc, xu, 0, &kr2);
+    have_kr2 = true;
     const int jm = corner_max(xi);
 #pragma unroll
     for (int k = 0; k < NX; ++k) xmax[k] = jm == 0 ? xu[0][k] : jm == 1 ? xu[1][k] : jm == 2 ? xu[2][k] : xu[3][k];
@@ -2890,7 +2930,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
         bd[(BD_G + j) * n + c] = xi.g[j];
         bd[(BD_M + j) * n + c] = xi.m[j];
       }
-      const BoundK b = bound_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3]);
+      const BoundK b =
+          bound_k(r, cc, SOC0 - x0 * (r.Ts / (3600 * r.Q)), Z[R_TE1], Z[R_TH0], Z[R_TEE], Z[R_TH3], &kr2);
 #pragma unroll
       for (int i = 0; i < 11; ++i) bd[(BD_K + i) * n + c] = bound_field(b, i);
       bd[BD_S0 * n + c] = S0;
@@ -2936,7 +2977,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) { xi.m[j] = io.xm_in[c * 4 + j]; xi.g[j] = io.xg_in[c * 4 + j]; }
     }
-    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0, xmax, fused && (PARTS & P_EKF) && have_xmax);
+    mats_handler<NZ>(r, cc, xi, zr, Zsoc, Tc + 273.15, L, MB ? s.x0[c] : 0.0, xmax, fused && (PARTS & P_EKF) && have_xmax,
+                     fused && (PARTS & P_EKF) && have_kr2 ? &kr2 : nullptr);
     if (io.lin_out) lin_store(io.lin_out + c * 35, L);
     if (io.x_out)
 #pragma unroll

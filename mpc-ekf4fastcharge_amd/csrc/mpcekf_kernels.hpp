@@ -216,6 +216,9 @@ int launch_predmat_wide(int64_t n, int Np, int Nc, const double *a, const double
                         double *G, void *stream);
 int launch_constraints_wide(const KCfg &c, int Np, int Nc, int64_t n, const double *lin, const double *uk_1,
                             const double *soc_k1, double *M, double *gam, void *stream);
+// selected columns of [n][stride] records to / from a compact [n][k] buffer (mpcekf_io.hip)
+int launch_cols(double *rec, int64_t n, int stride, const int *slots, int k, double *compact, bool scatter,
+                void *stream);
 int cell_lds_bytes(const KRom &r);
 int bounds_lds_bytes(const KRom &r);
 int plant_lds_bytes(const KRom &r);

@@ -206,8 +206,8 @@ static void tidx(const orc_rom *r, double T, int *j, double *g) {
   *j = k;
   *g = (Tc - r->TK[k]) / (r->TK[k + 1] - r->TK[k]);
 }
-/* ABI v3 row: the polynomial of theta's interval, Horner over 6 coefficients in
- * s = t - i (rom.py interp_poly, mpcekf_kernels.hip tabp) */
+/* ABI v3 row: the polynomial of theta's interval, Horner with explicit fma over 6
+ * coefficients in s = t - i (mpcekf_kernels.hip tabp; rom.py interp_poly without fma) */
 static double tab_poly(const double *c, int n, double x) {
   if (x != x) return NAN;
   double xc = fmin(fmax(x, 0.0), 1.0);
@@ -217,11 +217,11 @@ static double tab_poly(const double *c, int n, double x) {
   double s = t - (double)i;
   const double *p = c + (size_t)i * NPOLY;
   double v = p[5];
-  v = p[4] + s * v;
-  v = p[3] + s * v;
-  v = p[2] + s * v;
-  v = p[1] + s * v;
-  return p[0] + s * v;
+  v = fma(s, v, p[4]);
+  v = fma(s, v, p[3]);
+  v = fma(s, v, p[2]);
+  v = fma(s, v, p[1]);
+  return fma(s, v, p[0]);
 }
 /* Defined exp (the v3 Arrhenius factor; rom.py dexp, mpcekf_kernels.hip dexp): fdlibm's
  * reduction x = k ln2 + r (k = floor(x / ln2 + 1/2)) and its rational form for exp(r);

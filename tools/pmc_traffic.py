@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--np", type=int, default=5)
     ap.add_argument("--bounds", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--rom-lookup", default="quintic", help="when the bench line does not say (bench.py default)")
     a = ap.parse_args()
     base = a.base
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
@@ -75,7 +76,20 @@ def main():
         bid = importlib.import_module("mpc-ekf4fastcharge_amd._lib").load().mpcekf_build_id().decode()
     fetch = read_counter(os.path.join(base, "fetch"), "FETCH_SIZE")
     write = read_counter(os.path.join(base, "write"), "WRITE_SIZE")
-    out = {"unit": "bytes per launch", "build_id": bid, "cells": a.cells, "Np": a.np,
+    # the electrode tables the profiled bench ran (its JSON line's config.rom_lookup; bench.py
+    # attaches these figures only to a run with the same tables)
+    lookup = a.rom_lookup
+    for root, _, files in os.walk(base):
+        for fn in files:
+            if fn.endswith((".json", ".log")):
+                try:
+                    with open(os.path.join(root, fn)) as f:
+                        for line in f:
+                            if line.startswith("{") and '"rom_lookup"' in line:
+                                lookup = json.loads(line)["config"].get("rom_lookup", lookup)
+                except (OSError, ValueError, KeyError):
+                    pass
+    out = {"unit": "bytes per launch", "build_id": bid, "cells": a.cells, "Np": a.np, "rom_lookup": lookup,
            "bounds": a.bounds, "steps": a.steps, "fetch_kib_raw": fetch, "write_kib_raw": write,
            "correction": "reads x2 (gfx950 FETCH_SIZE halves 16-B/lane streaming reads)",
            "per_launch_bytes": {}}
