@@ -485,7 +485,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   // Model rows and tables staged in LDS when they fit; otherwise (NM above ~75 at the
   // default grid, or MPCEKF_ROM_GLOBAL=1) only the tables are, and the model rows are read
   // from the global blob (L2-resident).  Same arithmetic either way.
-  auto lds_need = [&]() { return std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r)), plant_lds_bytes(r)); };
+  auto lds_need = [&]() { return std::max(std::max(cell_lds_bytes(r), bounds_lds_bytes(r, 1024)), plant_lds_bytes(r)); };
   const char *gev = getenv("MPCEKF_ROM_GLOBAL");
   r.rom_global = gev && atoi(gev) == 1;
   // the plant's extras (res0 column, Cdleff tables) only while the whole cell blob still

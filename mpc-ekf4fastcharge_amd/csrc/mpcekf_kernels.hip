@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 #include "mpcekf_kernels.hpp"
@@ -61,6 +62,10 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #endif
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
+#endif
+// v3 lookups: one code path per call site (T-invariant rows read twice and self-blended)
+#ifndef MPCEKF_PL_UNIFIED
+#define MPCEKF_PL_UNIFIED 0
 #endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
@@ -194,7 +199,8 @@ __device__ __forceinline__ double tabp(const double *c, int n, double x, int ist
   return horner6(p[0], p[1], p[2], s);
 }
 // two adjacent rows of interval i (the T bracket): a from c + i * istride, b KPOLY after
-__device__ __forceinline__ void tabp2(const double *c, int n, double x, int istride, double &a, double &b) {
+__device__ __forceinline__ void tabp2(const double *c, int n, double x, int istride, double &a, double &b,
+                                      int ro = KPOLY) {
   if (x != x) {
     a = b = __builtin_nan("");
     return;
@@ -202,7 +208,8 @@ __device__ __forceinline__ void tabp2(const double *c, int n, double x, int istr
   double s;
   const int i = tab_interval(n, x, s);
   const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
-  const double2 a01 = p[0], a23 = p[1], a45 = p[2], b01 = p[3], b23 = p[4], b45 = p[5];
+  const double2 *q = reinterpret_cast<const double2 *>(c + (size_t)i * istride + ro);
+  const double2 a01 = p[0], a23 = p[1], a45 = p[2], b01 = q[0], b23 = q[1], b45 = q[2];
   a = horner6(a01, a23, a45, s);
   b = horner6(b01, b23, b45, s);
 }
@@ -257,7 +264,19 @@ struct ETab {
       const bool one = (r->tconst >> (fn * 2 + side)) & 1;
       const double *base = r->poly + r->poff[fn][side];
       double a;
+#if MPCEKF_PL_UNIFIED
+      // one code path per call site: a T-invariant (or single-temperature) function reads its
+      // row twice and blends it with itself (a + g (a - a) = a for a finite a)
+      {
+        const int rs = one ? KPOLY : nte * KPOLY, ro = (one || nte == 1) ? 0 : KPOLY;
+        double c;
+        tabp2(base + (one ? 0 : j * KPOLY), nth, th, rs, a, c, ro);
+        a = a + g * (c - a);
+      }
+      if (false) {
+#else
       if (one || nte == 1) {
+#endif
         a = tabp(base, nth, th, KPOLY);
       } else {
         double c;
@@ -3915,10 +3934,37 @@ int launch_init_state(int64_t n, int NM, double *ekf, double *bigx, const double
 }
 static int grid_for(int64_t n, int block) { return (int)((n + block - 1) / block); }
 
+// Compute units of the current device (cached per device).
+static int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+// Block size of a kernel whose blocks each take a CU's LDS (k_cell's ROM blob, k_hild's slots,
+// k_bounds' model blob), lpc lanes per cell, launch bound maxb: the fewest 64-lane waves per
+// block that still cover the batch in one round of blocks over the CUs.  A small batch then
+// runs one wave per CU (configs[1]: 16 CUs) instead of four waves on each of n/256 CUs sharing
+// the CU's LDS, L1 and address units; from 64 x #CUs x 4 lanes up it is maxb as before.
+// MPCEKF_SPREAD=0: always maxb (A/B; results identical, every lane's arithmetic is its own).
+static int spread_block(int64_t n, int lpc, int maxb) {
+  const char *e = std::getenv("MPCEKF_SPREAD");  // read per launch: tests toggle it in-process
+  if (e && std::atoi(e) == 0) return maxb;
+  const int64_t lanes = n * lpc, cus = cu_count();
+  int64_t b = (lanes + cus - 1) / cus;
+  b = (b + 63) / 64 * 64;
+  return (int)(b < 64 ? 64 : b > maxb ? maxb : b);
+}
+
 int cell_lds_bytes(const KRom &r) {
   return (int)((r.cell_len - (r.rom_global ? r.cell_tab : 0) + 1) * sizeof(double));
 }
-int bounds_lds_bytes(const KRom &r) { return (bounds_c0_base(r) + BOUNDS_BLOCK / 4 * 8) * (int)sizeof(double); }
+int bounds_lds_bytes(const KRom &r, int block) { return (bounds_c0_base(r) + block / 4 * 8) * (int)sizeof(double); }
 int plant_lds_bytes(const KRom &r) {
   return (int)((r.plant_len - (r.rom_global ? r.plant_tab : 0) + 1) * sizeof(double));
 }
@@ -3983,14 +4029,16 @@ int launch_bulk(const KRom &r, const KCfg &c, const KState &s, const double *iap
 template <int NZ, int PARTS, bool MB, bool GR, bool PL>
 static void launch_cell_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
+  const int block = spread_block(s.n, 1, 256);
   int lds = cell_lds_bytes(r);
-  if (io.hild) lds = lds > (int)(4 * HILD_LDS_PER_WAVE) ? lds : (int)(4 * HILD_LDS_PER_WAVE);  // the Hildreth slots
+  const int hl = block / 64 * (int)HILD_LDS_PER_WAVE;
+  if (io.hild) lds = lds > hl ? lds : hl;  // the Hildreth slots
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_cell<NZ, PARTS, MB, GR, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB, GR, PL>), dim3(grid_for(s.n, 256)), dim3(256), lds, st, r, c, s, io);
+  hipLaunchKernelGGL((k_cell<NZ, PARTS, MB, GR, PL>), dim3(grid_for(s.n, block)), dim3(block), lds, st, r, c, s, io);
 }
 
 template <int NZ, int PARTS, bool MB>
@@ -4076,13 +4124,13 @@ int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
 template <int NZ, bool GR>
 static void launch_bounds_g(const KRom &r, const KState &s, const double *bnd, double *zbk, hipStream_t st) {
   static bool attr = false;
-  int lds = bounds_lds_bytes(r);
+  const int block = spread_block(s.n, 4, BOUNDS_BLOCK);
+  int lds = bounds_lds_bytes(r, block);
   if (!attr) {
     (void)hipFuncSetAttribute((const void *)k_bounds<NZ, GR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_bounds<NZ, GR>), dim3(grid_for(4 * s.n, BOUNDS_BLOCK)), dim3(BOUNDS_BLOCK), lds, st, r, s, bnd,
-                     zbk);
+  hipLaunchKernelGGL((k_bounds<NZ, GR>), dim3(grid_for(4 * s.n, block)), dim3(block), lds, st, r, s, bnd, zbk);
 }
 
 template <int NZ>
@@ -4104,9 +4152,9 @@ int launch_bounds(const KRom &r, const KState &s, const double *bnd, double *zbk
   return (int)hipGetLastError();
 }
 
-static int hild_lds_bytes() {  // 4 waves per block; one block per CU (147 KiB of 160)
+static int hild_lds_bytes(int block = 256) {  // 4 waves per 256-thread block; one block per CU (147 KiB of 160)
   static_assert(4 * HILD_LDS_PER_WAVE <= 160 * 1024, "Hildreth slots exceed the LDS");
-  return 4 * HILD_LDS_PER_WAVE;
+  return block / 64 * HILD_LDS_PER_WAVE;
 }
 
 size_t hildreth_any_scratch(int64_t n, int Nc, int ncon) { return (size_t)n * (size_t)(ncon * Nc + 2 * ncon); }
@@ -4126,7 +4174,9 @@ int launch_hild(const KCfg &c, const KState &s, const KIO &io, void *stream) {
     (void)hipFuncSetAttribute((const void *)k_hild, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, 256)), dim3(256), hild_lds_bytes(), (hipStream_t)stream, c, s, io);
+  const int block = spread_block(s.n, 1, 256);
+  hipLaunchKernelGGL(k_hild, dim3(grid_for(s.n, block)), dim3(block), hild_lds_bytes(block), (hipStream_t)stream, c, s,
+                     io);
   if (!MPCEKF_HILD_INLINE_SLOW) {
     const int gs = grid_for(s.n, 64) < 256 ? grid_for(s.n, 64) : 256;
     hipLaunchKernelGGL(k_hild_slow, dim3(gs), dim3(64), HILD_LDS_PER_WAVE, (hipStream_t)stream, c, s, io);

@@ -220,7 +220,7 @@ int launch_constraints_wide(const KCfg &c, int Np, int Nc, int64_t n, const doub
 int launch_cols(double *rec, int64_t n, int stride, const int *slots, int k, double *compact, bool scatter,
                 void *stream);
 int cell_lds_bytes(const KRom &r);
-int bounds_lds_bytes(const KRom &r);
+int bounds_lds_bytes(const KRom &r, int block);
 int plant_lds_bytes(const KRom &r);
 
 }  // namespace mk

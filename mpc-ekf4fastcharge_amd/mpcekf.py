@@ -372,11 +372,15 @@ class Context:
         check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin)))
         return lin
 
-    def lin_fields(self, slots, set=None):
+    def lin_fields(self, slots, set=None, out=None):
         """Slots (MPCEKF_LIN_*) of the device-resident records of the last EKFmatsHandler:
-        [n, len(slots)]; ``set`` [n, len(slots)] is written into them first."""
+        [n, len(slots)]; ``set`` [n, len(slots)] is written into them first.  ``out``: a
+        C-contiguous float64 [n, len(slots)] array to fill instead of a new one."""
         sl = np.ascontiguousarray(slots, dtype=np.int32)
-        out = np.empty((self.n, sl.size))
+        if out is None:
+            out = np.empty((self.n, sl.size))
+        elif out.shape != (self.n, sl.size) or out.dtype != np.float64 or not out.flags.c_contiguous:
+            raise ValueError(f"lin_fields: out must be a C-contiguous float64 array of shape {(self.n, sl.size)}")
         st = None if set is None else np.ascontiguousarray(set, dtype=np.float64)
         check(self.L.mpcekf_lin_fields(self.h, iptr(sl), int(sl.size), dptr(st), dptr(out)))
         return out

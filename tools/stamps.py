@@ -2,7 +2,10 @@
 """Where k_cell's time goes: per-section shader cycles (profiling build).
 
     python mpc-ekf4fastcharge_amd/build.py --stamps
-    MPCEKF_LIB=mpc-ekf4fastcharge_amd/_build/libmpcekf_stamps.so python tools/stamps.py [ncells] [steps]
+    MPCEKF_LIB=mpc-ekf4fastcharge_amd/_build/libmpcekf_stamps.so python tools/stamps.py [ncells] [steps] [lookup]
+
+lookup: the ROM's electrode tables (rom.make_synth_rom: "linear" v2 tables, "quintic" /
+"cubic" v3 polynomials; default linear, the round-4 figures).
 
 Runs the bench workload; after each step k in a sample it reads the stamps and
 reports the median over waves of each section's cycles (max over the wave's
@@ -23,7 +26,8 @@ NAMES = ["plant (simStep) + scalar loads + lockout", "get_xind1", "catch-up1", "
          "get_xind2 + catch-up2", "get_vars2", "boundzk record", "mats_handler", "mpc_setup"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
-rom = P.make_synth_rom()
+lookup = sys.argv[3] if len(sys.argv) > 3 else "linear"
+rom = P.make_synth_rom(lookup=lookup)
 soc0, tc = bench.batch_inputs(n)
 ctx = M.Context(rom, n, M.make_config(bounds=True))
 ctx.init_cells(soc0, tc)
@@ -44,7 +48,7 @@ for k in range(steps):
         pacc.append(np.median(dp, axis=1))
 a = np.array(acc)
 tot = a.sum(1)
-print(f"k_cell sections (median over waves, shader cycles; {len(a)} sampled steps, total median {np.median(tot):.0f}):")
+print(f"k_cell sections ({lookup} tables; median over waves, shader cycles; {len(a)} sampled steps, total median {np.median(tot):.0f}):")
 for i, nm in enumerate(NAMES):
     print(f"  {nm:44s} {np.median(a[:, i]):9.0f}  ({100 * np.median(a[:, i] / tot):4.1f} %)")
 p = np.array(pacc)
