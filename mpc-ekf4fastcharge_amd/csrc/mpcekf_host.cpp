@@ -79,7 +79,7 @@ struct mpcekf_ctx {
   double *d_xg = nullptr;
   bool split_cell = false;    // fused step: k_cell as two kernels (MPCEKF_SPLIT_CELL=1; slower, 0.125 vs 0.118 ms)
   bool quad = false;          // fused step: iterEKF in k_ekf4 (lane quad per cell), then k_cell<P_MPC>
-  int ekf4_block = 512;       // k_ekf4 block size (MPCEKF_EKF4_BLOCK=1024: 4 waves per SIMD, 128 VGPRs)
+  int ekf4_block = 256;       // k_ekf4 launch bound (MPCEKF_EKF4_BLOCK=512 / 1024: 256 / 128 VGPRs)
   int *d_ts = nullptr;        // deferred time update: ts_ekf, ts_plant [n][NM]
   double *d_hist = nullptr;   // input rings hist_p, hist_u [LAZY_H][n]
   long long *d_stamps = nullptr;  // profiling builds: k_cell section stamps
@@ -349,6 +349,9 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     r.perm[q] = (short)perm[q];
   }
   std::memcpy(r.flags, flags, sizeof flags);
+  for (int q = 0; q < nz && q < 32; ++q)  // nz <= nzp <= 32 (checked above)
+    for (int b = 0; b < 8; ++b)
+      if (flags[q] >> b & 1) r.fmask[b] |= 1u << q;
   std::memcpy(r.c0k, c0k, sizeof c0k);
   r.NM = NM; r.nT = nT; r.nZ = nZ; r.nz = nz; r.nzp = nzp;
   r.nth = R->tab_ntheta; r.nte = R->tab_ntemp;
@@ -373,11 +376,20 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     }
   // v3 device layout (mpcekf_kernels.hip ETab::f): per function and electrode the nte rows of
   // each theta interval adjacent, [nth-1][nte][KPOLY] (cubics padded with c4 = c5 = 0), or
-  // [nth-1][1][KPOLY] when every row is equal (tconst: no T blend, the same value); Uocp1 last
+  // [nth-1][1][KPOLY] when every row is equal (T-invariant: the row blended with itself, the
+  // same value); Uocp1 last
   std::vector<double> ptab;
   const int np = R->tab_npoly;
   const size_t nint = (size_t)(nth - 1);
-  r.tconst = 0;
+  // the kernels' lookup descriptors (mpcekf_kernels.hip etab_desc): per function and side
+  // Ea/R, (off, istride), (jstride, ro) in doubles of ptab; Uocp1 of each side last
+  double desc[12][KDESC] = {};
+  auto pack2 = [](long long lo, long long hi) {
+    const unsigned long long w = (unsigned long long)(uint32_t)lo | (unsigned long long)(uint32_t)hi << 32;
+    double d;
+    std::memcpy(&d, &w, sizeof d);
+    return d;
+  };
   auto add_poly = [&](const double *src, int rows) {  // src [rows][nth-1][np] (ABI order)
     for (size_t i = 0; i < nint; ++i)
       for (int j = 0; j < rows; ++j)
@@ -391,9 +403,13 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       bool same = nte > 1;
       for (int j = 1; j < nte && same; ++j)
         same = std::memcmp(src, src + (size_t)j * nint * np, nint * np * sizeof(double)) == 0;
-      if (same) r.tconst |= 1 << (fn * 2 + sd);
-      r.poff[fn][sd] = (long long)ptab.size();
-      add_poly(src, same ? 1 : nte);
+      double *d = desc[fn * 2 + sd];
+      const double ea = e->Ea[fn];
+      d[0] = ea != 0.0 ? ea / R->R : 0.0;  // oracle: (Ea / R) * (1/Tref - 1/T)
+      const int rows = same ? 1 : nte;
+      d[1] = pack2((long long)ptab.size(), (long long)rows * KPOLY);          // off, istride
+      d[2] = pack2(same ? 0 : KPOLY, (same || nte == 1) ? 0 : KPOLY);          // jstride, ro
+      add_poly(src, rows);
     }
   if (!poly)  // v2: [fn][side][nte][nth] in the LDS blob
     for (int fn = 0; fn < 5; ++fn)
@@ -403,17 +419,17 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       }
   if (poly)
     for (int sd = 0; sd < 2; ++sd) {
-      r.poff1[sd] = (long long)ptab.size();
+      desc[10 + sd][1] = pack2((long long)ptab.size(), KPOLY);
       add_poly(els[sd]->Uocp1_p, 1);
     }
+  if (poly) {
+    if (ptab.size() >= (size_t)INT32_MAX) return fail(MPCEKF_E_ROM, "rom: v3 tables exceed 2^31 doubles");
+    for (auto &d : desc) tabs.insert(tabs.end(), d, d + KDESC);
+  }
   r.npoly = poly ? KPOLY : 0;
   r.arr = 0;
   for (int f = 0; f < 5; ++f)
-    for (int sd = 0; sd < 2; ++sd) {
-      const double ea = els[sd]->Ea[f];
-      r.ear[f][sd] = ea != 0.0 ? ea / R->R : 0.0;  // oracle: (Ea / R) * (1/Tref - 1/T)
-      r.arr |= ea != 0.0;
-    }
+    for (int sd = 0; sd < 2; ++sd) r.arr |= poly && els[sd]->Ea[f] != 0.0;
   // k_cell / k_bounds need no Cdleff table, unless k_cell also runs the plant (cell_plant)
   const char *cpe = getenv("MPCEKF_CELL_PLANT");
   bool cell_plant = !(cpe && atoi(cpe) == 0);
@@ -572,15 +588,24 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   }
   // MPCEKF_SPLIT_CELL=1: the fused step's k_cell as two kernels (results identical).
   if (const char *e = std::getenv("MPCEKF_SPLIT_CELL")) X->split_cell = std::atoi(e) != 0;
-  // k_ekf4 (a lane quad per cell for iterEKF; needs four distinct corners: nT > 1, nZ > 1)
-  // is kept as an option, off by default: measured against k_cell it loses at every batch
-  // size (0.080 vs 0.075 ms at 1,024 cells, 0.098 vs 0.090 at 16,384, 0.20 vs 0.11 at 65,536;
-  // profiles/r02g_*): the per-cell scalar work is replicated four times and the 512-thread
-  // blocks run two rounds per CU.  MPCEKF_QUAD=1 turns it on (results identical).
-  const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide && !rom->tab_npoly;
-  X->quad = false;
+  // k_ekf4 (a lane quad per cell for iterEKF; needs four distinct corners: nT > 1, nZ > 1).
+  // Round 2 measured it against k_cell under 128 / 256-register budgets (512- / 1024-thread
+  // blocks): it lost at every batch size (0.080 vs 0.075 ms at 1,024 cells, 0.20 vs 0.11 at
+  // 65,536; profiles/r02g_*).  Round 5's small-batch mapping is the 256-thread instantiation
+  // (512 registers, no spills) spread one wave per CU, chosen for batches up to
+  // MPCEKF_QUAD_MAX cells (results identical whichever path runs).  MPCEKF_QUAD=0/1 forces it.
+  const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide;
+  {
+    int64_t quad_max = 0;
+    if (const char *e = std::getenv("MPCEKF_QUAD_MAX")) quad_max = std::atoll(e);
+    X->quad = quad_ok && ncells <= quad_max;
+  }
+  X->ekf4_block = 256;
   if (const char *e = std::getenv("MPCEKF_QUAD")) X->quad = quad_ok && std::atoi(e) != 0;
-  if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) X->ekf4_block = std::atoi(e) == 1024 ? 1024 : 512;
+  if (const char *e = std::getenv("MPCEKF_EKF4_BLOCK")) {
+    const int v = std::atoi(e);
+    X->ekf4_block = v == 1024 || v == 512 ? v : 256;
+  }
   if (const char *e = std::getenv("MPCEKF_GRAPH")) X->graph = std::atoi(e) != 0;  // as mpcekf_set_graph
   // MPCEKF_FLUSH_ROLL=1: the rolling flush schedule (results identical)
   if (const char *e = std::getenv("MPCEKF_FLUSH_ROLL")) X->flush_roll = std::atoi(e) != 0;

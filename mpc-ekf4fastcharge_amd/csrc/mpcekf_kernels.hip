@@ -63,10 +63,6 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
 #endif
-// v3 lookups: one code path per call site (T-invariant rows read twice and self-blended)
-#ifndef MPCEKF_PL_UNIFIED
-#define MPCEKF_PL_UNIFIED 0
-#endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
@@ -239,12 +235,19 @@ __device__ __forceinline__ double dexp(double x) {
 // carries it (k_cell / k_bounds never read Cdleff).  A cell's temperature bracket
 // (j, g) is found once per step (bracket); a lookup is then the theta interpolation of
 // rows j and j + 1 and a + g (b - a), the sequence of oracle/mpcekf_oracle.c tab2/tidx.
-// ABI v3 tables (KRom::npoly): the LDS header holds no Uocp1 and no 2-D tables follow;
-// the rows are polynomials in KRom::poly ([EF_*][side][nte][nth-1][KPOLY], then Uocp1
-// [side][nth-1][KPOLY]), and a function with KRom::ear != 0 is multiplied by its
-// Arrhenius factor dexp(Ea/R (1/Tref - 1/T)).
+// ABI v3 tables (KRom::npoly): the LDS header holds no Uocp1 and no 2-D tables follow
+// but the lookup descriptors; the rows are polynomials in KRom::poly, and a function with
+// Ea != 0 is multiplied by its Arrhenius factor dexp(Ea/R (1/Tref - 1/T)).
+// permuted row q carries the (single-bit) flag G: bit q of that flag's row mask
+__device__ __forceinline__ bool rowf(const KRom &r, int q, unsigned G) {
+  return (r.fmask[__builtin_ctz(G)] >> q) & 1u;
+}
+
 enum { EF_U = 0, EF_DU, EF_K0, EF_RF, EF_CDL, NEF };
 __host__ __device__ constexpr int etab_header(int nth) { return 2 * nth + 5 * MAXTT; }
+// v3: the 12 lookup descriptors after the soc ends (d = fn * 2 + side, Uocp1 10 + side),
+// KDESC doubles each: Ea/R, then int32 pairs (off, istride), (jstride, ro) as raw bits
+__host__ __device__ constexpr int etab_desc(int hn) { return 2 * hn + 5 * MAXTT; }
 struct ETab {
   const double *b;  // LDS base of the tables
   const KRom *r;    // v3: the polynomial table and the Arrhenius energies
@@ -257,33 +260,23 @@ struct ETab {
   double xa;        // v3: 1/Tref - 1/T of this cell-step (T unclamped)
   // v3 device layout (host build_rom): per function and electrode, interval-major with the
   // nte temperature rows of an interval adjacent, [fn][side][nth-1][nte][KPOLY], so the two
-  // rows of a bracket are one 96-byte span; a T-invariant function (KRom::tconst: all rows
-  // equal, e.g. an exact Arrhenius one) keeps one row, [nth-1][1][KPOLY]; Uocp1 last.
+  // rows of a bracket are one 96-byte span; a T-invariant function (all rows equal, e.g. an
+  // exact Arrhenius one) keeps one row, [nth-1][1][KPOLY]; Uocp1 last.  Where each function's
+  // rows are and its Ea/R come from its descriptor in the LDS header (etab_desc): values in
+  // VGPRs read at the lookup, so a kernel holds no per-function scalars (the 2 x 5 offsets
+  // and energies as kernel arguments cost ~1,100 SGPR-spill reloads in k_cell).  One code
+  // path: the rows of interval i at bracket j are at off + j jstride + i istride and + ro
+  // (a T-invariant or single-temperature function: jstride = ro = 0, its row blended with
+  // itself, a + g (a - a) = a, oracle tab2)
   __device__ __forceinline__ double f(int side, int fn, double th) const {
     if (pl) {
-      const bool one = (r->tconst >> (fn * 2 + side)) & 1;
-      const double *base = r->poly + r->poff[fn][side];
-      double a;
-#if MPCEKF_PL_UNIFIED
-      // one code path per call site: a T-invariant (or single-temperature) function reads its
-      // row twice and blends it with itself (a + g (a - a) = a for a finite a)
-      {
-        const int rs = one ? KPOLY : nte * KPOLY, ro = (one || nte == 1) ? 0 : KPOLY;
-        double c;
-        tabp2(base + (one ? 0 : j * KPOLY), nth, th, rs, a, c, ro);
-        a = a + g * (c - a);
-      }
-      if (false) {
-#else
-      if (one || nte == 1) {
-#endif
-        a = tabp(base, nth, th, KPOLY);
-      } else {
-        double c;
-        tabp2(base + j * KPOLY, nth, th, nte * KPOLY, a, c);
-        a = a + g * (c - a);
-      }
-      const double ear = r->ear[fn][side];
+      const double *dp = b + etab_desc(hn) + (fn * 2 + side) * KDESC;
+      const double ear = dp[0];
+      const long long w0 = __double_as_longlong(dp[1]), w1 = __double_as_longlong(dp[2]);
+      const int off = (int)w0, istr = (int)(w0 >> 32), jstr = (int)w1, ro = (int)(w1 >> 32);
+      double a, c;
+      tabp2(r->poly + off + j * jstr, nth, th, istr, a, c, ro);
+      a = a + g * (c - a);
       if (ear != 0.0) a = a * dexp(ear * xa);
       return a;
     }
@@ -294,7 +287,10 @@ struct ETab {
     return a + g * (c - a);
   }
   __device__ __forceinline__ double u1(int side, double th) const {
-    if (pl) return tabp(r->poly + r->poff1[side], nth, th, KPOLY);
+    if (pl) {
+      const long long w0 = __double_as_longlong(b[etab_desc(hn) + (10 + side) * KDESC + 1]);
+      return tabp(r->poly + (int)w0, nth, th, (int)(w0 >> 32));
+    }
     return tabi(b + side * nth, nth, th);
   }
   __device__ __forceinline__ double tk(int i) const { return b[2 * hn + i]; }
@@ -700,61 +696,61 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   bool any = false;
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_NTH) { Z[q] = Z[q] + SOCnAvg; any |= Z[q] < 0; }
+    if (rowf(r, q, G_NTH)) { Z[q] = Z[q] + SOCnAvg; any |= Z[q] < 0; }
   if (any) {
     warn++;
 #pragma unroll
     for (int q = 0; q < NZ; ++q)
-      if ((r.flags[q] & G_NTH) && Z[q] < 0) Z[q] = 1e-6;
+      if ((rowf(r, q, G_NTH)) && Z[q] < 0) Z[q] = 1e-6;
   }
   any = false;
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_NTH) any |= Z[q] > 1;
+    if (rowf(r, q, G_NTH)) any |= Z[q] > 1;
   if (any) {
     warn++;
 #pragma unroll
     for (int q = 0; q < NZ; ++q)
-      if ((r.flags[q] & G_NTH) && Z[q] > 1) Z[q] = 1 - 1e-6;
+      if ((rowf(r, q, G_NTH)) && Z[q] > 1) Z[q] = 1 - 1e-6;
   }
   any = false;
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_PTH) { Z[q] = Z[q] + SOCpAvg; any |= Z[q] < 0; }
+    if (rowf(r, q, G_PTH)) { Z[q] = Z[q] + SOCpAvg; any |= Z[q] < 0; }
   if (any) {
     warn++;
 #pragma unroll
     for (int q = 0; q < NZ; ++q)
-      if ((r.flags[q] & G_PTH) && Z[q] < 0) Z[q] = 1e-6;
+      if ((rowf(r, q, G_PTH)) && Z[q] < 0) Z[q] = 1e-6;
   }
   any = false;
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_PTH) any |= Z[q] > 0.998;
+    if (rowf(r, q, G_PTH)) any |= Z[q] > 0.998;
   if (any) {
     warn++;
 #pragma unroll
     for (int q = 0; q < NZ; ++q)
-      if ((r.flags[q] & G_PTH) && Z[q] > 0.998) Z[q] = 0.998;
+      if ((rowf(r, q, G_PTH)) && Z[q] > 0.998) Z[q] = 0.998;
   }
   double Un = cc.et.f(0, EF_U, SOCnAvg), Up = cc.et.f(1, EF_U, SOCpAvg);
 #pragma unroll
   for (int q = 0; q < NZ; ++q) {
-    if (r.flags[q] & G_NPHISE) Z[q] = Z[q] + Un;
-    if (r.flags[q] & G_PPHISE) Z[q] = Z[q] + Up;
+    if (rowf(r, q, G_NPHISE)) Z[q] = Z[q] + Un;
+    if (rowf(r, q, G_PPHISE)) Z[q] = Z[q] + Up;
   }
   double PhieTilde3 = Z[R_PHIE];
   double Phise0 = Z[R_PHISE0];
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_PHIE) {
-      if (r.flags[q] & G_PHIE0) Z[q] = 0 - Phise0;
+    if (rowf(r, q, G_PHIE)) {
+      if (rowf(r, q, G_PHIE0)) Z[q] = 0 - Phise0;
       else Z[q] = Z[q] - Phise0;
     }
   any = false;
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_THETAE) { Z[q] = Z[q] + 1; any |= Z[q] < 0; }
+    if (rowf(r, q, G_THETAE)) { Z[q] = Z[q] + 1; any |= Z[q] < 0; }
   if (any) {  // iterEKF.m:384-389 would raise a MATLAB error
     warn++;
     st |= ST_ERROR | ST_THETAE_NEG;
@@ -771,7 +767,7 @@ __device__ __forceinline__ double get_vars(const KRom &r, const CellCtx &cc, con
   double V = posEta3 - negEta0 + PhieTilde3 + Uocpp3 - Uocpn0 + (Rfp * Z[R_IFDL3] - Rfn * Z[R_IFDL0]);
 #pragma unroll
   for (int q = 0; q < NZ; ++q)
-    if (r.flags[q] & G_PPHIS) Z[q] = Z[q] + V;
+    if (rowf(r, q, G_PPHIS)) Z[q] = Z[q] + V;
   Zsoc = SOC0 - x0 * (r.Ts / (3600 * r.Q));
   return V;
 }
@@ -2495,7 +2491,7 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
   for (int k = 0; k < NX; ++k)
 #pragma unroll
     for (int l = k + 1; l < NX; ++l) S1b[pk(k, l)] = 2 * S1b[pk(k, l)];
-  const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+  const bool ph0pp = rowf(r, R_PHISE0, G_PPHIS);
   double ChV[4][NX], cph0[4][NX];
   const double *Cm[4];
 #pragma unroll
@@ -2513,20 +2509,20 @@ __device__ __forceinline__ void cell_bounds(const KRom &r, const CellCtx &cc, co
   const double cv1 = b.C0, cv2 = b.r0n, cv3 = b.r0p, cv4 = b.dUn * b.r0n, cv5 = b.dUp * b.r0p, cv6 = -b.dUn * b.r0n;
 #pragma unroll 1
   for (int q = 0; q < r.nz; ++q) {  // one form at a time
-    const unsigned f = r.flags[q];
+    const bool fpp = rowf(r, q, G_PPHIS), fph = rowf(r, q, G_PHIE);
     double sz = 0.0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const double g = xi.g[j];
       double row[NX];
-      if (f & G_PPHIS) {
+      if (fpp) {
 #pragma unroll
         for (int k = 0; k < NX; ++k) row[k] = __builtin_fma(g, Cm[j][q * NX + k], ChV[j][k]);
       } else {
 #pragma unroll
         for (int k = 0; k < NX; ++k) row[k] = g * Cm[j][q * NX + k];
       }
-      if (f & G_PHIE)
+      if (fph)
 #pragma unroll
         for (int k = 0; k < NX; ++k) row[k] = row[k] - cph0[j][k];
       sz = sz + qform(S1b, row);
@@ -2760,7 +2756,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
           double a = 0.0;
 #pragma unroll
           for (int j = 0; j < 4; ++j) a = a + xi.g[j] * cc.L[xi.m[j] * cc.stride + q * NX + k];
-          if (r.flags[q] & G_PPHIS) a = a + ChVz[k];
+          if (rowf(r, q, G_PPHIS)) a = a + ChVz[k];
           row[k] = a;
         }
       };
@@ -2771,7 +2767,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
       for (int q = 0; q < nz; ++q) {
         double row[NA6];
         chrow(q, row);
-        if (r.flags[q] & G_PHIE)
+        if (rowf(r, q, G_PHIE))
 #pragma unroll
           for (int k = 0; k < NX; ++k) row[k] = row[k] - ph0[k];
         row[NX] = c0v[r.c0k[q]];
@@ -3100,7 +3096,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 // 1024-thread blocks (256 cells): the ~130 KB ROM blob is staged once per CU and the
 // CU runs 4 waves per SIMD.
 // ---------------------------------------------------------------------------
-template <int NZ, int BLOCK, bool GR>
+template <int NZ, int BLOCK, bool GR, bool PL>
 __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, const KState s, const KIO io) {
   extern __shared__ double lds[];
   const int lo = GR ? r.cell_tab : 0;  // GR: model rows from the global blob (k_plant)
@@ -3125,7 +3121,7 @@ __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, con
   cc.stride = r.cell_stride;
   const double Tc = s.Tc[c];
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
-  cc.et = etab<false>(r, tb + r.cell_tab, cc.T);  // linear tables only (the host keeps v3 ROMs on k_cell)
+  cc.et = etab<PL>(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
   const int t = io.lazy_t;
   if (live && j == 0) s.hflag[c] = 0;
@@ -3343,7 +3339,7 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
   const double ChV0 = bd[BD_C0 * n + c];
   const double res0n = bd[BD_R0N * n + c], res0p = bd[BD_R0P * n + c];
   const double dUn = bd[BD_DUN * n + c], dUp = bd[BD_DUP * n + c];
-  const bool ph0pp = r.flags[R_PHISE0] & G_PPHIS;
+  const bool ph0pp = rowf(r, R_PHISE0, G_PPHIS);
   double cph0[NX];
 #pragma unroll
   for (int k = 0; k < NX; ++k) {
@@ -3376,9 +3372,9 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
 #pragma unroll
   for (int q = 0; q < NZ; ++q) {
     double row[NX];
-    const unsigned f = r.flags[q];
+    const bool fpp = rowf(r, q, G_PPHIS), fph = rowf(r, q, G_PHIE);
     // uniform branches (the empty volatile asm keeps them from being if-converted)
-    if (f & G_PPHIS) {
+    if (fpp) {
       asm volatile("");
 #pragma unroll
       for (int k = 0; k < NX; ++k) row[k] = __builtin_fma(g, Cm[q * NX + k], ChV[k]);
@@ -3387,7 +3383,7 @@ __global__ void __launch_bounds__(BOUNDS_BLOCK) k_bounds(const KRom r, const KSt
 #pragma unroll
       for (int k = 0; k < NX; ++k) row[k] = g * Cm[q * NX + k];
     }
-    if (f & G_PHIE) {
+    if (fph) {
       asm volatile("");
 #pragma unroll
       for (int k = 0; k < NX; ++k) row[k] = row[k] - cph0[k];
@@ -3977,7 +3973,8 @@ int launch_plant(const KRom &r, const KState &s, const double *iapp, double *vou
   const hipStream_t st = (hipStream_t)stream;
   const int lds = plant_lds_bytes(r);
   if (MPCEKF_PLANT_QUAD) {
-    const dim3 g(grid_for(4 * s.n, PLANT4_BLOCK)), b(PLANT4_BLOCK);
+    const int block = spread_block(s.n, 4, PLANT4_BLOCK);
+    const dim3 g(grid_for(4 * s.n, block)), b(block);
     if (r.npoly) {
       if (r.rom_global) hipLaunchKernelGGL((k_plant4<true, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
       else hipLaunchKernelGGL((k_plant4<false, true>), g, b, lds, st, r, s, iapp, vout, lazy_t, tc_in);
@@ -4087,35 +4084,53 @@ int launch_cell(const KRom &r, const KCfg &c, const KState &s, const KIO &io, vo
   return (int)hipGetLastError();
 }
 
-template <int NZ, int BLOCK, bool GR>
+template <int NZ, int BLOCK, bool GR, bool PL>
 static void launch_ekf4_g(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void *)k_ekf4<NZ, BLOCK, GR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)k_ekf4<NZ, BLOCK, GR, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((k_ekf4<NZ, BLOCK, GR>), dim3(grid_for(s.n * 4, BLOCK)), dim3(BLOCK), cell_lds_bytes(r), st, r,
-                     c, s, io);
+  // BLOCK is the launch bound; the 256 instantiation (512 registers, no spills) runs the
+  // fewest waves per block that cover the batch in one round of CUs (spread_block)
+  const int block = BLOCK == 256 ? spread_block(s.n, 4, 256) : BLOCK;
+  hipLaunchKernelGGL((k_ekf4<NZ, BLOCK, GR, PL>), dim3(grid_for(s.n * 4, block)), dim3(block), cell_lds_bytes(r), st,
+                     r, c, s, io);
 }
 
 template <int NZ, int BLOCK>
 static void launch_ekf4_t(const KRom &r, const KCfg &c, const KState &s, const KIO &io, hipStream_t st) {
+  if (r.npoly) {
+    if (r.rom_global)
+      launch_ekf4_g<NZ, BLOCK, true, true>(r, c, s, io, st);
+    else
+      launch_ekf4_g<NZ, BLOCK, false, true>(r, c, s, io, st);
+    return;
+  }
   if (r.rom_global)
-    launch_ekf4_g<NZ, BLOCK, true>(r, c, s, io, st);
+    launch_ekf4_g<NZ, BLOCK, true, false>(r, c, s, io, st);
   else
-    launch_ekf4_g<NZ, BLOCK, false>(r, c, s, io, st);
+    launch_ekf4_g<NZ, BLOCK, false, false>(r, c, s, io, st);
 }
 
-// block = 512 (128 cells, 256 VGPRs, 2 waves per SIMD) or 1024 (256 cells, 128 VGPRs, 4 waves per SIMD)
+// block = 256 (the small-batch mapping: 512 registers, one wave per SIMD, spread over the
+// CUs), 512 (128 cells, 256 VGPRs, 2 waves per SIMD) or 1024 (256 cells, 128 VGPRs, 4 waves
+// per SIMD)
 int launch_ekf4(const KRom &r, const KCfg &c, const KState &s, const KIO &io, void *stream, int block) {
   if (s.n == 0) return 0;
-  if (r.npoly) return -1;  // k_ekf4 reads the v2 linear tables only (the host keeps v3 ROMs on k_cell)
   hipStream_t st = (hipStream_t)stream;
-  const bool big = block == 1024;
   switch (r.nzp) {
-    case 26: big ? launch_ekf4_t<26, 1024>(r, c, s, io, st) : launch_ekf4_t<26, 512>(r, c, s, io, st); break;
-    case 32: big ? launch_ekf4_t<32, 1024>(r, c, s, io, st) : launch_ekf4_t<32, 512>(r, c, s, io, st); break;
+    case 26:
+      if (block == 1024) launch_ekf4_t<26, 1024>(r, c, s, io, st);
+      else if (block == 512) launch_ekf4_t<26, 512>(r, c, s, io, st);
+      else launch_ekf4_t<26, 256>(r, c, s, io, st);
+      break;
+    case 32:
+      if (block == 1024) launch_ekf4_t<32, 1024>(r, c, s, io, st);
+      else if (block == 512) launch_ekf4_t<32, 512>(r, c, s, io, st);
+      else launch_ekf4_t<32, 256>(r, c, s, io, st);
+      break;
     default: return -1;
   }
   return (int)hipGetLastError();

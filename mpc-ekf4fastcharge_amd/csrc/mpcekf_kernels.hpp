@@ -42,6 +42,11 @@ struct KRom {
   double Ts, Q, F, R, Rc, Tref;
   double th0n, th100n, th0p, th100p;  // theta0(), theta100() of the plant (OB_step.m:207-210)
   unsigned char flags[MAXROWS];   // per permuted row
+  // the same flags as one row mask per flag bit (bit q: permuted row q carries flag 1 << b):
+  // a kernel tests row q's flag with one scalar bit test on a mask (rowf), so the unrolled
+  // row loops keep 8 uniform words live instead of a byte per row (rows >= 32 never reach
+  // a kernel: nzp is 26 or 32)
+  unsigned fmask[8];
   unsigned char c0k[MAXROWS];     // getChatZ Chat0 kind per permuted row
   short perm[MAXROWS];            // permuted row -> ROM row
   // blobs end with: electrode tables (mpcekf_kernels.hip ETab; *_tablen doubles), Tpts
@@ -60,17 +65,13 @@ struct KRom {
   int cell_plant;
   // ABI v3 electrode tables (mpcekf_kernels.hip ETab): npoly = KPOLY when the rows are
   // theta polynomials in `poly` (global, L2-resident), 0 for the v2 linear tables in LDS;
-  // ear = Ea/R of each function's Arrhenius factor [EF_*][side], arr = any of them != 0
+  // arr = any function has an Arrhenius factor.  Each function's rows and Ea/R are found
+  // through its descriptor in the blobs' LDS table header (etab_desc, KDESC doubles each).
   int npoly, arr;
   const double *poly;
-  double ear[5][2];
-  // v3 device layout of `poly` (mpcekf_kernels.hip ETab::f): offset of each function's
-  // rows [fn][side] and of Uocp1 [side]; tconst bit fn*2+side: the rows are all equal and
-  // the function keeps one (no T blend)
-  long long poff[5][2], poff1[2];
-  int tconst;
 };
 constexpr int KPOLY = 6;  // coefficients per theta interval the kernels evaluate (quintic; cubics padded)
+constexpr int KDESC = 3;  // doubles per v3 lookup descriptor (mpcekf_kernels.hip etab_desc)
 
 struct KCfg {
   double SigmaV, SigmaW, ref, u_max, u_min, du_min, du_max, v_max, phise_min, zmax, hild_tol;

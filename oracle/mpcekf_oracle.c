@@ -105,7 +105,7 @@ typedef struct {
    * Uocp1), all NULL for linear tables; Arrhenius energies of Uocp, dUocp, k0, Rf, Cdleff */
   const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p, *Uocp1_p;
   double Ea[5];
-  int tconst; /* bit f: every row of function f's polynomials is the same (read row 0, no T blend) */
+  int tconst; /* bit f: every row of function f's polynomials is the same (row 0 blended with itself) */
 } orc_electrode;
 
 typedef struct {
@@ -250,12 +250,21 @@ static double tab2(const orc_rom *r, const double *t, const double *tp, double E
   double g;
   tidx(r, T, &j, &g);
   const size_t rp = (size_t)(r->ntheta - 1) * NPOLY;
-  if (tp && one) j = 0; /* T-invariant rows: row 0, no blend (the library's tconst) */
-  double a = tp ? tab_poly(tp + j * rp, r->ntheta, th) : tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
-  if (r->ntemp > 1 && !(tp && one)) {
-    double b = tp ? tab_poly(tp + (j + 1) * rp, r->ntheta, th)
-                  : tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
+  double a;
+  if (tp) {
+    /* v3: rows j and j + 1 blended; a T-invariant function (all rows equal, `one`) or a
+     * single-temperature table blends row 0 with itself, a + g (a - a) (the library's one
+     * lookup path, mpcekf_kernels.hip ETab::f) */
+    if (one) j = 0;
+    a = tab_poly(tp + j * rp, r->ntheta, th);
+    const double b = (one || r->ntemp == 1) ? a : tab_poly(tp + (j + 1) * rp, r->ntheta, th);
     a = a + g * (b - a);
+  } else {
+    a = tab_interp(t + (size_t)j * r->ntheta, r->ntheta, th);
+    if (r->ntemp > 1) {
+      double b = tab_interp(t + (size_t)(j + 1) * r->ntheta, r->ntheta, th);
+      a = a + g * (b - a);
+    }
   }
   if (Ea != 0.0) a = a * orc_exp((Ea / r->R) * (1.0 / r->Tref - 1.0 / T));
   return a;

@@ -148,7 +148,7 @@ class PackedRom:
                 setattr(s, k + "_p", _p(arr(poly6(e.poly[k]))) if e.poly else _dp())
             for i, k in enumerate(EL_FNS):
                 s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
-                # rows all equal (an exact Arrhenius function): row 0, no T blend (the library's tconst)
+                # rows all equal (an exact Arrhenius function): row 0 blended with itself (the library's one path)
                 if e.poly and e.poly[k].shape[0] > 1 and all(np.array_equal(e.poly[k][0], e.poly[k][j])
                                                              for j in range(1, e.poly[k].shape[0])):
                     s.tconst |= 1 << i

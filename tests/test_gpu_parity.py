@@ -525,14 +525,17 @@ def test_model_blend_stage_entry_points_match_fused(rom, M):
             np.testing.assert_array_equal(ne, fused["nexec"][k])
 
 
-def test_lane_quad_ekf_kernel_is_exact(rom, oc, M):
-    """k_ekf4 (iterEKF with a lane quad per cell, MPCEKF_QUAD=1) gives the bits of the
-    lane-per-cell k_cell path over a closed loop, state included, and both are the C
-    oracle's trajectories."""
+@pytest.mark.parametrize("lookup,block", [("linear", 256), ("linear", 512), ("quintic", 256)])
+def test_lane_quad_ekf_kernel_is_exact(P, oc, M, lookup, block):
+    """k_ekf4 (iterEKF with a lane quad per cell, MPCEKF_QUAD=1; the 256-thread small-batch
+    instantiation spread over the CUs and the 512-thread one; v2 and v3 tables) gives the
+    bits of the lane-per-cell k_cell path over a closed loop, state included, and both are
+    the C oracle's trajectories."""
+    rom = P.make_synth_rom(lookup=lookup)
     n = 700
     soc0, tc = batch_inputs(n, seed=31)
     a = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=0)
-    b = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=1)
+    b = _run_with_env(M, rom, soc0, tc, 120, MPCEKF_QUAD=1, MPCEKF_EKF4_BLOCK=block)
     ref = oc.run(rom, soc0, tc, 120, nthreads=8)
     for k in ("u", "v", "soc", "phise", "nexec"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
