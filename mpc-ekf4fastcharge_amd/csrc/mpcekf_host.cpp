@@ -104,6 +104,11 @@ struct mpcekf_ctx {
   // staging for host trajectories / stage IO (grown on demand)
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
+  // pinned host bounce buffer of the stage entry points' host copies (Xfer), grown on
+  // demand; copies above bounce_max bytes (MPCEKF_BOUNCE_MAX) go to / from the caller's
+  // memory directly
+  char *h_bounce = nullptr;
+  size_t h_bytes = 0, bounce_max = (size_t)1 << 40;
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
   int timing_every = 1;  // sample every timing_every-th step (1 = every step)
@@ -166,6 +171,15 @@ struct mpcekf_ctx {
   int diag_bufs() {  // the linearisation records and uk_1 copy of the poles / sv diagnostics
     if (!d_lin) HIPCHK(hipMalloc((void **)&d_lin, (size_t)n * MPCEKF_LIN_SIZE * sizeof(double)));
     if (!d_uk1p) HIPCHK(hipMalloc((void **)&d_uk1p, (size_t)n * sizeof(double)));
+    return MPCEKF_OK;
+  }
+  int bounce(size_t bytes) {  // no copy through the buffer is pending: every call ends synchronised
+    if (bytes <= h_bytes) return MPCEKF_OK;
+    if (h_bounce) (void)hipHostFree(h_bounce);
+    h_bounce = nullptr;
+    h_bytes = 0;
+    HIPCHK(hipHostMalloc((void **)&h_bounce, bytes, hipHostMallocDefault));
+    h_bytes = bytes;
     return MPCEKF_OK;
   }
   int tmp(size_t bytes) {
@@ -593,10 +607,12 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   // blocks): it lost at every batch size (0.080 vs 0.075 ms at 1,024 cells, 0.20 vs 0.11 at
   // 65,536; profiles/r02g_*).  Round 5's small-batch mapping is the 256-thread instantiation
   // (512 registers, no spills) spread one wave per CU, chosen for batches up to
-  // MPCEKF_QUAD_MAX cells (results identical whichever path runs).  MPCEKF_QUAD=0/1 forces it.
+  // MPCEKF_QUAD_MAX cells, default 8,192 (results identical whichever path runs; same-box
+  // A/B, profiles/r05e_small_batch.txt: 1,024 cells 0.173 -> 0.160 ms per step, 4,096 0.176
+  // -> 0.164, 16,384 0.189 either way).  MPCEKF_QUAD=0/1 forces it.
   const bool quad_ok = rom->nT > 1 && rom->nZ > 1 && cfg->method == MPCEKF_METHOD_OB && !X->wide;
   {
-    int64_t quad_max = 0;
+    int64_t quad_max = 8192;
     if (const char *e = std::getenv("MPCEKF_QUAD_MAX")) quad_max = std::atoll(e);
     X->quad = quad_ok && ncells <= quad_max;
   }
@@ -612,6 +628,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   {
     int64_t side_max = 16384;
     if (const char *e = std::getenv("MPCEKF_BOUNDS_SIDE")) side_max = std::atoll(e);
+    if (const char *e = std::getenv("MPCEKF_BOUNCE_MAX")) X->bounce_max = (size_t)std::atoll(e);
     X->bounds_side = ncells <= side_max;
   }
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
@@ -698,6 +715,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);
+  if (X->h_bounce) (void)hipHostFree(X->h_bounce);
   if (X->fstream) (void)hipStreamDestroy(X->fstream);
   if (X->stream) (void)hipStreamDestroy(X->stream);
   delete X;
@@ -742,13 +760,7 @@ static int check_tc(const double *tc, size_t count) {
 
 // A stage call's temperature argument (OB_step's Tc, iterEKF's / EKFmatsHandler's Tk)
 // becomes the cell's temperature for this and later calls.
-static int set_tc(mpcekf_ctx *X, const double *tc) {
-  if (!tc) return MPCEKF_OK;
-  int rc = check_tc(tc, (size_t)X->n);
-  if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(X->s.Tc, tc, (size_t)X->n * 8, hipMemcpyHostToDevice, X->stream));
-  return MPCEKF_OK;
-}
+static int set_tc(mpcekf_ctx *X, const double *tc, struct Xfer *xf = nullptr);
 
 // initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.
 int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_degC) {
@@ -1177,23 +1189,73 @@ struct Slab {
     return p;
   }
 };
+// A stage call's host copies, through the context's pinned bounce buffer: inputs are copied
+// into it and sent from there, outputs land in it and are copied out after the call's stream
+// synchronisation (finish).  Copies straight from / into the caller's pageable arrays let the
+// runtime pin and cache those pages; the drop-ins' callers (MATLAB's mxArrays, numpy) free
+// and reallocate their arrays every call, and the stage sequence then stalled 10-20 ms in
+// whichever call came next (tools/dropin_probe.py: 0.6 ms with every array kept alive, 10-14
+// ms when freed, reused or not allocated; profiles/r05e_dropin_probe.jsonl).
+struct Xfer {
+  mpcekf_ctx *X;
+  size_t off = 0;
+  struct Out {
+    void *dst;
+    size_t at, bytes;
+  };
+  std::vector<Out> outs;
+  bool fits(size_t b) const { return b <= X->bounce_max; }
+  static size_t pad(size_t b) { return (b + 255) & ~(size_t)255; }
+  // capacity for the call's copies (sum of pad(bytes) over them)
+  int reserve(size_t bytes) { return X->bounce(bytes); }
+  hipError_t in(void *d, const void *h, size_t b) {
+    if (!b) return hipSuccess;
+    if (!fits(b)) return hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, X->stream);
+    char *p = X->h_bounce + off;
+    off += pad(b);
+    std::memcpy(p, h, b);
+    return hipMemcpyAsync(d, p, b, hipMemcpyHostToDevice, X->stream);
+  }
+  hipError_t out(void *h, const void *d, size_t b) {
+    if (!b) return hipSuccess;
+    if (!fits(b)) return hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, X->stream);
+    outs.push_back({h, off, b});
+    char *p = X->h_bounce + off;
+    off += pad(b);
+    return hipMemcpyAsync(p, d, b, hipMemcpyDeviceToHost, X->stream);
+  }
+  int finish() {
+    HIPCHK(hipStreamSynchronize(X->stream));
+    for (const Out &o : outs) std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    return MPCEKF_OK;
+  }
+};
+static int set_tc(mpcekf_ctx *X, const double *tc, Xfer *xf) {
+  if (!tc) return MPCEKF_OK;
+  int rc = check_tc(tc, (size_t)X->n);
+  if (rc) return rc;
+  if (xf) HIPCHK(xf->in(X->s.Tc, tc, (size_t)X->n * 8));
+  else HIPCHK(hipMemcpyAsync(X->s.Tc, tc, (size_t)X->n * 8, hipMemcpyHostToDevice, X->stream));
+  return MPCEKF_OK;
+}
 extern "C" {
 
 int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!iapp || !vcell) return fail(MPCEKF_E_ARG, "plant_step: null argument");
-  if ((rc = set_tc(X, tc_degC))) return rc;
   size_t n = (size_t)X->n;
+  Xfer xf{X};
+  if ((rc = xf.reserve(3 * Xfer::pad(n * 8)))) return rc;
+  if ((rc = set_tc(X, tc_degC, &xf))) return rc;
   if ((rc = X->tmp(2 * n * 8 + 512))) return rc;
   Slab sl{(char *)X->d_tmp};
   double *di = sl.take<double>(n), *dv = sl.take<double>(n);
-  HIPCHK(hipMemcpyAsync(di, iapp, n * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(xf.in(di, iapp, n * 8));
   if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, nullptr, X->stream), "plant"))) return rc;
   if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
-  HIPCHK(hipMemcpyAsync(vcell, dv, n * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
-  return MPCEKF_OK;
+  HIPCHK(xf.out(vcell, dv, n * 8));
+  return xf.finish();
 }
 
 int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
@@ -1201,8 +1263,11 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   int rc = need_init(X);
   if (rc) return rc;
   if (!vk || !ik) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
-  if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
+  Xfer xf{X};
+  if ((rc = xf.reserve(3 * Xfer::pad(n * 8) + 2 * Xfer::pad(n * nzz * 8) + Xfer::pad(16 * n) + Xfer::pad(32 * n))))
+    return rc;
+  if ((rc = set_tc(X, tk_degC, &xf))) return rc;
   if ((rc = X->tmp((2 * n + n * nzz) * 8 + 2048)) || (rc = X->stage_bufs())) return rc;
   Slab sl{(char *)X->d_tmp};
   double *dvk = sl.take<double>(n), *dik = sl.take<double>(n), *dzb = sl.take<double>(n * nzz);
@@ -1211,8 +1276,8 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   double *dzk = X->d_szk, *dxg = X->d_sxg;
   int *dxm = X->d_sxm;
   X->stage_zk = X->stage_lin = false;
-  HIPCHK(hipMemcpyAsync(dvk, vk, n * 8, hipMemcpyHostToDevice, X->stream));
-  HIPCHK(hipMemcpyAsync(dik, ik, n * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(xf.in(dvk, vk, n * 8));
+  HIPCHK(xf.in(dik, ik, n * 8));
   // iterEKF.m:55 lock-out must see the state before the time update: the bulk
   // update of a locked-out cell is harmless because the cell is stopped.
   // OB: the all-model time update (iterEKF.m:73-84); MB updates only its blended model (in k_cell)
@@ -1229,11 +1294,11 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   io.xg_out = dxg;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
   if (bnd_kernel && (rc = lerr(launch_bounds(X->r, X->s, X->d_bnd, dzb, X->stream), "bounds"))) return rc;
-  if (zk) HIPCHK(hipMemcpyAsync(zk, dzk, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
-  if (boundzk) HIPCHK(hipMemcpyAsync(boundzk, dzb, n * nzz * 8, hipMemcpyDeviceToHost, X->stream));
-  if (xind_model) HIPCHK(hipMemcpyAsync(xind_model, dxm, 4 * n * 4, hipMemcpyDeviceToHost, X->stream));
-  if (xind_gamma) HIPCHK(hipMemcpyAsync(xind_gamma, dxg, 4 * n * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
+  if (zk) HIPCHK(xf.out(zk, dzk, n * nzz * 8));
+  if (boundzk) HIPCHK(xf.out(boundzk, dzb, n * nzz * 8));
+  if (xind_model) HIPCHK(xf.out(xind_model, dxm, 4 * n * 4));
+  if (xind_gamma) HIPCHK(xf.out(xind_gamma, dxg, 4 * n * 8));
+  if ((rc = xf.finish())) return rc;
   X->stage_zk = true;
   return MPCEKF_OK;
 }
@@ -1245,8 +1310,12 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
   if (!zk != !xind_model || !xind_model != !xind_gamma)
     return fail(MPCEKF_E_ARG, "linearize: zk, xind_model and xind_gamma are all given or all NULL");
   if (!zk && !X->stage_zk) return fail(MPCEKF_E_STATE, "linearize: NULL zk / Xind but no mpcekf_ekf_step before it");
-  if ((rc = set_tc(X, tk_degC))) return rc;
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
+  Xfer xf{X};
+  if ((rc = xf.reserve(Xfer::pad(n * 8) + Xfer::pad(n * nzz * 8) + Xfer::pad(16 * n) + Xfer::pad(32 * n) +
+                       Xfer::pad(n * MPCEKF_LIN_SIZE * 8))))
+    return rc;
+  if ((rc = set_tc(X, tk_degC, &xf))) return rc;
   if ((rc = X->tmp((n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048)) || (rc = X->stage_bufs())) return rc;
   Slab sl{(char *)X->d_tmp};
   double *dzk = X->d_szk, *dxg = X->d_sxg, *dl = X->d_slin;
@@ -1255,9 +1324,9 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
     dzk = sl.take<double>(n * nzz);
     dxg = sl.take<double>(4 * n);
     dxm = sl.take<int>(4 * n);
-    HIPCHK(hipMemcpyAsync(dzk, zk, n * nzz * 8, hipMemcpyHostToDevice, X->stream));
-    HIPCHK(hipMemcpyAsync(dxm, xind_model, 4 * n * 4, hipMemcpyHostToDevice, X->stream));
-    HIPCHK(hipMemcpyAsync(dxg, xind_gamma, 4 * n * 8, hipMemcpyHostToDevice, X->stream));
+    HIPCHK(xf.in(dzk, zk, n * nzz * 8));
+    HIPCHK(xf.in(dxm, xind_model, 4 * n * 4));
+    HIPCHK(xf.in(dxg, xind_gamma, 4 * n * 8));
   }
   KIO io{};
   io.mode = MODE_LIN;
@@ -1267,8 +1336,8 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
   io.lin_out = dl;
   X->stage_lin = false;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
-  if (lin) HIPCHK(hipMemcpyAsync(lin, dl, n * MPCEKF_LIN_SIZE * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
+  if (lin) HIPCHK(xf.out(lin, dl, n * MPCEKF_LIN_SIZE * 8));
+  if ((rc = xf.finish())) return rc;
   X->stage_lin = true;
   return MPCEKF_OK;
 }
@@ -1289,17 +1358,18 @@ int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const
   Slab sl{(char *)X->d_tmp};
   double *dc = sl.take<double>(n * (size_t)nslots);
   int *ds = sl.take<int>((size_t)nslots);
-  HIPCHK(hipMemcpyAsync(ds, slots, (size_t)nslots * sizeof(int), hipMemcpyHostToDevice, X->stream));
+  Xfer xf{X};
+  if ((rc = xf.reserve(Xfer::pad((size_t)nslots * sizeof(int)) + 2 * Xfer::pad(bytes)))) return rc;
+  HIPCHK(xf.in(ds, slots, (size_t)nslots * sizeof(int)));
   if (set) {
-    HIPCHK(hipMemcpyAsync(dc, set, bytes, hipMemcpyHostToDevice, X->stream));
+    HIPCHK(xf.in(dc, set, bytes));
     if ((rc = lerr(launch_cols(X->d_slin, X->n, MPCEKF_LIN_SIZE, ds, nslots, dc, true, X->stream), "cols"))) return rc;
   }
   if (out) {
     if ((rc = lerr(launch_cols(X->d_slin, X->n, MPCEKF_LIN_SIZE, ds, nslots, dc, false, X->stream), "cols"))) return rc;
-    HIPCHK(hipMemcpyAsync(out, dc, bytes, hipMemcpyDeviceToHost, X->stream));
+    HIPCHK(xf.out(out, dc, bytes));
   }
-  HIPCHK(hipStreamSynchronize(X->stream));
-  return MPCEKF_OK;
+  return xf.finish();
 }
 
 int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec) {
@@ -1318,9 +1388,11 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *ds = sl.take<double>(n), *du = sl.take<double>(n);
   double *dju = sl.take<double>(n), *djf = sl.take<double>(n), *dnd = sl.take<double>(n);
   int *dn = sl.take<int>(n), *dv = sl.take<int>(n);
-  if (lin) HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  Xfer xf{X};
+  if ((rc = xf.reserve(Xfer::pad(n * MPCEKF_LIN_SIZE * 8) + 5 * Xfer::pad(n * 8) + 2 * Xfer::pad(n * 4)))) return rc;
+  if (lin) HIPCHK(xf.in(dl, lin, n * MPCEKF_LIN_SIZE * 8));
   else dl = X->d_slin;  // the device-resident record of the last mpcekf_linearize
-  HIPCHK(hipMemcpyAsync(ds, soc_k1, n * 8, hipMemcpyHostToDevice, X->stream));
+  HIPCHK(xf.in(ds, soc_k1, n * 8));
   KIO io{};
   io.mode = MODE_MPC;
   io.lin_in = dl;
@@ -1339,14 +1411,13 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
     if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
     if ((rc = lerr(launch_hild(X->k, X->s, io, X->stream), "hild"))) return rc;
   }
-  HIPCHK(hipMemcpyAsync(uk, du, n * 8, hipMemcpyDeviceToHost, X->stream));
-  if (nexec) HIPCHK(hipMemcpyAsync(nexec, dn, n * 4, hipMemcpyDeviceToHost, X->stream));
-  if (J_unc) HIPCHK(hipMemcpyAsync(J_unc, dju, n * 8, hipMemcpyDeviceToHost, X->stream));
-  if (J_fin) HIPCHK(hipMemcpyAsync(J_fin, djf, n * 8, hipMemcpyDeviceToHost, X->stream));
-  if (norm_du) HIPCHK(hipMemcpyAsync(norm_du, dnd, n * 8, hipMemcpyDeviceToHost, X->stream));
-  if (nviol) HIPCHK(hipMemcpyAsync(nviol, dv, n * 4, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
-  return MPCEKF_OK;
+  HIPCHK(xf.out(uk, du, n * 8));
+  if (nexec) HIPCHK(xf.out(nexec, dn, n * 4));
+  if (J_unc) HIPCHK(xf.out(J_unc, dju, n * 8));
+  if (J_fin) HIPCHK(xf.out(J_fin, djf, n * 8));
+  if (norm_du) HIPCHK(xf.out(norm_du, dnd, n * 8));
+  if (nviol) HIPCHK(xf.out(nviol, dv, n * 4));
+  return xf.finish();
 }
 
 int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
@@ -1359,17 +1430,20 @@ int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double
   Slab sl{(char *)X->d_tmp};
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *du = sl.take<double>(n), *dp = sl.take<double>(n * 2 * NA),
          *ds = sl.take<double>(n * NA);
-  if (lin) HIPCHK(hipMemcpyAsync(dl, lin, n * MPCEKF_LIN_SIZE * 8, hipMemcpyHostToDevice, X->stream));
+  Xfer xf{X};
+  if ((rc = xf.reserve(Xfer::pad(n * MPCEKF_LIN_SIZE * 8) + Xfer::pad(n * 8) + Xfer::pad(n * 2 * NA * 8) +
+                       Xfer::pad(n * NA * 8))))
+    return rc;
+  if (lin) HIPCHK(xf.in(dl, lin, n * MPCEKF_LIN_SIZE * 8));
   else dl = X->d_slin;
-  if (uk_1) HIPCHK(hipMemcpyAsync(du, uk_1, n * 8, hipMemcpyHostToDevice, X->stream));
+  if (uk_1) HIPCHK(xf.in(du, uk_1, n * 8));
   else HIPCHK(hipMemcpyAsync(du, X->s.uk_1, n * 8, hipMemcpyDeviceToDevice, X->stream));
   rc = X->wide ? launch_cl_diag_wide(X->k, X->n, dl, du, poles ? dp : nullptr, sv ? ds : nullptr, X->stream)
                : launch_cl_diag(X->k, X->n, dl, du, poles ? dp : nullptr, sv ? ds : nullptr, X->stream);
   if ((rc = lerr(rc, "cl_diag"))) return rc;
-  if (poles) HIPCHK(hipMemcpyAsync(poles, dp, n * 2 * NA * 8, hipMemcpyDeviceToHost, X->stream));
-  if (sv) HIPCHK(hipMemcpyAsync(sv, ds, n * NA * 8, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
-  return MPCEKF_OK;
+  if (poles) HIPCHK(xf.out(poles, dp, n * 2 * NA * 8));
+  if (sv) HIPCHK(xf.out(sv, ds, n * NA * 8));
+  return xf.finish();
 }
 
 // ---- context-free kernels ----------------------------------------------------
@@ -1572,12 +1646,13 @@ int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, doub
   // the SoA scalar block holds each slot as one contiguous [ncells] vector: exactly the
   // requested slots cross PCIe
   std::vector<double> sc(n * (size_t)nslots);
+  Xfer xf{X};
+  if ((rc = xf.reserve((size_t)nslots * Xfer::pad(n * 8) + 2 * Xfer::pad(n * 4)))) return rc;
   for (int j = 0; j < nslots; ++j)
-    HIPCHK(hipMemcpyAsync(sc.data() + (size_t)j * n, X->d_scal + (size_t)kScalMap[slots[j]] * n, n * 8,
-                          hipMemcpyDeviceToHost, X->stream));
-  if (warn) HIPCHK(hipMemcpyAsync(warn, X->s.warn, n * 4, hipMemcpyDeviceToHost, X->stream));
-  if (status) HIPCHK(hipMemcpyAsync(status, X->s.status, n * 4, hipMemcpyDeviceToHost, X->stream));
-  HIPCHK(hipStreamSynchronize(X->stream));
+    HIPCHK(xf.out(sc.data() + (size_t)j * n, X->d_scal + (size_t)kScalMap[slots[j]] * n, n * 8));
+  if (warn) HIPCHK(xf.out(warn, X->s.warn, n * 4));
+  if (status) HIPCHK(xf.out(status, X->s.status, n * 4));
+  if ((rc = xf.finish())) return rc;
   for (size_t c = 0; c < n; ++c)
     for (int j = 0; j < nslots; ++j) scal[c * nslots + j] = sc[(size_t)j * n + c];
   return MPCEKF_OK;
