@@ -63,6 +63,13 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_HILD_NEXTV  // k_hild: the next sweep's v accumulated in the row loop
 #define MPCEKF_HILD_NEXTV 1
 #endif
+// v3 lookups without branches (NaN theta, Ea = 0 and dexp's special cases by selects): one
+// basic block per lookup, so neighbouring lookups' L2 loads can overlap; quintic k_cell 45.3k
+// -> 43.6k instructions, 1,084 -> 837 branches, same-box 155.3 / 148.0 -> 151.9 / 147.7 us
+// (profiles/r05h_ab_branchfree.txt)
+#ifndef MPCEKF_PL_BRANCHFREE
+#define MPCEKF_PL_BRANCHFREE 1
+#endif
 
 // Section timestamps of k_cell for profiling builds (-DMPCEKF_STAMPS); compiled out otherwise.
 #ifdef MPCEKF_STAMPS
@@ -188,19 +195,24 @@ __device__ __forceinline__ int tab_interval(int n, double x, double &s) {
 }
 // one row: interval i's coefficients at c + i * istride
 __device__ __forceinline__ double tabp(const double *c, int n, double x, int istride) {
+#if !MPCEKF_PL_BRANCHFREE
   if (x != x) return __builtin_nan("");
+#endif
   double s;
-  const int i = tab_interval(n, x, s);
+  const int i = tab_interval(n, x, s);  // a NaN x: interval 0 (fmax), the NaN selected below
   const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
-  return horner6(p[0], p[1], p[2], s);
+  const double v = horner6(p[0], p[1], p[2], s);
+  return (MPCEKF_PL_BRANCHFREE && x != x) ? __builtin_nan("") : v;
 }
 // two adjacent rows of interval i (the T bracket): a from c + i * istride, b KPOLY after
 __device__ __forceinline__ void tabp2(const double *c, int n, double x, int istride, double &a, double &b,
                                       int ro = KPOLY) {
+#if !MPCEKF_PL_BRANCHFREE
   if (x != x) {
     a = b = __builtin_nan("");
     return;
   }
+#endif
   double s;
   const int i = tab_interval(n, x, s);
   const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
@@ -208,14 +220,23 @@ __device__ __forceinline__ void tabp2(const double *c, int n, double x, int istr
   const double2 a01 = p[0], a23 = p[1], a45 = p[2], b01 = q[0], b23 = q[1], b45 = q[2];
   a = horner6(a01, a23, a45, s);
   b = horner6(b01, b23, b45, s);
+  if (MPCEKF_PL_BRANCHFREE && x != x) a = b = __builtin_nan("");
 }
 // Defined exp of the v3 Arrhenius factor (oracle/mpcekf_oracle.c orc_exp, rom.py dexp):
 // x = k ln2 + r, k = floor(x / ln2 + 1/2), fdlibm's rational form for exp(r); only
 // +, -, *, /, floor and ldexp, exact or correctly rounded on both sides.
-__device__ __forceinline__ double dexp(double x) {
+// MPCEKF_PL_BRANCHFREE: the special cases by selects (the in-range arithmetic unchanged), so
+// that a lookup is one basic block
+__device__ __forceinline__ double dexp(double x0) {
+#if MPCEKF_PL_BRANCHFREE
+  const bool nan = x0 != x0, big = x0 > 709.782712893384, small = x0 < -745.1332191019412;
+  const double x = (nan || big || small) ? 0.0 : x0;
+#else
+  const double x = x0;
   if (x != x) return x;
   if (x > 709.782712893384) return __builtin_inf();
   if (x < -745.1332191019412) return 0.0;
+#endif
   const double k = floor(x * 1.44269504088896338700e+00 + 0.5);
   const double hi = x - k * dm::LN2_HI;
   const double lo = k * dm::LN2_LO;
@@ -226,7 +247,12 @@ __device__ __forceinline__ double dexp(double x) {
                                  t * (6.61375632143793436117e-05 +
                                       t * (-1.65339022054652515390e-06 + t * 4.13813679705723846039e-08))));
   const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+#if MPCEKF_PL_BRANCHFREE
+  const double v = ldexp(y, (int)k);
+  return nan ? x0 : big ? __builtin_inf() : small ? 0.0 : v;
+#else
   return ldexp(y, (int)k);
+#endif
 }
 
 // Electrode tables (include/mpcekf.h mpcekf_electrode; host: build_rom).  In LDS: a
@@ -277,7 +303,13 @@ struct ETab {
       double a, c;
       tabp2(r->poly + off + j * jstr, nth, th, istr, a, c, ro);
       a = a + g * (c - a);
+#if MPCEKF_PL_BRANCHFREE
+      // every function multiplied by its factor, dexp(+-0) = 1 exactly when Ea = 0 (a * 1 = a:
+      // the oracle's unmultiplied value): no branch between neighbouring lookups' loads
+      a = a * dexp(ear != 0.0 ? ear * xa : 0.0);
+#else
       if (ear != 0.0) a = a * dexp(ear * xa);
+#endif
       return a;
     }
     const double *t = b + etab_header(nth) + ((fn * 2 + side) * nte + j) * nth;
