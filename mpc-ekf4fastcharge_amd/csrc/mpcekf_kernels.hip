@@ -1264,6 +1264,16 @@ __device__ __forceinline__ double2 hx_r(const double2 *hl, const double2 xr3[3],
 __device__ __forceinline__ double2 hh_r(const double2 *hl, const double2 hr3[3], int i) {
   return i < HILD_REG_ROWS ? hr3[hslot(i)] : hh(hl, i);
 }
+// M(i, k) is a structural zero of constraintsMPC.m's M (a constant of the unrolled row loop)
+__device__ __forceinline__ constexpr bool mzero(int i, int k) {
+  return i < NC ? k > i
+       : i < 2 * NC ? k > i - NC
+       : i < 3 * NC ? (i - 2 * NC) != k
+       : i < 4 * NC ? (i - 3 * NC) != k
+       : i < 4 * NC + NP ? k > i - 4 * NC
+       : i < 4 * NC + 2 * NP ? k > i - 4 * NC - NP
+                             : k > i - 4 * NC - 2 * NP;
+}
 // v = X*lambda from +0 in ascending j (the sweep-start v of orc_hildreth)
 __device__ __forceinline__ void hild_v(const double2 *hl, const double2 xr3[3], const double L[NCON], double &v0,
                                        double &v1) {
@@ -1306,8 +1316,13 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
       xq[i % PF] = hx_r(hl, xr3, i + PF);
       hq[i % PF] = hh_r(hl, hr3, i + PF);
     }
-    double t = __builtin_fma(Mf(i, 0), v0, K[i]);
-    t = __builtin_fma(Mf(i, 1), v1, t);
+    // M(i, k) entries that are structural zeros (constraintsMPC.m's Cu / I blocks and the
+    // first row of each Toeplitz block) add +-0 to t: dropped here.  Exact for the fast form:
+    // with v finite a +-0 term changes at most the sign of a zero t, and num = H_ii L_i - t
+    // is then +0 either way (H_ii, L_i >= +0); a non-finite v marks the sweep bad in both forms
+    double t = K[i];
+    if (!mzero(i, 0)) t = __builtin_fma(Mf(i, 0), v0, t);
+    if (!mzero(i, 1)) t = __builtin_fma(Mf(i, 1), v1, t);
     const double num = __builtin_fma(hc.x, L[i], -t);
     const double q0 = num * hc.y;
     const double e2 = __builtin_fma(-hc.x, q0, num);

@@ -116,3 +116,39 @@ def test_dropin_device_sequence_through_gateway(P, M):
             np.testing.assert_array_equal(uk.ravel(), fused["u"][k])
     finally:
         mexshim.mex("destroy", h, nargout=0)
+
+
+def test_bounce_buffer_and_direct_copies_agree(P, M):
+    """The stage entry points' host copies through the pinned bounce buffer (default) and
+    straight from / into the caller's arrays (MPCEKF_BOUNCE_MAX=0) give the same bits, with
+    every output of the host route (zk / zbk / Xind, lin, lin_fields, the cost log, poles / sv)."""
+    import os
+    rom = P.make_synth_rom(lookup="quintic")
+    n, steps = 200, 12
+    soc0, tc = batch_inputs(n, seed=103)
+    res = []
+    for bmax in (None, "0"):
+        old = os.environ.pop("MPCEKF_BOUNCE_MAX", None)
+        if bmax is not None:
+            os.environ["MPCEKF_BOUNCE_MAX"] = bmax
+        try:
+            with M.Context(rom, n) as ctx:
+                ctx.init_cells(soc0, tc)
+                uk = np.zeros(n)
+                out = []
+                for k in range(steps):
+                    v = ctx.OB_step(uk, tc)
+                    zk, zbk, xi = ctx.iterEKF(v, uk, tc)
+                    lin = ctx.EKFmatsHandler(zk, xi, tc)   # host copy; the device record is kept as well
+                    f = ctx.lin_fields(SLOTS)
+                    poles, sv = ctx.mpc_diag(None)
+                    uk, ne, cost = ctx.iterMPC(None, zk[:, -1], cost=True)
+                    out.append([v, zk, zbk, xi["model"], xi["gamma"], lin, f, poles, sv, uk, ne, *cost.values()])
+                res.append(out)
+        finally:
+            os.environ.pop("MPCEKF_BOUNCE_MAX", None)
+            if old is not None:
+                os.environ["MPCEKF_BOUNCE_MAX"] = old
+    for a, b in zip(res[0], res[1]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
