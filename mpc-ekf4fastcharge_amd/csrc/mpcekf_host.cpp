@@ -105,10 +105,10 @@ struct mpcekf_ctx {
   double *d_tmp = nullptr;
   size_t tmp_bytes = 0;
   // pinned host bounce buffer of the stage entry points' host copies (Xfer), grown on
-  // demand; copies above bounce_max bytes (MPCEKF_BOUNCE_MAX) go to / from the caller's
-  // memory directly
+  // demand; copies above bounce_max bytes (MPCEKF_BOUNCE_MAX, default 256 MiB: every copy of
+  // a 65,536-cell stage call is below 15 MiB) go to / from the caller's memory directly
   char *h_bounce = nullptr;
-  size_t h_bytes = 0, bounce_max = (size_t)1 << 40;
+  size_t h_bytes = 0, bounce_max = (size_t)256 << 20;
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
   int timing_every = 1;  // sample every timing_every-th step (1 = every step)
@@ -831,7 +831,7 @@ int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const m
   // k_ekf4 path writes only the record; MB writes boundzk in k_cell)
   const bool bnd_kernel = bounds && !X->mb && (!cell_computes_bounds() || X->quad);
   // OB_step's simStep inside k_cell (KRom::cell_plant): no k_plant launch
-  const bool plant_in_cell = X->r.cell_plant && !X->mb && !X->quad;
+  const bool plant_in_cell = X->r.cell_plant && !X->mb;  // k_cell, or k_ekf4's lane quad (quad_plant)
   // hildreth.m at the end of k_cell (Np = 5, one k_cell per step): no k_hild launch
   const bool hild_in_cell = cell_runs_hild() && !X->wide && !X->split_cell && !X->quad;
   const size_t n = (size_t)X->n, per = n * (size_t)nsteps, nzz = (size_t)X->nz + 2;

@@ -3133,6 +3133,121 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   }
 }
 
+// OB_step's simStep (OB_step.m:188-357) at the start of k_ekf4's fused step: k_plant4's lane
+// quad (lane j = corner j: its gather, replay and 9 output rows; the blend by quad
+// broadcasts in the one-lane order; the per-cell scalar chain the same in all four lanes)
+// on cell_plant's cell-blob layout.  Every live lane stores the per-cell values (the same
+// bits), so each lane's later reads of them (the ring slot of this step) follow its own
+// store.  Returns Vcell in every lane of the quad; k_plant / cell_plant's bits.
+template <int NZ, bool PL>
+__device__ __forceinline__ double quad_plant(const KRom &r, const KState &s, const double *L, const double *tb,
+                                             const double *Tp, const double *Zp, int64_t c, int j, bool live,
+                                             int lazy_t, double Iapp, double tcs, int st) {
+  constexpr int OA = NZ * NX + NZ, OR0 = NZ * NX + NZ + NX + NPK, OD = NZ * NX;
+  const int stride = r.cell_stride;
+  if (lazy_t && live) {  // this step's inputs, for the deferred updates of every model
+    const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
+    s.hist_u[slot] = Iapp;
+    s.hist_p[slot] = s.priorI[c];
+  }
+  if (st & ST_ERROR) return __builtin_nan("");
+  const double T = tcs + 273.15;  // OB_step.m:75
+  const ETab et = etab<PL>(r, tb + r.cell_tab, T);
+  double SOCnAvg = s.SOCn[c], SOCpAvg = s.SOCp[c];
+  const double SOC0n = s.SOC0n[c], SOC0p = s.SOC0p[c];
+  const double negSOC = SOCnAvg, posSOC = SOCpAvg;  // obs.negSOC / posSOC: pre-update (OB_step.m:226-227)
+  double cellSOC = (SOCnAvg - r.th0n) / (r.th100n - r.th0n);
+  int iZu = 0, iZl = 0, iTu = 0, iTl = 0;
+  if (r.nZ > 1) {
+    int a, b;
+    two_nearest(Zp, r.nZ, cellSOC, a, b);
+    iZu = a > b ? a : b; iZl = a < b ? a : b;
+  }
+  if (r.nT > 1) {
+    int a, b;
+    two_nearest(Tp, r.nT, T, a, b);
+    iTu = a > b ? a : b; iTl = a < b ? a : b;
+  }
+  // this lane's corner: mm = {Tl Zl, Tl Zu, Tu Zl, Tu Zu}[j]
+  const int mj = ((j & 2) ? iTu : iTl) * r.nZ + ((j & 1) ? iZu : iZl);
+  double *bx = s.bigx + ((size_t)c * r.NM + mj) * 6;
+  double xs[6];
+  {
+    const double2 *p = reinterpret_cast<const double2 *>(bx);
+    const double2 q0 = p[0], q1 = p[1], q2 = p[2];
+    xs[0] = q0.x; xs[1] = q0.y; xs[2] = q1.x; xs[3] = q1.y; xs[4] = q2.x; xs[5] = q2.y;
+  }
+  const int tsj = lazy_t ? s.ts_plant[c * r.NM + mj] : 0;
+  const double Cdleffn = et.f(0, EF_CDL, SOC0n), Cdleffp = et.f(1, EF_CDL, SOC0p);  // OB_step.m:212-219
+  double dUn = et.f(0, EF_DU, SOCnAvg), dUp = et.f(1, EF_DU, SOCpAvg);
+  double dQn = fabs(r.th100n - r.th0n), dQp = fabs(r.th100p - r.th0p);
+  double res0n = -dQn / (3600 * r.Q - Cdleffn * dQn * dUn);
+  double res0p = dQp / (3600 * r.Q - Cdleffp * dQp * dUp);
+  SOCnAvg = SOCnAvg + res0n * Iapp * r.Ts;
+  SOCpAvg = SOCpAvg + res0p * Iapp * r.Ts;
+  if (SOCnAvg < 0) SOCnAvg = 0;
+  if (SOCnAvg > 1) SOCnAvg = 1;
+  if (SOCpAvg < 0) SOCpAvg = 0;
+  if (SOCpAvg > 1) SOCpAvg = 1;
+  const double Zu = Zp[iZu], Zl = Zp[iZl], Tu = Tp[iTu], Tl = Tp[iTl];
+  double aZ = 0.0, aT = 0.0;
+  if (Zu != Zl) aZ = (cellSOC - Zl) / (Zu - Zl);
+  if (Tu != Tl) aT = (T - Tl) / (Tu - Tl);
+  const double *a = L + mj * stride + OA;
+  if (lazy_t)  // OB_step.m:198-200 for the skipped steps, RCH ring inputs per round trip
+    for (int k0 = tsj + 1; k0 < lazy_t; k0 += RCH) {
+      double u[RCH];
+      ring_chunk(s.hist_u, s, c, k0, lazy_t - 1, u);
+#pragma unroll
+      for (int i = 0; i < RCH; ++i)
+        if (k0 + i < lazy_t) {
+#pragma unroll
+          for (int e = 0; e < NX; ++e) xs[e] = __builtin_fma(a[e], xs[e], u[i]);
+          xs[NX] = __builtin_fma(1.0, xs[NX], u[i]);  // the integrator: a = 1
+        }
+    }
+  const double *B = L + mj * stride;
+  double yk[NPLANT];
+#pragma unroll
+  for (int q = 0; q < NPLANT; ++q) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NX; ++k) acc = acc + B[q * NX + k] * xs[k];
+    acc = acc + B[OR0 + q] * xs[5];
+    const double y = acc + B[OD + q] * Iapp;
+    const double y0 = qbc<0>(y), y1 = qbc<1>(y), y2 = qbc<2>(y), y3 = qbc<3>(y);
+    yk[q] = (1 - aT) * ((1 - aZ) * y0 + aZ * y1) + aT * ((1 - aZ) * y2 + aZ * y3);
+  }
+  double th0 = fmin(fmax(yk[R_TH0] + SOC0n, 1e-6), 1 - 1e-6);
+  double th3 = fmin(fmax(yk[R_TH3] + SOC0p, 1e-6), 1 - 1e-6);
+  double te1 = fmax(yk[R_TE1] + 1, 1e-6);
+  double teE = fmax(yk[R_TEE] + 1, 1e-6);
+  double i0n = et.f(0, EF_K0, negSOC) * sqrt(te1 * (1 - th0) * th0);  // OB_step.m:329-332
+  double i0p = et.f(1, EF_K0, posSOC) * sqrt(teE * (1 - th3) * th3);
+  double negEta0 = 2 * r.R * T / r.F * dasinh(yk[R_IF0] / (2 * i0n));
+  double posEta3 = 2 * r.R * T / r.F * dasinh(yk[R_IF3] / (2 * i0p));
+  double Uocpn0 = et.f(0, EF_U, th0), Uocpp3 = et.f(1, EF_U, th3);
+  const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
+  double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
+  V = V - r.Rc * Iapp;
+  if (live) {
+    s.SOCn[c] = SOCnAvg;
+    s.SOCp[c] = SOCpAvg;
+  }
+  if (live && lazy_t && tsj < lazy_t) {  // advance this corner through step t in place
+    double2 *p = reinterpret_cast<double2 *>(bx);
+    double x[6];
+#pragma unroll
+    for (int e = 0; e < NX; ++e) x[e] = __builtin_fma(a[e], xs[e], Iapp);
+    x[NX] = __builtin_fma(1.0, xs[NX], Iapp);
+    p[0] = make_double2(x[0], x[1]);
+    p[1] = make_double2(x[2], x[3]);
+    p[2] = make_double2(x[4], x[5]);
+    s.ts_plant[c * r.NM + mj] = lazy_t;
+  }
+  return V;
+}
+
 // ---------------------------------------------------------------------------
 // k_ekf4: the fused step's iterEKF ('OB', iterEKF.m:55-210) with a lane quad per cell,
 // lane j = corner j of getXind: its record's catch-up, its getVariables term, its
@@ -3166,12 +3281,21 @@ __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, con
   cc.Zp = Zp;
   cc.erec = s.ekf + (size_t)c * r.NM * REC;
   cc.stride = r.cell_stride;
-  const double Tc = s.Tc[c];
+  const bool fplant = io.plant;  // OB_step's simStep runs here (KRom::cell_plant; k_cell's fplant)
+  const double Tc = fplant && io.tc_in ? io.tc_in[c] : s.Tc[c];
+  if (fplant && io.tc_in && live && j == 0) s.Tc[c] = Tc;  // this step's TC (runMPC.m:85-92)
   cc.T = Tc > 100 ? Tc : Tc + 273.15;  // iterEKF.m:62-66
   cc.et = etab<PL>(r, tb + r.cell_tab, cc.T);
   int st = s.status[c];
   const int t = io.lazy_t;
   if (live && j == 0) s.hflag[c] = 0;
+  // runMPC.m:85: [voltage, ...] = OB_step(uk, TC, cellState, ROM) first
+  double vplant = 0.0;
+  if (fplant) {
+    if (gt == 0 && t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
+    vplant = quad_plant<NZ, PL>(r, s, cc.L, tb, Tp, Zp, c, j, live, t, s.uk[c], Tc, st);
+    if (live && j == 0) s.vk[c] = vplant;
+  }
   auto fail_outputs = [&]() {
     if (!live) return;
     if (j == 0) {
@@ -3198,7 +3322,7 @@ __global__ void __launch_bounds__(BLOCK) k_ekf4(const KRom r, const KCfg cf, con
     fail_outputs();
     return;
   }
-  const double ik = s.uk[c], vk = s.vk[c];
+  const double ik = s.uk[c], vk = fplant ? vplant : s.vk[c];
   int warn = s.warn[c];
   if (warn > cf.max_warn) {  // iterEKF.m:55-59
     st |= ST_LOCKOUT | ST_ERROR;

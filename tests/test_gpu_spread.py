@@ -48,3 +48,34 @@ def test_spread_equals_packed_and_oracle(P, M, oc, n, lookup):
     ref = oc.run(rom, soc0, tc, steps, nthreads=min(16, os.cpu_count() or 1))
     for k in ("u", "v", "soc", "phise", "nexec"):
         np.testing.assert_array_equal(a[k], ref[k], err_msg=k)
+
+
+def test_quad_plant_with_temperature_profile(P, M, oc):
+    """The lane-quad k_ekf4 with OB_step's simStep inside (quad_plant) under a per-step,
+    per-cell temperature profile (the plant stores each step's TC for the EKF): the lane per
+    cell k_cell path's bits and the C oracle's."""
+    rom = P.make_synth_rom(lookup="quintic")
+    n, steps = 300, 40
+    soc0, tc = batch_inputs(n, seed=211)
+    prof = tc[None, :] + 8.0 * np.sin(np.arange(steps)[:, None] / 7.0 + np.arange(n)[None, :] / 50.0)
+    out = {}
+    for quad in ("0", "1"):
+        old = os.environ.get("MPCEKF_QUAD")
+        os.environ["MPCEKF_QUAD"] = quad
+        try:
+            with M.Context(rom, n) as ctx:
+                ctx.init_cells(soc0, tc)
+                out[quad] = ctx.step(steps, tc=prof)
+                out[quad]["state"] = ctx.get_state()
+        finally:
+            if old is None:
+                del os.environ["MPCEKF_QUAD"]
+            else:
+                os.environ["MPCEKF_QUAD"] = old
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        np.testing.assert_array_equal(out["0"][k], out["1"][k], err_msg=k)
+    for k in ("ekf", "bigX", "scal", "lam"):
+        np.testing.assert_array_equal(out["0"]["state"][k], out["1"]["state"][k], err_msg=k)
+    ref = oc.run(rom, soc0, tc, steps, nthreads=min(16, os.cpu_count() or 1), tc_traj=prof)
+    for k in ("u", "v", "soc", "phise", "nexec"):
+        np.testing.assert_array_equal(out["1"][k], ref[k], err_msg=k)
