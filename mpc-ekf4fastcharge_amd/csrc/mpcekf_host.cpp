@@ -14,6 +14,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpcekf.h"
@@ -1204,7 +1205,9 @@ struct Xfer {
     size_t at, bytes;
   };
   std::vector<Out> outs;
-  bool fits(size_t b) const { return b <= X->bounce_max; }
+  // bounced when below the cap and inside the buffer the call reserved (a copy beyond the
+  // reservation goes direct rather than past the buffer's end)
+  bool fits(size_t b) const { return b <= X->bounce_max && off + pad(b) <= X->h_bytes; }
   static size_t pad(size_t b) { return (b + 255) & ~(size_t)255; }
   // capacity for the call's copies (sum of pad(bytes) over them)
   int reserve(size_t bytes) { return X->bounce(bytes); }
@@ -1224,9 +1227,17 @@ struct Xfer {
     off += pad(b);
     return hipMemcpyAsync(p, d, b, hipMemcpyDeviceToHost, X->stream);
   }
+  // after the call's synchronisation: the outputs out of the bounce buffer; copies of 4 MiB
+  // and more each get a thread (iterEKF's zk and zbk are 15 MiB each at 65,536 cells)
   int finish() {
     HIPCHK(hipStreamSynchronize(X->stream));
-    for (const Out &o : outs) std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    std::vector<std::thread> th;
+    for (const Out &o : outs)
+      if (o.bytes >= ((size_t)4 << 20) && th.size() < 3)
+        th.emplace_back([this, o]() { std::memcpy(o.dst, X->h_bounce + o.at, o.bytes); });
+      else
+        std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    for (std::thread &t : th) t.join();
     return MPCEKF_OK;
   }
 };
