@@ -6,6 +6,7 @@ included, so any difference is a bug).
   configs[2]  65 536 cells x 1 000 steps, a 1/64 strided sample of cells checked
               (cells are independent, runMPC.m:83-112, so the oracle runs the sample alone)
   configs[4]  65 536 cells x 1 000 steps at Np = 20 / Nc = 10, a 1/256 sample
+  and configs[2] / configs[4] again on the v3 (quintic) ROM the bench runs
 
 The 1 000-step window covers the part of the charge where ~2 % of cells run
 hildreth.m into maxIter (steps ~350-800).  The GPU runs in chunks of
@@ -79,6 +80,24 @@ def test_configs2_65536_cells_1010_steps_sampled(rom, oc, M):
     steps, stride = 1010, 64
     out = _gpu_sampled(M, rom, soc0, tc, steps, stride)
     ref = oc.run(rom, soc0[::stride], tc[::stride], steps, nthreads=NTHREADS)
+    _check(out, ref)
+
+
+@pytest.fixture(scope="module")
+def rom_v3(P):
+    return P.make_synth_rom(lookup="quintic")
+
+
+@pytest.mark.parametrize("Np,Nc,stride", [(5, 2, 64), (20, 10, 256)])
+def test_bench_workloads_on_the_v3_rom_sampled(rom_v3, oc, M, Np, Nc, stride):
+    """The bench's own workloads — configs[2] (Np = 5) and configs[4] (Np = 20) on the v3
+    quintic ROM bench.py runs by default — over the full 1,010-step window, sampled, bitwise
+    against the C oracle."""
+    soc0, tc = batch_inputs(65536)
+    steps = 1010
+    cfg = M.make_config(Np=Np, Nc=Nc)
+    out = _gpu_sampled(M, rom_v3, soc0, tc, steps, stride, cfg=cfg)
+    ref = oc.run(rom_v3, soc0[::stride], tc[::stride], steps, nthreads=NTHREADS, Np=Np, Nc=Nc)
     _check(out, ref)
 
 
