@@ -64,15 +64,20 @@ def _agree_steps(ref, g, rtol):
     return int(np.argmax(bad)) if bad.any() else int(bad.shape[0])
 
 
-def test_lockout_and_error_cells(rom, oc, M):
-    # SOC0 = 130 % drives getVariables' clamps every call -> warnCount > 10 -> lock-out
+@pytest.mark.parametrize("lookup,quad", [("linear", "1"), ("quintic", "1"), ("quintic", "0")])
+def test_lockout_and_error_cells(P, oc, M, lookup, quad):
+    # SOC0 = 130 % drives getVariables' clamps every call -> warnCount > 10 -> lock-out; on the
+    # v3 ROM the locked-out cells' NaN states reach the branch-free lookups; quad: the small-batch
+    # lane-quad path (the default at 4 cells) or the lane per cell k_cell
+    rom = P.make_synth_rom(lookup=lookup)
     soc0 = np.array([10.0, 130.0, 20.0, 130.0])
     tc = np.array([25.0, 25.0, 15.0, 35.0])
     steps = 30
     ref = oc.run(rom, soc0, tc, steps, nthreads=1)
-    out = M.runMPC(rom, soc0, tc, steps)
-    assert np.array_equal(out["status"], ref["status"])
-    assert (out["status"][[1, 3]] & 1).all()
+    out = _run_with_env(M, rom, soc0, tc, steps, MPCEKF_QUAD=quad)
+    status = out["state"]["status"]
+    assert np.array_equal(status, ref["status"])
+    assert (status[[1, 3]] & 1).all()
     for k in ("u", "v", "soc", "phise"):
         _bitwise(out[k], ref[k], k)
 
