@@ -1232,11 +1232,17 @@ struct Xfer {
   int finish() {
     HIPCHK(hipStreamSynchronize(X->stream));
     std::vector<std::thread> th;
-    for (const Out &o : outs)
-      if (o.bytes >= ((size_t)4 << 20) && th.size() < 3)
-        th.emplace_back([this, o]() { std::memcpy(o.dst, X->h_bounce + o.at, o.bytes); });
-      else
-        std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    for (const Out &o : outs) {
+      bool spawned = false;
+      if (o.bytes >= ((size_t)4 << 20) && th.size() < 3) {
+        try {  // no exception crosses the C-ABI: a thread that cannot start copies inline
+          th.emplace_back([this, o]() { std::memcpy(o.dst, X->h_bounce + o.at, o.bytes); });
+          spawned = true;
+        } catch (...) {
+        }
+      }
+      if (!spawned) std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    }
     for (std::thread &t : th) t.join();
     return MPCEKF_OK;
   }
