@@ -410,6 +410,8 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       for (int j = 0; j < rows; ++j)
         for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[((size_t)j * nint + i) * np + c] : 0.0);
   };
+  bool theta_const = true;
+  if (const char *ev = std::getenv("MPCEKF_THETA_CONST")) theta_const = std::atoi(ev) != 0;
   for (int fn = 0; fn < 5 && poly; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
     for (int sd = 0; sd < 2; ++sd) {
       const mpcekf_electrode *e = els[sd];
@@ -422,7 +424,16 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       const double ea = e->Ea[fn];
       d[0] = ea != 0.0 ? ea / R->R : 0.0;  // oracle: (Ea / R) * (1/Tref - 1/T)
       const int rows = same ? 1 : nte;
-      d[1] = pack2((long long)ptab.size(), (long long)rows * KPOLY);          // off, istride
+      // a theta-invariant function (every interval's coefficients those of interval 0, e.g.
+      // a Cdleff or an Arrhenius k0 that depends on T only): istride 0, so every lane reads
+      // interval 0's rows -- one broadcast line instead of a 64-lane gather -- and evaluates
+      // them at its own s, the same coefficients and the same s as the oracle's interval:
+      // the same bits.  MPCEKF_THETA_CONST=0 keeps the gather (A/B).
+      bool thc = nint > 1 && theta_const;
+      for (int jr = 0; jr < rows && thc; ++jr)
+        for (size_t i = 1; i < nint && thc; ++i)
+          thc = std::memcmp(src + ((size_t)jr * nint + i) * np, src + (size_t)jr * nint * np, np * sizeof(double)) == 0;
+      d[1] = pack2((long long)ptab.size(), thc ? 0 : (long long)rows * KPOLY);  // off, istride
       d[2] = pack2(same ? 0 : KPOLY, (same || nte == 1) ? 0 : KPOLY);          // jstride, ro
       add_poly(src, rows);
     }
