@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define MPCEKF_ABI_VERSION 3
+#define MPCEKF_ABI_VERSION 4
 
 /* return codes */
 #define MPCEKF_OK 0
@@ -96,6 +96,18 @@ typedef struct {
   const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p; /* [ntemp][ntheta-1][tab_npoly] */
   const double *Uocp1_p;                                   /* [ntheta-1][tab_npoly]        */
   double Ea[5];            /* J/mol: Arrhenius factor of Uocp, dUocp, k0, Rf, Cdleff; 0 = none */
+  /* ABI v4 (tab_npoly != 0): a function on its own theta nodes -- a lookup-table handle
+   * (interp1 / pchip over measured breakpoints, which no uniform-grid polynomial follows
+   * across a slope break).  Index f: Uocp, dUocp, k0, Rf, Cdleff, Uocp1.  nnode[f] = 0: the
+   * uniform-grid *_p above; m = nnode[f] >= 2: node[f] [m] strictly ascending (interior nodes
+   * in (0, 1)) and node_p[f] [ntemp][m-1][tab_npoly] (Uocp1: [m-1][tab_npoly]), segment k's
+   * polynomial in d = theta - node[f][k]: theta clamped to [0, 1], k = #{j in 1..m-2 :
+   * node[f][j] <= theta} (the end segments extend past the end nodes), then Horner and the
+   * temperature blend and Arrhenius factor as for v3.  The uniform *_p of such a function may
+   * be NULL.  An interp1-linear row is (y_k, slope_k, 0, 0): the handle's value to rounding. */
+  int32_t nnode[6];
+  const double *node[6];
+  const double *node_p[6];
 } mpcekf_electrode;
 
 /* The ROM struct of runMPC.m:5 as plain arrays.  Set-points ascending. */
@@ -115,7 +127,7 @@ typedef struct {
   int32_t tab_ntheta;      /* theta grid points of the electrode tables (>= 2)     */
   int32_t tab_ntemp;       /* temperature grid points (>= 1)                       */
   const double *tab_T_K;   /* [tab_ntemp] ascending, Kelvin                        */
-  int32_t tab_npoly;       /* ABI v3: 0 = linear tables; 4 / 6 = cubic / quintic *_p */
+  int32_t tab_npoly;       /* ABI v3: 0 = linear tables; 4 / 6 = cubic / quintic *_p (and v4 node_p) */
   mpcekf_electrode neg, pos;
 } mpcekf_rom;
 
@@ -217,6 +229,16 @@ int mpcekf_get_zk(mpcekf_ctx *ctx, double *zk, double *boundzk);
 int mpcekf_cl_eig(int32_t n, const double *a, double *re, double *im, double *sv);
 
 /* ---- stage entry points (one MATLAB function each; all batched over cells) ----
+ * Each has an _async twin with the same arguments ("every call returns
+ * after hipStreamSynchronize unless _async is used"): it enqueues the call's copies and
+ * kernels on the context's stream in order and returns without waiting.  Host inputs are
+ * copied before it returns (the caller may free or reuse them; an input above
+ * MPCEKF_BOUNCE_MAX bytes is read in place and must stay alive until the synchronisation).
+ * Host outputs are written by the time mpcekf_sync(ctx) or the next synchronous stage call
+ * returns -- not before; the caller keeps those arrays alive and unread until then.  Errors
+ * of the enqueued copies are reported by that synchronisation.  The synchronous calls copy
+ * outputs in chunks whose DMA overlaps the host-side copy (a worker pool, MPCEKF_CHUNK bytes
+ * per chunk, MPCEKF_COPY_THREADS workers).
  * The temperature argument (Tc of OB_step.m:1, Tk of iterEKF.m:30 / EKFmatsHandler.m:1,
  * degC, [ncells]) sets each cell's temperature for this and later calls; NULL keeps it. */
 /* OB_step: applies iapp[c] to the plant state at tc_degC[c], returns vcell[c]. */
@@ -252,6 +274,17 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *ctx, const double *lin, const double *soc_k1,
  * Reads nothing else of the context's state and changes none of it.  lin = NULL: the
  * device-resident record of the last mpcekf_linearize. */
 int mpcekf_mpc_diag(mpcekf_ctx *ctx, const double *lin, const double *uk_1, double *poles, double *sv);
+/* the _async twins (see above) */
+int mpcekf_plant_step_async(mpcekf_ctx *ctx, const double *iapp, const double *tc_degC, double *vcell);
+int mpcekf_ekf_step_async(mpcekf_ctx *ctx, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                          double *boundzk, int32_t *xind_model, double *xind_gamma);
+int mpcekf_linearize_async(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                           const double *tk_degC, double *lin);
+int mpcekf_lin_fields_async(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, const double *set, double *out);
+int mpcekf_mpc_step_async(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
+int mpcekf_mpc_step_ex_async(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                             double *J_unc, double *J_fin, double *norm_du, int32_t *nviol);
+int mpcekf_mpc_diag_async(mpcekf_ctx *ctx, const double *lin, const double *uk_1, double *poles, double *sv);
 
 /* Context-free batched kernels (device chosen by `device`).
  * predMat with A = diag(a), B = ones: a,C [n][6], D [n] -> Phi [n][Np][7], G [n][Np][Nc]. */
@@ -332,7 +365,7 @@ int mpcekf_dev_free(void *ptr);
 int mpcekf_dev_copy(void *dst, const void *src, int64_t bytes, int32_t kind);
 int mpcekf_dev_copy2d(void *dst, int64_t dpitch, const void *src, int64_t spitch, int64_t width, int64_t height,
                       int32_t kind);
-int mpcekf_sync(mpcekf_ctx *ctx);
+int mpcekf_sync(mpcekf_ctx *ctx);  /* also completes the _async stage calls' host outputs */
 
 /* ---- state access (open-loop parity, checkpoint/restore) ---- */
 typedef struct {
@@ -369,6 +402,8 @@ int mpcekf_set_state(mpcekf_ctx *ctx, const mpcekf_state *st);
  * PCIe: 8 * nslots (+ 4 + 4) per cell. */
 int mpcekf_get_scalars(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
                        int32_t *status);
+int mpcekf_get_scalars_async(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                             int32_t *status);
 
 #ifdef __cplusplus
 }

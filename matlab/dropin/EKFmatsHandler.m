@@ -14,9 +14,12 @@ function [MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)
     mpcekf_mex('linearize', S.h, zk, Xind.model, Xind.gamma, tk);
   end
   f = mpcekf_mex('linfields', S.h, [21:27, 29, 30:35]);      % Cphi (6), Dphi, bphi, xhat (6)
-  MPC = struct('Cphi', f(1:6, :)', 'Dphi', f(7, :), 'bphi', f(8, :), 'lin', [], 'tick', Xind.tick);
+  tick = [];
+  if isfield(Xind, 'tick'), tick = Xind.tick; end
+  MPC = struct('Cphi', f(1:6, :)', 'Dphi', f(7, :), 'bphi', f(8, :), 'lin', [], 'tick', tick);
   [~, imax] = max(Xind.gamma(:, 1));
   MPC.iT = Xind.theT(imax, 1);  MPC.iZ = Xind.theZ(imax, 1);  MPC.pickWeight = Xind.gamma(imax, 1);
   xhat = f(9:14, :);
   MPC.xhat = xhat;
+  mpcekf_session('set', 'xhat_dev', xhat);                   % the device records' xhat (iterMPC)
 end

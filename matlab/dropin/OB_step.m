@@ -18,13 +18,29 @@ function [Vcell, obs, cellState] = OB_step(Iapp, Tc, cellState, ROM, initCfg)
     if strcmp(S.kf.method, 'MB'), cfg.method = 1; end
     % the electrode tables hold the ROM set-points and the distinct Tc (mpcekf_rom_struct
     % keeps only their span when they do not fit its 8 table temperatures, e.g. a per-cell
-    % Tc of thousands of distinct values)
-    h = mpcekf_mex('create', mpcekf_rom_struct(ROM, [], [], unique(Tc(:)')), cfg, S.device, n);
+    % Tc of thousands of distinct values), built as mpcekf_export_rom builds them
+    % (mpcekf_build_tables: node tables for lookup-table handles, ntheta by the error
+    % budget) with the budget checked at the distinct Tc this run uses.  A ROM whose tables
+    % miss the budget there is refused ('mpcekf:budget'), unless initCfg.tabBudget = 'warn':
+    % then it runs with a warning and cellState.tab_error says how far its lookups are off.
+    Tu = unique(Tc(:)');
+    [R, terr, tok] = mpcekf_build_tables(ROM, [], Tu, struct('Teval', Tu + 273.15, 'strict', false));
+    if ~tok
+      msg = sprintf(['OB_step drop-in: the electrode tables miss the error budget at the run''s ' ...
+                     'temperatures (neg Uocp %.3g V, k0 %.3g; pos Uocp %.3g V, k0 %.3g)'], ...
+                    terr.neg.Uocp, terr.neg.k0_rel, terr.pos.Uocp, terr.pos.k0_rel);
+      if isfield(initCfg, 'tabBudget') && strcmpi(initCfg.tabBudget, 'warn')
+        warning('mpcekf:budget', '%s', msg);
+      else
+        error('mpcekf:budget', '%s (initCfg.tabBudget = ''warn'' runs it anyway)', msg);
+      end
+    end
+    h = mpcekf_mex('create', R, cfg, S.device, n);
     mpcekf_session('set', 'h', h);
     mpcekf_mex('init', h, reshape(initCfg.SOC0, 1, n), Tc .* ones(1, n));
     fn = ROM.cellData.function.neg;
     cellState = struct('initialized', true, 'h', h, 'n', n, 'Ts', ROM.xraData.Tsamp, ...
-                       'theta0n', fn.theta0(), 'theta100n', fn.theta100());
+                       'theta0n', fn.theta0(), 'theta100n', fn.theta100(), 'tab_error', terr);
   end
   n = cellState.n;
   s = mpcekf_mex('scalars', cellState.h, [1 2]);             % pre-update averages (OB_step.m:226-228),

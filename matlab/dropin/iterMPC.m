@@ -3,7 +3,9 @@ function [uk, mpcData] = iterMPC(xk, cellState, mpcData)
 % is EKFmatsHandler's device-resident records (cellState.MPC.lin empty) or, when a caller
 % built cellState.MPC.lin itself, those 35 x ncells records; their xhat rows are the
 % caller's xk (6 x ncells, the state iterMPC.m:29 augments) -- written to the device only
-% when xk is not the xhat EKFmatsHandler returned.  uk_1 and the Hildreth warm start live
+% when xk is not the xhat the device records hold now (the session tracks it: the last
+% EKFmatsHandler's xhat, or the xk an earlier iterMPC wrote over it), so a call without an
+% override after one with it restores EKFmatsHandler's xhat as the reference would.  uk_1 and the Hildreth warm start live
 % in the context.  When runMPC.m has set mpcData.k, row k of mpcData.cost
 % (iterMPC.m:89-95: t, J_uncon, J_final, norm_DU, viol, nexec) is filled, one column per
 % cell.
@@ -11,11 +13,11 @@ function [uk, mpcData] = iterMPC(xk, cellState, mpcData)
   lin = cellState.MPC.lin;
   if isempty(lin)
     n = size(cellState.MPC.xhat, 2);
-    if ~isempty(xk)
-      xk = reshape(xk, 6, []) .* ones(1, n);
-      if ~isequal(xk, cellState.MPC.xhat)
-        mpcekf_mex('linfields', S.h, 30:35, xk);              % MPCEKF_LIN_XHAT
-      end
+    if isempty(xk), xk = cellState.MPC.xhat; end
+    xk = reshape(xk, 6, []) .* ones(1, n);
+    if ~isequal(xk, S.xhat_dev)                               % what the device records hold
+      mpcekf_mex('linfields', S.h, 30:35, xk);                % MPCEKF_LIN_XHAT
+      mpcekf_session('set', 'xhat_dev', xk);
     end
   else
     n = size(lin, 2);

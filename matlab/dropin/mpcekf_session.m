@@ -7,7 +7,10 @@ function S = mpcekf_session(op, name, value)
   persistent P
   % zk_last / ekf_tick: the zk the last iterEKF returned and a counter of iterEKF calls, so
   % EKFmatsHandler knows when the library's device copies of zk and Xind are the caller's
-  if isempty(P), P = struct('h', [], 'kf', [], 'mpc', [], 'device', 0, 'zk_last', [], 'ekf_tick', 0); end
+  % xhat_dev: the xhat the device-resident linearisation records hold (EKFmatsHandler's, or
+  % the xk an iterMPC call wrote over it)
+  if isempty(P), P = struct('h', [], 'kf', [], 'mpc', [], 'device', 0, 'zk_last', [], 'ekf_tick', 0, ...
+                            'xhat_dev', []); end
   switch op
     case 'set'
       P.(name) = value;

@@ -1,7 +1,8 @@
 function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC, order)
 % MPCEKF_EXPORT_ROM  Tabulate a reference ROM (.mat) into the JSON file the MI355X
-% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py, format v3; v2 with
-% order = 1).
+% framework loads with ROM.load_json (mpc-ekf4fastcharge_amd/rom.py, format v3 -- v4 when
+% a handle is a lookup table on its own breakpoints (node tables, mpcekf_build_tables);
+% v2 with order = 1).
 %
 %   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json')          % quintics, ntheta by budget
 %   mpcekf_export_rom('ROM_NMC30_HRA.mat', 'rom_nmc30.json', 1025, [15 25 35])
@@ -44,17 +45,11 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC, order)
   S = load(matFile);
   if isfield(S, 'ROM'), ROM = S.ROM; else, f = fieldnames(S); ROM = S.(f{1}); end
   fn = ROM.cellData.function;
-  if order > 1 && isempty(ntheta)
-    % the operating theta range of each electrode (0-100 % SOC, widened by 0.04)
-    lim = @(g) [max(0, min(g.soc(0, 298.15), g.soc(1, 298.15)) - 0.04), min(1, max(g.soc(0, 298.15), g.soc(1, 298.15)) + 0.04)];
-    for ntheta = [257, 513, 1025, 2049, 4097]
-      R = mpcekf_rom_struct(ROM, ntheta, TdegC, [], order);
-      th = linspace(0, 1, ntheta);
-      [en, okn] = mpcekf_check_tables(fn.neg, R.neg, th, R.tab_T_K, R.Tref, R.R, lim(fn.neg));
-      [ep, okp] = mpcekf_check_tables(fn.pos, R.pos, th, R.tab_T_K, R.Tref, R.R, lim(fn.pos));
-      if okn && okp, break; end
-    end
-    assert(okn && okp, 'mpcekf_export_rom: the tables miss the error budget at %d theta points', ntheta);
+  if order > 1
+    % the table step shared with the OB_step drop-in: node tables for lookup-table handles
+    % (ABI v4), uniform quintics otherwise, ntheta by the error budget (or the given one,
+    % still checked); refuses a file that misses the budget
+    R = mpcekf_build_tables(ROM, TdegC, [], struct('order', order, 'ntheta', ntheta));
   else
     R = mpcekf_rom_struct(ROM, ntheta, TdegC, [], order);
   end
@@ -63,6 +58,7 @@ function mpcekf_export_rom(matFile, jsonFile, ntheta, TdegC, order)
   out = struct();
   out.format = 'mpcekf-rom-v2';
   if order > 1, out.format = 'mpcekf-rom-v3'; end
+  if isfield(R.neg, 'nodes') || isfield(R.pos, 'nodes'), out.format = 'mpcekf-rom-v4'; end
   out.source = matFile;
   out.T_degC = arr(R.T_degC);
   out.SOC_pct = arr(R.SOC_pct);
@@ -98,6 +94,12 @@ function e = jsonify(t)
     e.Ea = struct();
     for k = 1:5
       if t.Ea(k) ~= 0, e.Ea.(names{k}) = t.Ea(k); end
+    end
+  end
+  if isfield(t, 'nodes')  % v4: {"nodes": {"Uocp": {"x": {shape, order, data}, "p": {...}}, ...}}
+    e.nodes = struct();
+    for k = fieldnames(t.nodes)'
+      e.nodes.(k{1}) = struct('x', arr(t.nodes.(k{1}).x), 'p', arr(t.nodes.(k{1}).p));
     end
   end
 end

@@ -164,6 +164,31 @@ static int electrode_v3(const mxArray *e, mpcekf_electrode *out, int ntemp, int 
   return np;
 }
 
+/* ABI v4 (optional): e.nodes.{Uocp,dUocp,k0,Rf,Cdleff,Uocp1}, each a struct with x (1 x m
+ * ascending theta nodes) and p (ntemp x (m-1) x npoly; Uocp1 (m-1) x npoly) -- a function
+ * on its own breakpoints (include/mpcekf.h nnode / node / node_p; mpcekf_build_tables fills
+ * them for lookup-table handles).  npoly must be the poly tables' (tab_npoly). */
+static void electrode_v4(const mxArray *e, mpcekf_electrode *out, int ntemp, int npoly) {
+  const mxArray *nd = mxGetField(e, 0, "nodes");
+  if (!nd || mxIsEmpty(nd)) return;
+  if (!mxIsStruct(nd)) mexErrMsgIdAndTxt("mpcekf:arg", "nodes: expected a struct");
+  if (!npoly) mexErrMsgIdAndTxt("mpcekf:arg", "nodes: needs the poly tables (ABI v3) beside them");
+  const char *names[6] = {"Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"};
+  for (int f = 0; f < 6; ++f) {
+    const mxArray *t = mxGetField(nd, 0, names[f]);
+    if (!t || mxIsEmpty(t)) continue;
+    const mxArray *x = field(t, "x"), *p = field(t, "p");
+    const size_t m = mxGetNumberOfElements(x);
+    const size_t rows = f == 5 ? 1 : (size_t)ntemp;
+    if (m < 2 || mxGetNumberOfElements(p) != rows * (m - 1) * (size_t)npoly)
+      mexErrMsgIdAndTxt("mpcekf:arg", "nodes.%s: x needs >= 2 nodes and p %s x (m-1) x %d", names[f],
+                        f == 5 ? "1" : "ntemp", npoly);
+    out->nnode[f] = (int32_t)m;
+    out->node[f] = dvec(x, m, names[f]);
+    out->node_p[f] = rowmajor(p, names[f]);
+  }
+}
+
 static void electrode(const mxArray *e, mpcekf_electrode *out, int ntemp, int ntheta) {
   out->theta0 = scalar(field(e, "theta0"), "theta0");
   out->theta100 = scalar(field(e, "theta100"), "theta100");
@@ -214,6 +239,8 @@ static void rom_from_struct(const mxArray *R, mpcekf_rom *r) {
   const int npp = electrode_v3(field(R, "pos"), &r->pos, r->tab_ntemp, r->tab_ntheta);
   if (npn != npp) mexErrMsgIdAndTxt("mpcekf:arg", "ROM: poly tables for both electrodes or neither, same order");
   r->tab_npoly = npn;
+  electrode_v4(field(R, "neg"), &r->neg, r->tab_ntemp, npn);
+  electrode_v4(field(R, "pos"), &r->pos, r->tab_ntemp, npn);
 }
 
 static void cfg_from_struct(const mxArray *s, mpcekf_config *c) {

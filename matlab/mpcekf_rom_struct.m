@@ -1,4 +1,4 @@
-function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC, order)
+function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC, order, nodes)
 % MPCEKF_ROM_STRUCT  The reference ROM struct (runMPC.m:5) as the plain arrays of the
 % library's mpcekf_rom (include/mpcekf.h): what mpcekf_mex('create', R, ...) takes and
 % what mpcekf_export_rom writes to JSON.
@@ -15,7 +15,12 @@ function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC, order)
 % budget holds).  order 1: the v2 linear tables (default ntheta 101), where an Arrhenius
 % k0 interpolated linearly in T is off by about h^2/8 (Ea/(R T^2))^2 between table
 % points (DESIGN.md 3: ~1.4 % at h = 5 K, Ea = 50 kJ/mol).
+% nodes (ABI v4, default false): also the node tables of lookup-table handles
+% (mpcekf_tabulate_electrode); mpcekf_build_tables sets it and checks the budget.
+% Tref (the Arrhenius reference temperature of the v3 factor) is ROM.cellData.const.Tref
+% when the ROM has one, else 298.15 K.
   if nargin < 5 || isempty(order), order = 5; end
+  if nargin < 6 || isempty(nodes), nodes = false; end
   if nargin < 2 || isempty(ntheta), ntheta = 101 + 412 * (order > 1); end
   if nargin < 4 || isempty(TC), TC = 25; end
   if nargin < 3 || isempty(TdegC)
@@ -50,8 +55,10 @@ function R = mpcekf_rom_struct(ROM, ntheta, TdegC, TC, order)
   R.T_degC = ROM.xraData.T(:)';  R.SOC_pct = ROM.xraData.SOC(:)';  R.Ts = ROM.xraData.Tsamp;
   R.A = A;  R.C = C;  R.D = D;
   R.names = names;  R.tf_code = int32(code - 1);  R.xloc = xloc(:)';
-  R.F = cd.const.F;  R.R = cd.const.R;  R.Q = fn.const.Q();  R.Rc = fn.const.Rc();  R.Tref = 298.15;
+  R.F = cd.const.F;  R.R = cd.const.R;  R.Q = fn.const.Q();  R.Rc = fn.const.Rc();
+  R.Tref = 298.15;
+  if isfield(cd.const, 'Tref') && ~isempty(cd.const.Tref), R.Tref = cd.const.Tref; end
   R.tab_T_K = TK;
-  R.neg = mpcekf_tabulate_electrode(fn.neg, th, TK, order, R.Tref, R.R);
-  R.pos = mpcekf_tabulate_electrode(fn.pos, th, TK, order, R.Tref, R.R);
+  R.neg = mpcekf_tabulate_electrode(fn.neg, th, TK, order, R.Tref, R.R, nodes && order > 1);
+  R.pos = mpcekf_tabulate_electrode(fn.pos, th, TK, order, R.Tref, R.R, nodes && order > 1);
 end

@@ -1,4 +1,4 @@
-function e = mpcekf_tabulate_electrode(f, th, TK, order, Tref, R)
+function e = mpcekf_tabulate_electrode(f, th, TK, order, Tref, R, nodes)
 % MPCEKF_TABULATE_ELECTRODE  One electrode's cellData.function handles on the (T, theta)
 % grid TK (K, 1..8 ascending) x th (uniform over [0, 1]): the fields of the library's
 % mpcekf_electrode (include/mpcekf.h), 2-D tables as ntemp x ntheta.  The handles are
@@ -12,9 +12,18 @@ function e = mpcekf_tabulate_electrode(f, th, TK, order, Tref, R)
 % f(th,Tref) exp(Ea/R (1/Tref - 1/T)) gets its Ea and rows f(th, Tref), so the library
 % evaluates it exactly at any T.  order 1: the v2 tables only.  The same steps as
 % rom.py tabulate_handles (tested there against closed-form handles).
+%
+% nodes (ABI v4, default false; mpcekf_build_tables sets it): a function whose handle
+% carries theta breakpoints (mpcekf_handle_nodes: interp1 / pchip / griddedInterpolant over
+% measured data) also gets e.nodes.(name) = struct('x', 1 x m nodes, 'p', ntemp x (m-1) x
+% (order+1)) (Uocp1: (m-1) x (order+1)): per segment the cubic through the handle at
+% x_k + h (0, 1/3, 2/3, 1) in d = theta - x_k, zero-padded -- exact to rounding for any
+% handle that is a cubic or less between its breakpoints (rom.py fit_segments).  The
+% library then looks such a function up on its own nodes.
   if nargin < 4 || isempty(order), order = 5; end
   if nargin < 5 || isempty(Tref), Tref = 298.15; end
   if nargin < 6 || isempty(R), R = 8.3144621; end
+  if nargin < 7 || isempty(nodes), nodes = false; end
   nt = numel(TK);  nth = numel(th);
   e = struct();
   e.theta0 = f.theta0();  e.theta100 = f.theta100();
@@ -57,6 +66,47 @@ function e = mpcekf_tabulate_electrode(f, th, TK, order, Tref, R)
   end
   [y, d1, d2] = fd_derivs(u1, th);
   e.poly.Uocp1 = hermite(y, d1, d2, h, order);
+  if ~nodes, return; end
+  % ABI v4 node tables; discovery on the cellData handles themselves (the wrappers above
+  % capture the whole struct f)
+  src = {{f.Uocp}, {f.dUocp}, {f.k0}, {f.Rf}, {f.Cdl, f.wDL}};
+  e.nodes = struct();
+  for k = 1:5
+    xn = [];
+    for q = 1:numel(src{k}), xn = union(xn, mpcekf_handle_nodes(src{k}{q})); end
+    if numel(xn) < 2, continue; end
+    P = zeros(nt, numel(xn) - 1, order + 1);
+    for j = 1:nt
+      Tr = TK(j);
+      if e.Ea(k) ~= 0, Tr = Tref; end
+      P(j, :, :) = reshape(fit_segments(@(t) fns{k}(t, Tr), xn, order + 1), [1, numel(xn) - 1, order + 1]);
+    end
+    e.nodes.(names{k}) = struct('x', xn, 'p', P);
+  end
+  xn = mpcekf_handle_nodes(f.Uocp);
+  if numel(xn) >= 2
+    e.nodes.Uocp1 = struct('x', xn, 'p', fit_segments(u1, xn, order + 1));
+  end
+end
+
+function C = fit_segments(f, x, np)
+  % rom.py fit_segments: the cubic through f at x_k + h (0, 1/3, 2/3, 1) per segment, in
+  % d = theta - x_k; a segment whose quadratic and cubic terms are rounding noise is stored
+  % as interp1's (y_k, (y_k+1 - y_k) / h); zero-padded to np coefficients
+  V = inv(fliplr(vander([0, 1/3, 2/3, 1])));      % increasing powers of t = d / h
+  m = numel(x);
+  C = zeros(m - 1, np);
+  for k = 1:m - 1
+    a = x(k);  b = x(k + 1);  h = b - a;
+    ys = [f(a); f(a + h / 3); f(a + 2 * h / 3); f(b)];
+    q = V * ys;
+    sc = max(max(abs(ys)), realmin);
+    if abs(q(3)) <= 64 * eps * sc && abs(q(4)) <= 64 * eps * sc
+      C(k, 1:2) = [ys(1), (ys(4) - ys(1)) / h];
+    else
+      C(k, 1:4) = [q(1), q(2) / h, q(3) / h^2, q(4) / h^3];
+    end
+  end
 end
 
 function [y, d1, d2] = fd_derivs(f, th)

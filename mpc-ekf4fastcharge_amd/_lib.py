@@ -31,7 +31,8 @@ class Electrode(C.Structure):
     _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
                 ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp),
                 ("Uocp_p", _dp), ("dUocp_p", _dp), ("k0_p", _dp), ("Rf_p", _dp), ("Cdleff_p", _dp),
-                ("Uocp1_p", _dp), ("Ea", C.c_double * 5)]
+                ("Uocp1_p", _dp), ("Ea", C.c_double * 5),
+                ("nnode", C.c_int32 * 6), ("node", _dp * 6), ("node_p", _dp * 6)]   # ABI v4
 
 
 class Rom(C.Structure):
@@ -80,10 +81,13 @@ EXPORTS = [
     "mpcekf_build_id", "mpcekf_cl_eig", "mpcekf_mpc_diag", "mpcekf_set_graph",
     "mpcekf_dev_alloc", "mpcekf_dev_free", "mpcekf_dev_copy", "mpcekf_dev_copy2d", "mpcekf_sync",
     "mpcekf_get_scalars", "mpcekf_lin_fields",
+    # the _async stage twins (include/mpcekf.h)
+    "mpcekf_plant_step_async", "mpcekf_ekf_step_async", "mpcekf_linearize_async", "mpcekf_lin_fields_async",
+    "mpcekf_mpc_step_async", "mpcekf_mpc_step_ex_async", "mpcekf_mpc_diag_async", "mpcekf_get_scalars_async",
 ]
 
 COPY_H2D, COPY_D2H, COPY_D2D = 0, 1, 2
-ABI_VERSION = 3   # include/mpcekf.h MPCEKF_ABI_VERSION
+ABI_VERSION = 4   # include/mpcekf.h MPCEKF_ABI_VERSION
 
 _lib = None
 
@@ -138,6 +142,9 @@ def load():
     L.mpcekf_sync.argtypes = [vp]
     L.mpcekf_get_scalars.argtypes = [vp, _ip, C.c_int32, _dp, _ip, _ip]
     L.mpcekf_lin_fields.argtypes = [vp, _ip, C.c_int32, _dp, _dp]
+    for nm in ("plant_step", "ekf_step", "linearize", "lin_fields", "mpc_step", "mpc_step_ex", "mpc_diag",
+               "get_scalars"):   # the _async twins take the synchronous call's arguments
+        getattr(L, f"mpcekf_{nm}_async").argtypes = getattr(L, f"mpcekf_{nm}").argtypes
     for nm in EXPORTS:
         if nm not in ("mpcekf_abi_version", "mpcekf_last_error", "mpcekf_config_defaults", "mpcekf_build_id"):
             getattr(L, nm).restype = C.c_int

@@ -6,12 +6,17 @@
 // stage entry points.  No C++ exception crosses the ABI.
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
@@ -22,6 +27,9 @@
 #include "mpcekf_kernels.hpp"
 
 using namespace mk;
+namespace mk {
+int launch_rows(const double *src, int64_t n, const int *rows, int k, double *dst, void *stream);  // mpcekf_io.hip
+}
 
 namespace {
 
@@ -52,6 +60,110 @@ int dalloc(T **p, size_t n) {
   if (n == 0) return MPCEKF_OK;
   HIPCHK(hipMalloc((void **)p, n * sizeof(T)));
   return MPCEKF_OK;
+}
+
+// The output side of the stage calls' host copies (round 6): a pool of worker threads that
+// copy device-to-host chunks out of the pinned bounce buffer as their DMA completes.  A call
+// enqueues each output as chunks of `chunk` bytes, an event recorded after each chunk's DMA;
+// a worker waits for that event and copies the chunk to the caller's array.  So the DMA of
+// chunk k + 1 overlaps the copy of chunk k, several threads take the page faults of a
+// caller's freshly allocated array at once, and an _async call returns with its copies still
+// in flight (finished by the next synchronisation).
+struct Copier {
+  struct Job {
+    hipEvent_t ev;
+    const char *src;
+    char *dst;
+    size_t bytes;
+  };
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<Job> q;
+  size_t busy = 0;
+  bool stop = false;
+  hipError_t err = hipSuccess;
+  std::vector<std::thread> th;
+  int device = 0;
+  void start(int n, int dev) {
+    device = dev;
+    for (int i = 0; i < n; ++i) {
+      try {
+        th.emplace_back([this]() { run(); });
+      } catch (...) {  // no thread: the remaining jobs are copied by drain() itself
+        break;
+      }
+    }
+  }
+  void run() {
+    (void)hipSetDevice(device);
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !q.empty(); });
+      if (q.empty()) return;  // stop
+      Job j = q.front();
+      q.pop_front();
+      ++busy;
+      lk.unlock();
+      do_job(j);
+      lk.lock();
+      --busy;
+      if (q.empty() && !busy) idle.notify_all();
+    }
+  }
+  void do_job(const Job &j) {
+    hipError_t e = hipEventSynchronize(j.ev);
+    if (e == hipSuccess) std::memcpy(j.dst, j.src, j.bytes);
+    else {
+      std::lock_guard<std::mutex> g(mu);
+      if (err == hipSuccess) err = e;
+    }
+  }
+  void push(const Job &j) {
+    if (th.empty()) {  // no worker: copied at the synchronisation, in order
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(j);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(j);
+    }
+    cv.notify_one();
+  }
+  // every queued copy done; returns (and clears) the first HIP error a worker met
+  hipError_t drain() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (th.empty()) {
+      while (!q.empty()) {
+        Job j = q.front();
+        q.pop_front();
+        lk.unlock();
+        do_job(j);
+        lk.lock();
+      }
+    } else {
+      idle.wait(lk, [&] { return q.empty() && !busy; });
+    }
+    hipError_t e = err;
+    err = hipSuccess;
+    return e;
+  }
+  ~Copier() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    for (std::thread &t : th) t.join();
+  }
+};
+
+int copy_threads() {  // MPCEKF_COPY_THREADS, else half the CPUs this process may use, 1..8
+  if (const char *e = std::getenv("MPCEKF_COPY_THREADS")) return std::max(0, std::min(64, std::atoi(e)));
+  cpu_set_t set;
+  int n = 8;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set) / 2;
+  return std::max(1, std::min(8, n));
 }
 
 }  // namespace
@@ -110,6 +222,37 @@ struct mpcekf_ctx {
   // a 65,536-cell stage call is below 15 MiB) go to / from the caller's memory directly
   char *h_bounce = nullptr;
   size_t h_bytes = 0, bounce_max = (size_t)256 << 20;
+  // round 6: the buffer is bump-allocated over the calls up to the next synchronisation
+  // (xoff), so _async calls keep their regions until their copies finish; outputs leave it
+  // in chunks of xchunk bytes (MPCEKF_CHUNK, default 4 MiB), one event each (xev, reused
+  // after the synchronisation), copied out by the worker pool `copier`
+  size_t xoff = 0, xchunk = (size_t)4 << 20;
+  std::vector<hipEvent_t> xev;
+  size_t xev_used = 0;
+  bool xpending = false;
+  Copier *copier = nullptr;
+  hipError_t next_event(hipEvent_t *e) {
+    if (xev_used == xev.size()) {
+      hipEvent_t ne = nullptr;
+      hipError_t r = hipEventCreateWithFlags(&ne, hipEventDisableTiming);
+      if (r != hipSuccess) return r;
+      xev.push_back(ne);
+    }
+    *e = xev[xev_used++];
+    return hipSuccess;
+  }
+  // the synchronisation every synchronous stage call (and mpcekf_sync) ends with: the
+  // stream, then every output copy still queued; the bounce buffer and events free again
+  int drain() {
+    hipError_t e = hipStreamSynchronize(stream);
+    hipError_t c = copier ? copier->drain() : hipSuccess;
+    xoff = 0;
+    xev_used = 0;
+    xpending = false;
+    if (e != hipSuccess) return fail(MPCEKF_E_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    if (c != hipSuccess) return fail(MPCEKF_E_HIP, "output copy: %s", hipGetErrorString(c));
+    return MPCEKF_OK;
+  }
   // per-kernel HIP-event timing (mpcekf_set_timing)
   bool timing = false;
   int timing_every = 1;  // sample every timing_every-th step (1 = every step)
@@ -174,12 +317,24 @@ struct mpcekf_ctx {
     if (!d_uk1p) HIPCHK(hipMalloc((void **)&d_uk1p, (size_t)n * sizeof(double)));
     return MPCEKF_OK;
   }
-  int bounce(size_t bytes) {  // no copy through the buffer is pending: every call ends synchronised
-    if (bytes <= h_bytes) return MPCEKF_OK;
+  // room for `bytes` more of the current epoch's copies: when the buffer is too small, the
+  // pending calls are completed first (drain) and the buffer regrown.  A failed pinned
+  // allocation is not an error: the buffer stays empty and every copy goes direct (Xfer::fits).
+  int bounce(size_t bytes) {
+    if (xoff + bytes <= h_bytes) return MPCEKF_OK;
+    if (xpending || xoff) {
+      int rc = drain();
+      if (rc) return rc;
+      if (bytes <= h_bytes) return MPCEKF_OK;
+    }
     if (h_bounce) (void)hipHostFree(h_bounce);
     h_bounce = nullptr;
     h_bytes = 0;
-    HIPCHK(hipHostMalloc((void **)&h_bounce, bytes, hipHostMallocDefault));
+    if (hipHostMalloc((void **)&h_bounce, bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      h_bounce = nullptr;
+      return MPCEKF_OK;
+    }
     h_bytes = bytes;
     return MPCEKF_OK;
   }
@@ -253,8 +408,18 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   if (R->tab_npoly != 0 && R->tab_npoly != 4 && R->tab_npoly != KPOLY)
     return fail(MPCEKF_E_ARG, "rom: tab_npoly = %d (0: linear tables, 4: cubic, 6: quintic)", R->tab_npoly);
   for (const mpcekf_electrode *e : {&R->neg, &R->pos}) {
-    if (R->tab_npoly && (!e->Uocp_p || !e->dUocp_p || !e->k0_p || !e->Rf_p || !e->Cdleff_p || !e->Uocp1_p))
-      return fail(MPCEKF_E_ROM, "rom: tab_npoly = %d but a polynomial table is missing", R->tab_npoly);
+    const double *ps[6] = {e->Uocp_p, e->dUocp_p, e->k0_p, e->Rf_p, e->Cdleff_p, e->Uocp1_p};
+    for (int f = 0; f < 6; ++f) {
+      const int m = e->nnode[f];
+      if (m != 0 && (!R->tab_npoly || m < 2 || !e->node[f] || !e->node_p[f]))
+        return fail(MPCEKF_E_ROM, "rom: nnode[%d] = %d needs tab_npoly, >= 2 nodes and their tables", f, m);
+      if (R->tab_npoly && m == 0 && !ps[f])
+        return fail(MPCEKF_E_ROM, "rom: tab_npoly = %d but polynomial table %d is missing", R->tab_npoly, f);
+      for (int j = 0; j < m; ++j)  // strictly ascending, finite; interior nodes inside (0, 1)
+        if (!std::isfinite(e->node[f][j]) || (j && !(e->node[f][j] > e->node[f][j - 1])) ||
+            (j > 0 && j < m - 1 && !(e->node[f][j] > 0.0 && e->node[f][j] < 1.0)))
+          return fail(MPCEKF_E_ROM, "rom: theta nodes of table %d must be finite, ascending, interior in (0, 1)", f);
+    }
     for (int f = 0; f < 5; ++f)
       if (!std::isfinite(e->Ea[f])) return fail(MPCEKF_E_ROM, "rom: Ea[%d] is not finite", f);
   }
@@ -397,8 +562,9 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
   const int np = R->tab_npoly;
   const size_t nint = (size_t)(nth - 1);
   // the kernels' lookup descriptors (mpcekf_kernels.hip etab_desc): per function and side
-  // Ea/R, (off, istride), (jstride, ro) in doubles of ptab; Uocp1 of each side last
+  // Ea/R, (off, istride), (jstride, ro), (mapoff, nu) in doubles of ptab; Uocp1 of each side last
   double desc[12][KDESC] = {};
+  bool any_nodes = false;
   auto pack2 = [](long long lo, long long hi) {
     const unsigned long long w = (unsigned long long)(uint32_t)lo | (unsigned long long)(uint32_t)hi << 32;
     double d;
@@ -410,11 +576,56 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       for (int j = 0; j < rows; ++j)
         for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[((size_t)j * nint + i) * np + c] : 0.0);
   };
+  // ABI v4: a function on its own nodes -- its rows [rows][m-1][np] interval-major like v3's,
+  // and a bucket map: nu (a power of two) buckets over [0, 1] with at most one interior node
+  // inside each, so that floor(theta nu) and one compare give the oracle's segment
+  // k = #{j in 1..m-2 : x_j <= theta}; entry u = (k of u / nu, x_k, x_k+1 or +inf, 0)
+  auto add_nodes = [&](double *d, const double *x, int m, const double *src, int rows) -> int {
+    const int nseg = m - 1;
+    int nu = 1;
+    for (;; nu *= 2) {
+      bool ok = true;
+      for (int j = 2; j < m - 1 && ok; ++j)  // interior nodes j-1, j in one bucket?
+        ok = std::floor(x[j] * nu) != std::floor(x[j - 1] * nu);
+      if (ok) break;
+      if (nu >= (1 << 20)) return fail(MPCEKF_E_ROM, "rom: theta nodes closer than 2^-20");
+    }
+    d[1] = pack2((long long)ptab.size(), (long long)rows * KPOLY);
+    d[2] = pack2(rows > 1 ? KPOLY : 0, rows > 1 ? KPOLY : 0);
+    for (int i = 0; i < nseg; ++i)
+      for (int j = 0; j < rows; ++j)
+        for (int c = 0; c < KPOLY; ++c) ptab.push_back(c < np ? src[((size_t)j * nseg + i) * np + c] : 0.0);
+    if (ptab.size() & 1) ptab.push_back(0.0);  // 16-byte map entries
+    d[3] = pack2((long long)ptab.size(), nu);
+    for (int u = 0; u < nu; ++u) {
+      const double e = (double)u / nu;  // exact: nu is a power of two
+      int k = 0;
+      while (k + 1 <= m - 2 && x[k + 1] <= e) ++k;
+      ptab.push_back((double)k);
+      ptab.push_back(x[k]);
+      ptab.push_back(k + 1 <= m - 2 ? x[k + 1] : HUGE_VAL);
+      ptab.push_back(0.0);
+    }
+    any_nodes = true;
+    return MPCEKF_OK;
+  };
   bool theta_const = true;
   if (const char *ev = std::getenv("MPCEKF_THETA_CONST")) theta_const = std::atoi(ev) != 0;
   for (int fn = 0; fn < 5 && poly; ++fn)  // EF_U, EF_DU, EF_K0, EF_RF, EF_CDL
     for (int sd = 0; sd < 2; ++sd) {
       const mpcekf_electrode *e = els[sd];
+      if (e->nnode[fn] >= 2) {  // v4: on its own nodes
+        const int m = e->nnode[fn];
+        const double *src = e->node_p[fn];
+        const size_t rl = (size_t)(m - 1) * np;
+        bool same = nte > 1;
+        for (int j = 1; j < nte && same; ++j) same = std::memcmp(src, src + j * rl, rl * sizeof(double)) == 0;
+        double *d = desc[fn * 2 + sd];
+        d[0] = e->Ea[fn] != 0.0 ? e->Ea[fn] / R->R : 0.0;
+        int rc = add_nodes(d, e->node[fn], m, src, same ? 1 : nte);
+        if (rc) return rc;
+        continue;
+      }
       const double *src =
           fn == 0 ? e->Uocp_p : fn == 1 ? e->dUocp_p : fn == 2 ? e->k0_p : fn == 3 ? e->Rf_p : e->Cdleff_p;
       bool same = nte > 1;
@@ -445,6 +656,11 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
       }
   if (poly)
     for (int sd = 0; sd < 2; ++sd) {
+      if (els[sd]->nnode[5] >= 2) {
+        int rc = add_nodes(desc[10 + sd], els[sd]->node[5], els[sd]->nnode[5], els[sd]->node_p[5], 1);
+        if (rc) return rc;
+        continue;
+      }
       desc[10 + sd][1] = pack2((long long)ptab.size(), KPOLY);
       add_poly(els[sd]->Uocp1_p, 1);
     }
@@ -453,6 +669,7 @@ static int build_rom(mpcekf_ctx *X, const mpcekf_rom *R) {
     for (auto &d : desc) tabs.insert(tabs.end(), d, d + KDESC);
   }
   r.npoly = poly ? KPOLY : 0;
+  r.nodes = any_nodes ? 1 : 0;
   r.arr = 0;
   for (int f = 0; f < 5; ++f)
     for (int sd = 0; sd < 2; ++sd) r.arr |= poly && els[sd]->Ea[f] != 0.0;
@@ -641,8 +858,12 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
     int64_t side_max = 16384;
     if (const char *e = std::getenv("MPCEKF_BOUNDS_SIDE")) side_max = std::atoll(e);
     if (const char *e = std::getenv("MPCEKF_BOUNCE_MAX")) X->bounce_max = (size_t)std::atoll(e);
+    if (const char *e = std::getenv("MPCEKF_CHUNK")) X->xchunk = std::max<size_t>((size_t)std::atoll(e), 4096);
     X->bounds_side = ncells <= side_max;
   }
+  X->copier = new (std::nothrow) Copier();
+  if (!X->copier) { mpcekf_ctx_destroy(X); return fail(MPCEKF_E_HIP, "out of host memory"); }
+  X->copier->start(copy_threads(), device);
   hipError_t e = hipStreamCreateWithFlags(&X->stream, hipStreamNonBlocking);
   if (e == hipSuccess && (X->flush_roll || X->bounds_side)) {
     e = hipStreamCreateWithFlags(&X->fstream, hipStreamNonBlocking);
@@ -713,8 +934,11 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
 int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   if (!X) return MPCEKF_OK;
   (void)hipSetDevice(X->device);
-  if (X->stream) (void)hipStreamSynchronize(X->stream);
+  if (X->stream) (void)X->drain();  // pending _async copies finish before their buffers go
   if (X->fstream) (void)hipStreamSynchronize(X->fstream);
+  delete X->copier;
+  X->copier = nullptr;
+  for (hipEvent_t e : X->xev) (void)hipEventDestroy(e);
   for (hipEvent_t e : X->ev) (void)hipEventDestroy(e);
   if (X->ev_fork) (void)hipEventDestroy(X->ev_fork);
   if (X->ev_join) (void)hipEventDestroy(X->ev_join);
@@ -1173,7 +1397,8 @@ int mpcekf_dev_copy2d(void *dst, int64_t dpitch, const void *src, int64_t spitch
 int mpcekf_sync(mpcekf_ctx *X) {
   if (!X) return fail(MPCEKF_E_ARG, "null ctx");
   HIPCHK(hipSetDevice(X->device));
-  HIPCHK(hipStreamSynchronize(X->stream));
+  int rc = X->drain();  // the _async stage calls' host outputs are written when this returns
+  if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());
   return MPCEKF_OK;
 }
@@ -1202,61 +1427,60 @@ struct Slab {
   }
 };
 // A stage call's host copies, through the context's pinned bounce buffer: inputs are copied
-// into it and sent from there, outputs land in it and are copied out after the call's stream
-// synchronisation (finish).  Copies straight from / into the caller's pageable arrays let the
-// runtime pin and cache those pages; the drop-ins' callers (MATLAB's mxArrays, numpy) free
-// and reallocate their arrays every call, and the stage sequence then stalled 10-20 ms in
-// whichever call came next (tools/dropin_probe.py: 0.6 ms with every array kept alive, 10-14
-// ms when freed, reused or not allocated; profiles/r05e_dropin_probe.jsonl).
+// into it and sent from there; outputs are DMA'd into it in chunks and copied out by the
+// context's worker pool as each chunk's event completes (Copier), which the call's
+// synchronisation (finish) waits for -- or, for an _async call (finish_async), the next one.
+// Copies straight from / into the caller's pageable arrays let the runtime pin and cache
+// those pages; the drop-ins' callers (MATLAB's mxArrays, numpy) free and reallocate their
+// arrays every call, and the stage sequence then stalled 10-20 ms in whichever call came
+// next (tools/dropin_probe.py: 0.6 ms with every array kept alive, 10-14 ms when freed,
+// reused or not allocated; profiles/r05e_dropin_probe.jsonl).
 struct Xfer {
   mpcekf_ctx *X;
-  size_t off = 0;
-  struct Out {
-    void *dst;
-    size_t at, bytes;
-  };
-  std::vector<Out> outs;
-  // bounced when below the cap and inside the buffer the call reserved (a copy beyond the
+  // bounced when below the cap and inside the buffer reserved (a copy beyond the
   // reservation goes direct rather than past the buffer's end)
-  bool fits(size_t b) const { return b <= X->bounce_max && off + pad(b) <= X->h_bytes; }
+  bool fits(size_t b) const { return b <= X->bounce_max && X->xoff + pad(b) <= X->h_bytes; }
   static size_t pad(size_t b) { return (b + 255) & ~(size_t)255; }
-  // capacity for the call's copies (sum of pad(bytes) over them)
-  int reserve(size_t bytes) { return X->bounce(bytes); }
+  // capacity for the call's copies: pad(bytes) summed over those that will be bounced
+  // (bounce_max caps a copy; MPCEKF_BOUNCE_MAX=0 pins nothing)
+  int reserve(const std::vector<size_t> &copies) {
+    size_t sum = 0;
+    for (size_t b : copies)
+      if (b && b <= X->bounce_max) sum += pad(b);
+    return sum ? X->bounce(sum) : MPCEKF_OK;
+  }
   hipError_t in(void *d, const void *h, size_t b) {
     if (!b) return hipSuccess;
     if (!fits(b)) return hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, X->stream);
-    char *p = X->h_bounce + off;
-    off += pad(b);
+    char *p = X->h_bounce + X->xoff;
+    X->xoff += pad(b);
     std::memcpy(p, h, b);
     return hipMemcpyAsync(d, p, b, hipMemcpyHostToDevice, X->stream);
   }
   hipError_t out(void *h, const void *d, size_t b) {
     if (!b) return hipSuccess;
     if (!fits(b)) return hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, X->stream);
-    outs.push_back({h, off, b});
-    char *p = X->h_bounce + off;
-    off += pad(b);
-    return hipMemcpyAsync(p, d, b, hipMemcpyDeviceToHost, X->stream);
-  }
-  // after the call's synchronisation: the outputs out of the bounce buffer; copies of 4 MiB
-  // and more each get a thread (iterEKF's zk and zbk are 15 MiB each at 65,536 cells)
-  int finish() {
-    HIPCHK(hipStreamSynchronize(X->stream));
-    std::vector<std::thread> th;
-    for (const Out &o : outs) {
-      bool spawned = false;
-      if (o.bytes >= ((size_t)4 << 20) && th.size() < 3) {
-        try {  // no exception crosses the C-ABI: a thread that cannot start copies inline
-          th.emplace_back([this, o]() { std::memcpy(o.dst, X->h_bounce + o.at, o.bytes); });
-          spawned = true;
-        } catch (...) {
-        }
-      }
-      if (!spawned) std::memcpy(o.dst, X->h_bounce + o.at, o.bytes);
+    char *p = X->h_bounce + X->xoff;
+    X->xoff += pad(b);
+    for (size_t o = 0; o < b; o += X->xchunk) {
+      const size_t len = std::min(X->xchunk, b - o);
+      hipError_t e = hipMemcpyAsync(p + o, (const char *)d + o, len, hipMemcpyDeviceToHost, X->stream);
+      hipEvent_t ev = nullptr;
+      if (e == hipSuccess) e = X->next_event(&ev);
+      if (e == hipSuccess) e = hipEventRecord(ev, X->stream);
+      if (e != hipSuccess) return e;
+      X->copier->push({ev, p + o, (char *)h + o, len});
     }
-    for (std::thread &t : th) t.join();
+    return hipSuccess;
+  }
+  // the synchronous call's end: every output (this call's and any earlier _async call's) written
+  int finish() { return X->drain(); }
+  // an _async call's end: its copies stay in flight until mpcekf_sync or a synchronous call
+  int finish_async() {
+    X->xpending = true;
     return MPCEKF_OK;
   }
+  int end(bool async) { return async ? finish_async() : finish(); }
 };
 static int set_tc(mpcekf_ctx *X, const double *tc, Xfer *xf) {
   if (!tc) return MPCEKF_OK;
@@ -1268,13 +1492,13 @@ static int set_tc(mpcekf_ctx *X, const double *tc, Xfer *xf) {
 }
 extern "C" {
 
-int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
+static int plant_step_impl(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!iapp || !vcell) return fail(MPCEKF_E_ARG, "plant_step: null argument");
   size_t n = (size_t)X->n;
   Xfer xf{X};
-  if ((rc = xf.reserve(3 * Xfer::pad(n * 8)))) return rc;
+  if ((rc = xf.reserve({n * 8, n * 8, n * 8}))) return rc;
   if ((rc = set_tc(X, tc_degC, &xf))) return rc;
   if ((rc = X->tmp(2 * n * 8 + 512))) return rc;
   Slab sl{(char *)X->d_tmp};
@@ -1283,17 +1507,23 @@ int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, 
   if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, nullptr, X->stream), "plant"))) return rc;
   if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
   HIPCHK(xf.out(vcell, dv, n * 8));
-  return xf.finish();
+  return xf.end(async);
+}
+int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
+  return plant_step_impl(X, iapp, tc_degC, vcell, false);
+}
+int mpcekf_plant_step_async(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
+  return plant_step_impl(X, iapp, tc_degC, vcell, true);
 }
 
-int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
-                    double *boundzk, int32_t *xind_model, double *xind_gamma) {
+static int ekf_step_impl(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                    double *boundzk, int32_t *xind_model, double *xind_gamma, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!vk || !ik) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
   Xfer xf{X};
-  if ((rc = xf.reserve(3 * Xfer::pad(n * 8) + 2 * Xfer::pad(n * nzz * 8) + Xfer::pad(16 * n) + Xfer::pad(32 * n))))
+  if ((rc = xf.reserve({n * 8, n * 8, n * 8, n * nzz * 8, n * nzz * 8, 16 * n, 32 * n})))
     return rc;
   if ((rc = set_tc(X, tk_degC, &xf))) return rc;
   if ((rc = X->tmp((2 * n + n * nzz) * 8 + 2048)) || (rc = X->stage_bufs())) return rc;
@@ -1326,13 +1556,21 @@ int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const dou
   if (boundzk) HIPCHK(xf.out(boundzk, dzb, n * nzz * 8));
   if (xind_model) HIPCHK(xf.out(xind_model, dxm, 4 * n * 4));
   if (xind_gamma) HIPCHK(xf.out(xind_gamma, dxg, 4 * n * 8));
-  if ((rc = xf.finish())) return rc;
+  if ((rc = xf.end(async))) return rc;
   X->stage_zk = true;
   return MPCEKF_OK;
 }
+int mpcekf_ekf_step(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                    double *boundzk, int32_t *xind_model, double *xind_gamma) {
+  return ekf_step_impl(X, vk, ik, tk_degC, zk, boundzk, xind_model, xind_gamma, false);
+}
+int mpcekf_ekf_step_async(mpcekf_ctx *X, const double *vk, const double *ik, const double *tk_degC, double *zk,
+                    double *boundzk, int32_t *xind_model, double *xind_gamma) {
+  return ekf_step_impl(X, vk, ik, tk_degC, zk, boundzk, xind_model, xind_gamma, true);
+}
 
-int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
-                     const double *tk_degC, double *lin) {
+static int linearize_impl(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                     const double *tk_degC, double *lin, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!zk != !xind_model || !xind_model != !xind_gamma)
@@ -1340,8 +1578,7 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
   if (!zk && !X->stage_zk) return fail(MPCEKF_E_STATE, "linearize: NULL zk / Xind but no mpcekf_ekf_step before it");
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
   Xfer xf{X};
-  if ((rc = xf.reserve(Xfer::pad(n * 8) + Xfer::pad(n * nzz * 8) + Xfer::pad(16 * n) + Xfer::pad(32 * n) +
-                       Xfer::pad(n * MPCEKF_LIN_SIZE * 8))))
+  if ((rc = xf.reserve({n * 8, n * nzz * 8, 16 * n, 32 * n, n * MPCEKF_LIN_SIZE * 8})))
     return rc;
   if ((rc = set_tc(X, tk_degC, &xf))) return rc;
   if ((rc = X->tmp((n * nzz + 4 * n) * 8 + 4 * n * 4 + 2048)) || (rc = X->stage_bufs())) return rc;
@@ -1365,18 +1602,30 @@ int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model,
   X->stage_lin = false;
   if ((rc = lerr(launch_cell(X->r, X->k, X->s, io, X->stream), "cell"))) return rc;
   if (lin) HIPCHK(xf.out(lin, dl, n * MPCEKF_LIN_SIZE * 8));
-  if ((rc = xf.finish())) return rc;
+  if ((rc = xf.end(async))) return rc;
   X->stage_lin = true;
   return MPCEKF_OK;
 }
+int mpcekf_linearize(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                     const double *tk_degC, double *lin) {
+  return linearize_impl(X, zk, xind_model, xind_gamma, tk_degC, lin, false);
+}
+int mpcekf_linearize_async(mpcekf_ctx *X, const double *zk, const int32_t *xind_model, const double *xind_gamma,
+                     const double *tk_degC, double *lin) {
+  return linearize_impl(X, zk, xind_model, xind_gamma, tk_degC, lin, true);
+}
 
-int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const double *set, double *out) {
+static int lin_fields_impl(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const double *set, double *out, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!X->stage_lin) return fail(MPCEKF_E_STATE, "lin_fields: no mpcekf_linearize record on the device");
   if (nslots < 0 || nslots > MPCEKF_LIN_SIZE || (nslots && !slots)) return fail(MPCEKF_E_ARG, "lin_fields: bad slots");
-  for (int i = 0; i < nslots; ++i)
+  uint64_t seen = 0;  // a repeated slot would have several threads scatter into one record element
+  for (int i = 0; i < nslots; ++i) {
     if (slots[i] < 0 || slots[i] >= MPCEKF_LIN_SIZE) return fail(MPCEKF_E_ARG, "lin_fields: slot %d", slots[i]);
+    if (seen >> slots[i] & 1) return fail(MPCEKF_E_ARG, "lin_fields: slot %d given twice", slots[i]);
+    seen |= (uint64_t)1 << slots[i];
+  }
   if (!nslots || (!set && !out)) return MPCEKF_OK;
   // the slots gathered into / scattered from a compact [ncells][nslots] device buffer, which
   // crosses PCIe in one copy: only the named doubles move (per-slot pitched copies of 8-byte
@@ -1387,7 +1636,7 @@ int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const
   double *dc = sl.take<double>(n * (size_t)nslots);
   int *ds = sl.take<int>((size_t)nslots);
   Xfer xf{X};
-  if ((rc = xf.reserve(Xfer::pad((size_t)nslots * sizeof(int)) + 2 * Xfer::pad(bytes)))) return rc;
+  if ((rc = xf.reserve({(size_t)nslots * sizeof(int), bytes, bytes}))) return rc;
   HIPCHK(xf.in(ds, slots, (size_t)nslots * sizeof(int)));
   if (set) {
     HIPCHK(xf.in(dc, set, bytes));
@@ -1397,15 +1646,24 @@ int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const
     if ((rc = lerr(launch_cols(X->d_slin, X->n, MPCEKF_LIN_SIZE, ds, nslots, dc, false, X->stream), "cols"))) return rc;
     HIPCHK(xf.out(out, dc, bytes));
   }
-  return xf.finish();
+  return xf.end(async);
+}
+int mpcekf_lin_fields(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const double *set, double *out) {
+  return lin_fields_impl(X, slots, nslots, set, out, false);
+}
+int mpcekf_lin_fields_async(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, const double *set, double *out) {
+  return lin_fields_impl(X, slots, nslots, set, out, true);
 }
 
 int mpcekf_mpc_step(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec) {
   return mpcekf_mpc_step_ex(X, lin, soc_k1, uk, nexec, nullptr, nullptr, nullptr, nullptr);
 }
+int mpcekf_mpc_step_async(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec) {
+  return mpcekf_mpc_step_ex_async(X, lin, soc_k1, uk, nexec, nullptr, nullptr, nullptr, nullptr);
+}
 
-int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
-                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol) {
+static int mpc_step_ex_impl(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
@@ -1417,7 +1675,7 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
   double *dju = sl.take<double>(n), *djf = sl.take<double>(n), *dnd = sl.take<double>(n);
   int *dn = sl.take<int>(n), *dv = sl.take<int>(n);
   Xfer xf{X};
-  if ((rc = xf.reserve(Xfer::pad(n * MPCEKF_LIN_SIZE * 8) + 5 * Xfer::pad(n * 8) + 2 * Xfer::pad(n * 4)))) return rc;
+  if ((rc = xf.reserve({n * MPCEKF_LIN_SIZE * 8, n * 8, n * 8, n * 8, n * 8, n * 8, n * 4, n * 4}))) return rc;
   if (lin) HIPCHK(xf.in(dl, lin, n * MPCEKF_LIN_SIZE * 8));
   else dl = X->d_slin;  // the device-resident record of the last mpcekf_linearize
   HIPCHK(xf.in(ds, soc_k1, n * 8));
@@ -1445,10 +1703,18 @@ int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, d
   if (J_fin) HIPCHK(xf.out(J_fin, djf, n * 8));
   if (norm_du) HIPCHK(xf.out(norm_du, dnd, n * 8));
   if (nviol) HIPCHK(xf.out(nviol, dv, n * 4));
-  return xf.finish();
+  return xf.end(async);
+}
+int mpcekf_mpc_step_ex(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol) {
+  return mpc_step_ex_impl(X, lin, soc_k1, uk, nexec, J_unc, J_fin, norm_du, nviol, false);
+}
+int mpcekf_mpc_step_ex_async(mpcekf_ctx *X, const double *lin, const double *soc_k1, double *uk, int32_t *nexec,
+                       double *J_unc, double *J_fin, double *norm_du, int32_t *nviol) {
+  return mpc_step_ex_impl(X, lin, soc_k1, uk, nexec, J_unc, J_fin, norm_du, nviol, true);
 }
 
-int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
+static int mpc_diag_impl(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (!lin && !X->stage_lin) return fail(MPCEKF_E_STATE, "mpc_diag: NULL lin but no mpcekf_linearize record");
@@ -1459,8 +1725,7 @@ int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double
   double *dl = sl.take<double>(n * MPCEKF_LIN_SIZE), *du = sl.take<double>(n), *dp = sl.take<double>(n * 2 * NA),
          *ds = sl.take<double>(n * NA);
   Xfer xf{X};
-  if ((rc = xf.reserve(Xfer::pad(n * MPCEKF_LIN_SIZE * 8) + Xfer::pad(n * 8) + Xfer::pad(n * 2 * NA * 8) +
-                       Xfer::pad(n * NA * 8))))
+  if ((rc = xf.reserve({n * MPCEKF_LIN_SIZE * 8, n * 8, n * 2 * NA * 8, n * NA * 8})))
     return rc;
   if (lin) HIPCHK(xf.in(dl, lin, n * MPCEKF_LIN_SIZE * 8));
   else dl = X->d_slin;
@@ -1471,7 +1736,13 @@ int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double
   if ((rc = lerr(rc, "cl_diag"))) return rc;
   if (poles) HIPCHK(xf.out(poles, dp, n * 2 * NA * 8));
   if (sv) HIPCHK(xf.out(sv, ds, n * NA * 8));
-  return xf.finish();
+  return xf.end(async);
+}
+int mpcekf_mpc_diag(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
+  return mpc_diag_impl(X, lin, uk_1, poles, sv, false);
+}
+int mpcekf_mpc_diag_async(mpcekf_ctx *X, const double *lin, const double *uk_1, double *poles, double *sv) {
+  return mpc_diag_impl(X, lin, uk_1, poles, sv, true);
 }
 
 // ---- context-free kernels ----------------------------------------------------
@@ -1662,8 +1933,8 @@ int mpcekf_get_state(mpcekf_ctx *X, mpcekf_state *st) {
   return MPCEKF_OK;
 }
 
-int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
-                       int32_t *status) {
+static int get_scalars_impl(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                            int32_t *status, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
   if (nslots < 0 || nslots > MPCEKF_NSCAL || (nslots && (!slots || !scal)))
@@ -1671,19 +1942,33 @@ int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, doub
   for (int j = 0; j < nslots; ++j)
     if (slots[j] < 0 || slots[j] >= MPCEKF_NSCAL) return fail(MPCEKF_E_ARG, "get_scalars: slot %d", slots[j]);
   const size_t n = (size_t)X->n;
-  // the SoA scalar block holds each slot as one contiguous [ncells] vector: exactly the
-  // requested slots cross PCIe
-  std::vector<double> sc(n * (size_t)nslots);
+  // the SoA scalar block holds each slot as one contiguous [ncells] vector; a gather kernel
+  // (k_rows) lays the requested ones out cell-major, so exactly those bytes cross PCIe in one
+  // copy and the host does no transposition (nor the _async form at its synchronisation)
+  int rows[MPCEKF_NSCAL];
+  for (int j = 0; j < nslots; ++j) rows[j] = kScalMap[slots[j]];
+  if ((rc = X->tmp(n * (size_t)nslots * 8 + 1024))) return rc;
+  Slab sl{(char *)X->d_tmp};
+  double *dc = sl.take<double>(n * (size_t)nslots);
+  int *dr = sl.take<int>(MPCEKF_NSCAL);
   Xfer xf{X};
-  if ((rc = xf.reserve((size_t)nslots * Xfer::pad(n * 8) + 2 * Xfer::pad(n * 4)))) return rc;
-  for (int j = 0; j < nslots; ++j)
-    HIPCHK(xf.out(sc.data() + (size_t)j * n, X->d_scal + (size_t)kScalMap[slots[j]] * n, n * 8));
+  if ((rc = xf.reserve({sizeof rows, n * (size_t)nslots * 8, n * 4, n * 4}))) return rc;
+  if (nslots) {
+    HIPCHK(xf.in(dr, rows, (size_t)nslots * sizeof(int)));
+    if ((rc = lerr(launch_rows(X->d_scal, X->n, dr, nslots, dc, X->stream), "rows"))) return rc;
+    HIPCHK(xf.out(scal, dc, n * (size_t)nslots * 8));
+  }
   if (warn) HIPCHK(xf.out(warn, X->s.warn, n * 4));
   if (status) HIPCHK(xf.out(status, X->s.status, n * 4));
-  if ((rc = xf.finish())) return rc;
-  for (size_t c = 0; c < n; ++c)
-    for (int j = 0; j < nslots; ++j) scal[c * nslots + j] = sc[(size_t)j * n + c];
-  return MPCEKF_OK;
+  return xf.end(async);
+}
+int mpcekf_get_scalars(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                       int32_t *status) {
+  return get_scalars_impl(X, slots, nslots, scal, warn, status, false);
+}
+int mpcekf_get_scalars_async(mpcekf_ctx *X, const int32_t *slots, int32_t nslots, double *scal, int32_t *warn,
+                             int32_t *status) {
+  return get_scalars_impl(X, slots, nslots, scal, warn, status, true);
 }
 
 int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {

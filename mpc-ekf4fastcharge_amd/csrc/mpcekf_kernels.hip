@@ -222,6 +222,29 @@ __device__ __forceinline__ void tabp2(const double *c, int n, double x, int istr
   b = horner6(b01, b23, b45, s);
   if (MPCEKF_PL_BRANCHFREE && x != x) a = b = __builtin_nan("");
 }
+// ABI v4 rows on a function's own theta nodes (include/mpcekf.h node / node_p): the segment
+// k = #{j in 1..m-2 : x_j <= theta} (oracle node_poly) from the function's uniform bucket map
+// (host build_rom: nu buckets over [0, 1], nu a power of two, each bucket holding at most
+// one interior node; entry u = (k of u / nu, x_k, x_k+1 or +inf)): floor(theta nu) is exact,
+// so the bucket's left edge lies at or below theta and one compare with x_k+1 finishes the
+// search.  s = theta - x_k, then Horner over the segment's 6 coefficients as tabp2.
+__device__ __forceinline__ void tabn2(const double *c, const double *map, int nu, double x, int istride, double &a,
+                                      double &b, int ro) {
+  const double xc = fmin(fmax(x, 0.0), 1.0);  // NaN x: 0 (fmax), the NaN selected below
+  int u = (int)floor(xc * (double)nu);
+  u = u > nu - 1 ? nu - 1 : u;
+  const double2 *m = reinterpret_cast<const double2 *>(map + (size_t)u * KMAP);
+  const double2 m0 = m[0], m1 = m[1];
+  const bool up = xc >= m1.x;
+  const int i = (int)m0.x + (up ? 1 : 0);
+  const double s = xc - (up ? m1.x : m0.y);
+  const double2 *p = reinterpret_cast<const double2 *>(c + (size_t)i * istride);
+  const double2 *q = reinterpret_cast<const double2 *>(c + (size_t)i * istride + ro);
+  const double2 a01 = p[0], a23 = p[1], a45 = p[2], b01 = q[0], b23 = q[1], b45 = q[2];
+  a = horner6(a01, a23, a45, s);
+  b = horner6(b01, b23, b45, s);
+  if (x != x) a = b = __builtin_nan("");
+}
 // Defined exp of the v3 Arrhenius factor (oracle/mpcekf_oracle.c orc_exp, rom.py dexp):
 // x = k ln2 + r, k = floor(x / ln2 + 1/2), fdlibm's rational form for exp(r); only
 // +, -, *, /, floor and ldexp, exact or correctly rounded on both sides.
@@ -272,7 +295,8 @@ __device__ __forceinline__ bool rowf(const KRom &r, int q, unsigned G) {
 enum { EF_U = 0, EF_DU, EF_K0, EF_RF, EF_CDL, NEF };
 __host__ __device__ constexpr int etab_header(int nth) { return 2 * nth + 5 * MAXTT; }
 // v3: the 12 lookup descriptors after the soc ends (d = fn * 2 + side, Uocp1 10 + side),
-// KDESC doubles each: Ea/R, then int32 pairs (off, istride), (jstride, ro) as raw bits
+// KDESC doubles each: Ea/R, then int32 pairs (off, istride), (jstride, ro), (mapoff, nu) as
+// raw bits (nu = 0: the uniform grid; v4: the function's bucket map at poly + mapoff)
 __host__ __device__ constexpr int etab_desc(int hn) { return 2 * hn + 5 * MAXTT; }
 struct ETab {
   const double *b;  // LDS base of the tables
@@ -301,7 +325,16 @@ struct ETab {
       const long long w0 = __double_as_longlong(dp[1]), w1 = __double_as_longlong(dp[2]);
       const int off = (int)w0, istr = (int)(w0 >> 32), jstr = (int)w1, ro = (int)(w1 >> 32);
       double a, c;
-      tabp2(r->poly + off + j * jstr, nth, th, istr, a, c, ro);
+      int nu = 0, moff = 0;
+      if (r->nodes) {  // a uniform flag: v3 ROMs never read the map word
+        const long long w3 = __double_as_longlong(dp[3]);
+        nu = __builtin_amdgcn_readfirstlane((int)(w3 >> 32));
+        moff = __builtin_amdgcn_readfirstlane((int)w3);
+      }
+      if (nu == 0)
+        tabp2(r->poly + off + j * jstr, nth, th, istr, a, c, ro);
+      else
+        tabn2(r->poly + off + j * jstr, r->poly + moff, nu, th, istr, a, c, ro);
       a = a + g * (c - a);
 #if MPCEKF_PL_BRANCHFREE
       // every function multiplied by its factor, dexp(+-0) = 1 exactly when Ea = 0 (a * 1 = a:
@@ -320,7 +353,17 @@ struct ETab {
   }
   __device__ __forceinline__ double u1(int side, double th) const {
     if (pl) {
-      const long long w0 = __double_as_longlong(b[etab_desc(hn) + (10 + side) * KDESC + 1]);
+      const double *dp = b + etab_desc(hn) + (10 + side) * KDESC;
+      const long long w0 = __double_as_longlong(dp[1]);
+      if (r->nodes) {
+        const long long w3 = __double_as_longlong(dp[3]);
+        const int nu = __builtin_amdgcn_readfirstlane((int)(w3 >> 32));
+        if (nu) {
+          double a, c;
+          tabn2(r->poly + (int)w0, r->poly + __builtin_amdgcn_readfirstlane((int)w3), nu, th, (int)(w0 >> 32), a, c, 0);
+          return a;
+        }
+      }
       return tabp(r->poly + (int)w0, nth, th, (int)(w0 >> 32));
     }
     return tabi(b + side * nth, nth, th);
@@ -1045,7 +1088,7 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
         double t = K[i];
 #pragma unroll
         for (int k = 0; k < NC; ++k) t = __builtin_fma(Mf(i, k), v[k], t);
-        w = __builtin_fma(hii, lam[i], -t) / hii;
+        w = hild_w(t, hii, 1.0 / hii, lam[i]);
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1155,31 +1198,11 @@ __device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], X
     fin = fin && isfinite(xval(Xs, j, 0)) && isfinite(xval(Xs, j, 1)) && isfinite(Mf(j, 0)) && isfinite(Mf(j, 1));
 }
 
-// x / y, correctly rounded, with the divisor-only part of the hardware division
-// sequence (v_rcp_f64 + two Newton steps) independent of x, so it overlaps the
-// sweep's serial chain.  For |x|, |y| in [2^-400, 2^400] (or x == 0)
-// v_div_scale / v_div_fmas / v_div_fixup are identities and this is bit-identical
-// to the compiled x / y (tools/micro/div_check.hip: 2.1e9 random pairs, 0
-// mismatches); y == +-0 gives x * (1/y) = x / y exactly (inf / NaN by IEEE).  The
-// caller checks the domain (hild_stage once per divisor, the x range per sweep).
-__device__ __forceinline__ double div_fast(double x, double y) {
-  double r = __builtin_amdgcn_rcp(y);
-  const double r0 = r;
-  double e = __builtin_fma(-y, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-y, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  const double q0 = x * r;
-  const double e2 = __builtin_fma(-y, q0, x);
-  const double q = __builtin_fma(e2, r, q0);
-  return y == 0.0 ? x * r0 : q;
-}
-
 // Per-lane LDS of the rank-2 sweeps: the 18 distinct X(:,i) (rows 0-7 of
 // [Cu; -Cu; I; -I] are +-a, +-b, +-c) and the 18 distinct (H_ii, 1/H_ii) pairs (H_ii of
 // a negated row is bit-identical: (-1)(-x) = x, and its 0 * (-x) term only meets
 // a nonzero sum or +0).  Layout [slot][64 lanes] double2: every read is one
-// conflict-free ds_read_b128 per wave.  1/H_ii is div_fast's divisor-only part.
+// conflict-free ds_read_b128 per wave.  1/H_ii is the correctly rounded reciprocal of hild_w.
 constexpr int HS_X = 3 + 3 * NP, HS_SLOTS = 2 * HS_X;
 constexpr int HILD_LDS_PER_WAVE = HS_SLOTS * 64 * 16;  // bytes
 __device__ __forceinline__ constexpr int hslot(int i) {
@@ -1187,28 +1210,20 @@ __device__ __forceinline__ constexpr int hslot(int i) {
 }
 __device__ __forceinline__ constexpr bool hneg(int i) { return i == 2 || i == 3 || i == 6 || i == 7; }
 // The first row of each Toeplitz block is (H(0), 0): all zero when H(0) = 0, as for the
-// SOC block (predMat: G(1,1) = +0), so its H_ii may be 0.  These rows keep x / +-0 =
-// x * (1 / +-0) exactly (inf / NaN by IEEE) through a select; a zero H_ii elsewhere sends
-// the lane to the exact path.
-__device__ __forceinline__ constexpr bool hzero_row(int i) { return i >= 8 && (i - 8) % NP == 0; }
+// SOC block (predMat: G(1,1) = +0), so its H_ii may be 0; 1/H_ii is then +-inf and hild_w's
+// fma gives x / +-0's inf / NaN by IEEE without a select.
 __device__ __forceinline__ double2 hx(const double2 *hl, int i) {  // X(:,i)
   const double2 x = hl[hslot(i) * 64];
   return hneg(i) ? make_double2(-x.x, -x.y) : x;
 }
-__device__ __forceinline__ double2 hh(const double2 *hl, int i) {  // (H_ii, 1/H_ii refined)
+__device__ __forceinline__ double2 hh(const double2 *hl, int i) {  // (H_ii, 1/H_ii)
   return hl[(HS_X + hslot(i)) * 64];
 }
 __device__ __forceinline__ double2 *hild_lane_lds(double2 *base) {  // blocks of 256 threads
   return base + (threadIdx.x >> 6) * (HS_SLOTS * 64) + (threadIdx.x & 63);
 }
-__device__ __forceinline__ double rcp_refined(double y) {
-  double r = __builtin_amdgcn_rcp(y);
-  double e = __builtin_fma(-y, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-y, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-// Fills the lane's slots; returns whether every H_ii is in div_fast's divisor domain.
+// Fills the lane's slots; returns whether every H_ii is in hild_w's reciprocal domain
+// (hild_rok: 0 or [2^-1020, 2^1020]), where a row is the single fma(-t, 1/H_ii, lambda_i).
 __device__ __forceinline__ bool hild_stage(const Cons &Cn, const XS &Xs, double2 *hl) {
   ConsM Mf{Cn};
   bool yok = true;
@@ -1217,11 +1232,9 @@ __device__ __forceinline__ bool hild_stage(const Cons &Cn, const XS &Xs, double2
     const int i = sl == 0 ? 0 : sl == 1 ? 1 : sl == 2 ? 5 : 8 + (sl - 3);  // representative row
     const double x0 = xval(Xs, i, 0), x1 = xval(Xs, i, 1);
     const double hii = (0.0 + Mf(i, 0) * x0) + Mf(i, 1) * x1;  // orc_hildreth's H(i,i)
-    const double ay = fabs(hii);
-    const bool zero_ok = hzero_row(i) && hii == 0.0;
-    yok = yok && (zero_ok || (ay >= 0x1p-400 && ay <= 0x1p400));
+    yok = yok && hild_rok(hii);
     hl[sl * 64] = make_double2(x0, x1);
-    hl[(HS_X + sl) * 64] = make_double2(hii, zero_ok ? __builtin_amdgcn_rcp(hii) : rcp_refined(hii));
+    hl[(HS_X + sl) * 64] = make_double2(hii, 1.0 / hii);  // the oracle's 1.0 / hii (IEEE)
   }
   return yok;
 }
@@ -1242,12 +1255,13 @@ __device__ __forceinline__ void hild_unstage(const double2 *hl, XS &Xs) {
 
 // One rank-2 sweep (orc_hildreth, finite X and M): v = X*lambda from +0 at the sweep
 // start (fma, ascending j), t_i = fma(M_i1, v1, fma(M_i0, v0, K_i)),
-// w = fma(H_ii, lambda_i, -t_i) / H_ii, lambda_i = max(w, 0), v += X(:,i) * d by fma.
+// w = fma(-t_i, 1/H_ii, lambda_i) (hild_w with every H_ii in its domain and lambda finite),
+// lambda_i = max(w, 0), v += X(:,i) * d by fma.  A row's dependent chain is t (2 fma) ->
+// w -> max -> d -> v: 6 operations (10 with round 5's division).
 // The fast form: straight line, no frozen lanes (the caller keeps a converged lane's
-// lambda aside), division by div_fast's last three steps.  It reports max |d| (the
-// reference's inf-norm test, hildreth.m:39), max / min |numerator| (div_fast's
-// dividend domain) and whether v ended finite (false once any d was not finite: inf
-// and NaN stay in v).
+// lambda aside).  It reports max |d| (the reference's inf-norm test, hildreth.m:39) and
+// whether v ended finite (false once any d was not finite: inf and NaN stay in v; every
+// lambda was finite until then, so each row was hild_w's fma form).
 // The constant rows 0-7 ([Cu; -Cu; I; -I]) use 3 of the 18 slots (X: +-a, +-b, +-c; their
 // (H_ii, 1/H_ii)): those 6 pairs are held in registers (xr3 / hr3, read back from the
 // lane's LDS slots once per solve), so a sweep reads LDS for the 15 Toeplitz rows only.
@@ -1292,8 +1306,7 @@ __device__ __forceinline__ void hild_v(const double2 *hl, const double2 xr3[3], 
 // X(:,i) the row already read (MPCEKF_HILD_NEXTV; 0: hild_v at every sweep start).
 __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, const double2 xr3[3],
                                            const double2 hr3[3], const double K[NCON], double L[NCON],
-                                           double &v0, double &v1, double &dmax, double &xmax, double &xmin,
-                                           bool &vfin) {
+                                           double &v0, double &v1, double &dmax, bool &vfin) {
   ConsM Mf{Cn};
   asm volatile("" ::: "memory");  // reload the LDS slots each sweep (no hoisting)
   if (!MPCEKF_HILD_NEXTV) hild_v(hl, xr3, L, v0, v1);
@@ -1318,18 +1331,13 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     }
     // M(i, k) entries that are structural zeros (constraintsMPC.m's Cu / I blocks and the
     // first row of each Toeplitz block) add +-0 to t: dropped here.  Exact for the fast form:
-    // with v finite a +-0 term changes at most the sign of a zero t, and num = H_ii L_i - t
-    // is then +0 either way (H_ii, L_i >= +0); a non-finite v marks the sweep bad in both forms
+    // with v finite a +-0 term changes at most the sign of a zero t, and -t * (1/H_ii) + L_i
+    // is then L_i, or +0 when L_i = +0 (round to nearest: -0 + +0 = +0), or NaN for 1/H_ii
+    // infinite, either way; a non-finite v marks the sweep bad in both forms
     double t = K[i];
     if (!mzero(i, 0)) t = __builtin_fma(Mf(i, 0), v0, t);
     if (!mzero(i, 1)) t = __builtin_fma(Mf(i, 1), v1, t);
-    const double num = __builtin_fma(hc.x, L[i], -t);
-    const double q0 = num * hc.y;
-    const double e2 = __builtin_fma(-hc.x, q0, num);
-    const double wf = __builtin_fma(e2, hc.y, q0);
-    const double w = hzero_row(i) ? (hc.x == 0.0 ? q0 : wf) : wf;
-    xmax = fmax(xmax, fabs(num));
-    xmin = fmin(xmin, fabs(num));
+    const double w = __builtin_fma(-t, hc.y, L[i]);
     const double nl = w > 0 ? w : 0.0;
     const double d = nl - L[i];
     dmax = fmax(dmax, fabs(d));
@@ -1372,7 +1380,7 @@ __device__ __forceinline__ void sweep_careful(const Cons &Cn, const double2 *hl,
     double t = __builtin_fma(Mf(i, 0), v0, K[i]);
     t = __builtin_fma(Mf(i, 1), v1, t);
     const double li = L[i];
-    const double w = __builtin_fma(hr.x, li, -t) / hr.x;
+    const double w = hild_w(t, hr.x, hr.y, li);
     const double nl = w > 0 ? w : 0.0;
     if (!(fabs(nl - li) < tol)) conv = false;
     const double nli = done ? li : nl;
@@ -1418,10 +1426,10 @@ __device__ __forceinline__ void sweep_dense(const Cons &Cn, const XS &Xs, const 
 // nothing kept).  hl = the lane's LDS slots (HILD_LDS_PER_WAVE per wave).
 //
 // hild_fast (k_hild): the fast rank-2 sweep for lanes with finite X, M, every H_ii in
-// div_fast's divisor domain and a finite warm start.  Lanes keep sweeping after they
+// hild_w's reciprocal domain and a finite warm start.  Lanes keep sweeping after they
 // converge; the lambda they converged with goes to L0 (their warm start is no longer
-// needed) and comes back after the loop.  A lane whose sweep ends with a non-finite v
-// or a dividend outside div_fast's domain, and every lane outside the fast form's
+// needed) and comes back after the loop.  A lane whose sweep ends with a non-finite v,
+// and every lane outside the fast form's
 // domain, returns `slow` with its warm start intact in L0: every sweep before the
 // flag was bit-identical to the exact form, so restarting it with the exact rules
 // gives the exact form's result.
@@ -1455,10 +1463,10 @@ __device__ __forceinline__ bool hild_fast(const Cons &Cn, const double E[NC][NC]
 #pragma unroll 1
   for (int it = 1; it <= maxIter; ++it) {
     if (__all(!active)) break;
-    double dmax = 0.0, xmax = 0.0, xmin = 0x1p1000;
+    double dmax = 0.0;
     bool vfin;
-    sweep_fast(Cn, hl, xr3, hr3, K, L, v0, v1, dmax, xmax, xmin, vfin);
-    const bool bad = !(vfin && xmax <= 0x1p400 && xmin >= 0x1p-400);
+    sweep_fast(Cn, hl, xr3, hr3, K, L, v0, v1, dmax, vfin);
+    const bool bad = !vfin;
     const bool conv = dmax < tol;
     const bool newconv = active && !bad && conv;
     if (active && bad) slow = true;
@@ -3953,7 +3961,7 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
       double w;
       if (fin) {
         const double t = row_t_rt(Nc, M + i * Nc, v, K[i]);
-        w = __builtin_fma(hii, lam[i], -t) / hii;
+        w = hild_w(t, hii, 1.0 / hii, lam[i]);
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = 0; j < nC; ++j) {

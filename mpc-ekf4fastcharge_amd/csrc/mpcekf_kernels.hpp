@@ -67,11 +67,14 @@ struct KRom {
   // theta polynomials in `poly` (global, L2-resident), 0 for the v2 linear tables in LDS;
   // arr = any function has an Arrhenius factor.  Each function's rows and Ea/R are found
   // through its descriptor in the blobs' LDS table header (etab_desc, KDESC doubles each).
-  int npoly, arr;
+  // nodes = some function is on its own theta nodes (ABI v4: its descriptor names a bucket
+  // map; the lookups test this uniform flag before reading it).
+  int npoly, arr, nodes;
   const double *poly;
 };
 constexpr int KPOLY = 6;  // coefficients per theta interval the kernels evaluate (quintic; cubics padded)
-constexpr int KDESC = 3;  // doubles per v3 lookup descriptor (mpcekf_kernels.hip etab_desc)
+constexpr int KDESC = 4;  // doubles per v3 / v4 lookup descriptor (mpcekf_kernels.hip etab_desc)
+constexpr int KMAP = 4;   // doubles per v4 bucket-map entry: k0, x_k0, x_k0+1, 0
 
 struct KCfg {
   double SigmaV, SigmaW, ref, u_max, u_min, du_min, du_max, v_max, phise_min, zmax, hild_tol;

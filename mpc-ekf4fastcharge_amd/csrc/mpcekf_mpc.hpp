@@ -23,6 +23,20 @@ namespace mk {
 // live registers.
 __device__ __forceinline__ void launder(double &x) { asm volatile("" : "+v"(x)); }
 
+// hildreth.m:35's update, w = -(K_i + H(i,:)*lambda - H_ii lambda_i) / H_ii with
+// t_i = K_i + H(i,:)*lambda, spelled as oracle/mpcekf_oracle.c hild_w (round 6):
+// fma(-t_i, 1/H_ii, lambda_i) with the correctly rounded 1/H_ii formed once per solve, when
+// H_ii is 0 or in [2^-1020, 2^1020] (hild_rok) and lambda_i is finite; the division form
+// fma(H_ii, lambda_i, -t_i) / H_ii otherwise.  H_ii = +-0: 1/H_ii = +-inf, and the fma gives
+// x / +-0's inf / NaN by IEEE, as the division does.
+__device__ __forceinline__ bool hild_rok(double h) {
+  const double a = fabs(h);
+  return h == 0.0 || (a >= 0x1p-1020 && a <= 0x1p1020);
+}
+__device__ __forceinline__ double hild_w(double t, double h, double rinv, double l) {
+  return (hild_rok(h) && isfinite(l)) ? __builtin_fma(-t, rinv, l) : __builtin_fma(h, l, -t) / h;
+}
+
 // predMat.m with A = diag(a), B = ones, evaluated on the structure of Abar:
 // identical nonzero arithmetic to the dense products of orc_predmat.
 template <int NP>

@@ -576,14 +576,6 @@ __device__ __forceinline__ double bcast8(double v, int j) {  // j a constant aft
   }
 }
 
-__device__ __forceinline__ double rcp_refined_w(double y) {
-  double r = __builtin_amdgcn_rcp(y);
-  double e = __builtin_fma(-y, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-y, r, 1.0);
-  return __builtin_fma(r, e, r);
-}
-
 // The row term b_k of hild_row_t for lane k (columns k and k + 8): a_0 = fma(M_i0, v_0, K_i),
 // a_k = M_ik v_k, as fma(M_ik, v_k, kz) with kz = K_i in lane 0 and +0 elsewhere (fma(m, v, +0)
 // differs from m*v only in the sign of a zero product, which cannot reach t); then
@@ -610,8 +602,8 @@ __device__ __forceinline__ double row_term8(int i, int k, double v0, double v1, 
 }
 // The I / -I rows (one M entry, +-1 in column j): the tree of hild_row_t adds K_i and +-v_j
 // to zeros only, which is exact, so t = K_i +- v_j in one rounding (the sign of a zero t
-// aside, which cannot reach lambda: num = fma(H_ii, lambda_i, -t) then has the same
-// magnitude and nl = max(w, +0)).  v_j comes from lane j % 8 of the group (v0 for j < 8,
+// aside, which cannot reach lambda: hild_w's fma(-t, 1/H_ii, lambda_i) is then lambda_i, +0
+// when lambda_i = +0, or NaN when 1/H_ii is infinite, for either sign).  v_j comes from lane j % 8 of the group (v0 for j < 8,
 // v1 above) by bcast8; K_i is read in every lane.
 template <int NC>
 __device__ __forceinline__ constexpr bool unit_row(int i) {
@@ -687,7 +679,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
   const int64_t n = s.n, slot = (int64_t)blockIdx.x * T::GROUPS + g;
   static_assert(T::ZERO_LDS % 2 == 0 && T::CELL_LDS % 2 == 0, "16-byte aligned (H_ii, 1/H_ii) pairs");
   double *base = lds + T::ZERO_LDS + g * T::CELL_LDS;
-  double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii refined)
+  double2 *hr = reinterpret_cast<double2 *>(base);  // (H_ii, 1/H_ii)
   double *lam = base + 2 * NCON, *Kl = lam + NCON, *hp = Kl + NCON;
   static_assert(4 * NCON + 3 * HPW <= T::CELL_LDS &&
                     2 * (T::ZERO_LDS + T::GROUPS * T::CELL_LDS + T::WAVES * T::JUNK) * 8 <= 160 * 1024,
@@ -741,10 +733,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       xb[k * NC + m] = x[m];
     }
     const int i = u < NC ? u : u < 2 * NC ? u + NC : u + 2 * NC;  // constraint row (+ NC: its negated copy)
-    const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && h == 0.0;  // (H(0), 0, ..) rows
-    const double ay = fabs(h);
-    ok = ok && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
-    const double2 hh = make_double2(h, zrow ? __builtin_amdgcn_rcp(h) : rcp_refined_w(h));
+    ok = ok && hild_rok(h);                          // hild_w's fma form for every row
+    const double2 hh = make_double2(h, 1.0 / h);     // the oracle's 1.0 / hii (IEEE)
     hr[i] = hh;
     if (u < 2 * NC) hr[i + NC] = hh;
     __syncthreads();
@@ -767,12 +757,10 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     for (int i = k; i < NCON; i += LN) {
       const double li = s.lam[(size_t)i * n + c];
       const double hii = w.hii[(size_t)c * NCON + i];
-      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0 && hii == 0.0;  // (H(0), 0, ..) rows
-      const double ay = fabs(hii);
-      ok = ok && isfinite(li) && (zrow || (ay >= 0x1p-400 && ay <= 0x1p400));
+      ok = ok && isfinite(li) && hild_rok(hii);
       lam[i] = li;
       Kl[i] = w.K[(size_t)c * NCON + i];
-      hr[i] = make_double2(hii, zrow ? __builtin_amdgcn_rcp(hii) : rcp_refined_w(hii));
+      hr[i] = make_double2(hii, 1.0 / hii);
     }
     for (int j = k; j < 3 * HPW; j += LN) {
       const int b = j / HPW, q = j % HPW;
@@ -850,12 +838,8 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
     asm volatile("" ::: "memory");
     double u0 = 0.0, u1 = 0.0;  // the next sweep's v
     // hildreth.m:39's stop test as a wave mask (|d| < tol on every row; a NaN d is "not
-    // converged", as in orc_hildreth; the 8 lanes of a group compute the same d), and the
-    // fast division's domain as the range of the dividends' high words (sign cleared):
-    // |num| in [2^-400, 2^400) exactly when hi(2^-400) <= hi(|num|) < hi(2^400).  Integer,
-    // so no canonicalising max/min.
+    // converged", as in orc_hildreth; the 8 lanes of a group compute the same d)
     uint64_t convm = ~0ull;
-    unsigned xhi = 0u, xlo = 0x7fffffffu;
     // A row's LDS operands are read PF rows ahead: the compiler pulls a row's first
     // operations up into the row before, and a one-row distance then left the reads ~20
     // instructions to land (PF = 2: 3.70 -> 3.59 ms per step at configs[4]).
@@ -881,18 +865,10 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       const double t = rowT(i, v0, v1, o.kz, o.m0, o.m1);
       const double li = o.li;
       const double2 h = o.h;
-      // w = (H_ii lambda_i - t) / H_ii: x * (1/y) refined by one residual step, correctly
-      // rounded for |x|, |y| in [2^-400, 2^400] (tools/micro/div_check.hip); a zero
-      // H(0) row keeps x / +-0 = x * (1 / +-0) by IEEE.
-      const double num = __builtin_fma(h.x, li, -t);
-      const double q0 = num * h.y;
-      const double e2 = __builtin_fma(-h.x, q0, num);
-      const double wf = __builtin_fma(e2, h.y, q0);
-      const bool zrow = i >= 4 * NC && (i - 4 * NC) % NP == 0;
-      const double wv = zrow ? (h.x == 0.0 ? q0 : wf) : wf;
-      const unsigned hb = (unsigned)__double2hiint(num) & 0x7fffffffu;
-      xhi = hb > xhi ? hb : xhi;
-      xlo = hb < xlo ? hb : xlo;
+      // w = lambda_i - t / H_ii as hild_w's fma(-t, 1/H_ii, lambda_i): every H_ii is in its
+      // domain (checked at the staging) and lambda_i finite while v is (a zero H(0) row's
+      // 1/H_ii = +-inf gives x / +-0 by IEEE)
+      const double wv = __builtin_fma(-t, h.y, li);
       const double nl = wv > 0 ? wv : 0.0;
       const double d = nl - li;
       convm &= __ballot(fabs(d) < tol);
@@ -904,14 +880,14 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       u0 = __builtin_fma(x0, nl, u0);
       u1 = __builtin_fma(x1, nl, u1);
       // every accumulation finishes in its row: left alone, the compiler sank the ones not
-      // needed before the sweep end (u, the stop flag, the domain range) and held every
-      // row's dividend, lambda and step live across the sweep
-      asm volatile("" : "+v"(xhi), "+v"(xlo), "+v"(u0), "+v"(u1), "+v"(v1), "+s"(convm));
+      // needed before the sweep end (u, the stop flag) and held every row's lambda and step
+      // live across the sweep
+      asm volatile("" : "+v"(u0), "+v"(u1), "+v"(v1), "+s"(convm));
     }
-    // a non-finite v (a zero-diagonal row going to or from +inf) or a dividend outside
-    // the fast division's domain: the exact path redoes this cell from its warm start,
-    // still in s.lam (every sweep before was bit-identical to the exact form)
-    const bool bad = !(isfinite(v0) && isfinite(v1) && xhi < 0x58f00000u && xlo >= 0x26f00000u);  // hi(2^+-400)
+    // a non-finite v (a zero-diagonal row going to or from +inf): the exact path redoes
+    // this cell from its warm start, still in s.lam (every sweep before was bit-identical
+    // to the exact form)
+    const bool bad = !(isfinite(v0) && isfinite(v1));
     if ((__ballot(bad) >> gshift) & 0xFFull) {
       slow = true;
       break;
@@ -1066,7 +1042,7 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
       const double li = lam[(size_t)i * n + c];
       double wv;
       if (fin) {
-        wv = __builtin_fma(hii, li, -row_t_rt<NP, NC>(Hall, i, v, Ki)) / hii;
+        wv = hild_w(row_t_rt<NP, NC>(Hall, i, v, Ki), hii, 1.0 / hii, li);
       } else {  // dense H(i,:)*lambda, 4 interleaved partial sums (orc_hildreth)
         double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1

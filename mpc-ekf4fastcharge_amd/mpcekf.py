@@ -89,9 +89,19 @@ class _PackedRom:
             for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
                 setattr(s, k, dptr(arr(getattr(e, k))))
             for k in EL_TABLES + ("Uocp1",):    # ABI v3 theta polynomials (NULL: v2 linear tables)
-                setattr(s, k + "_p", dptr(arr(e.poly[k])) if e.poly else _lib._dp())
+                has = bool(e.poly) and k in e.poly
+                setattr(s, k + "_p", dptr(arr(e.poly[k])) if has else _lib._dp())
             for i, k in enumerate(EL_TABLES):  # ABI v3 Arrhenius energies (0: none)
                 s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
+            for i, k in enumerate(EL_TABLES + ("Uocp1",)):  # ABI v4: functions on their own nodes
+                if e.nodes and k in e.nodes:
+                    x, c = e.nodes[k]
+                    c = np.asarray(c, dtype=np.float64)
+                    if c.shape[-1] < rom.npoly:   # one coefficient count (tab_npoly): zero-padded
+                        c = np.concatenate([c, np.zeros(c.shape[:-1] + (rom.npoly - c.shape[-1],))], -1)
+                    s.nnode[i] = int(np.asarray(x).size)
+                    s.node[i] = dptr(arr(x))
+                    s.node_p[i] = dptr(arr(c))
         r.tab_npoly = rom.npoly
         self.s = r
 
@@ -213,6 +223,21 @@ class Context:
         n, nm, nz, nc = C.c_int64(), C.c_int32(), C.c_int32(), C.c_int32()
         check(self.L.mpcekf_ctx_info(h, C.byref(n), C.byref(nm), C.byref(nz), C.byref(nc)))
         self.n, self.NM, self.nz, self.ncon = n.value, nm.value, nz.value, nc.value
+        # asynchronous = True: the stage functions below call the _async C-ABI twins (SURVEY.md
+        # §8(b)): they return before their host outputs are written; sync() (or any synchronous
+        # stage call) completes them.  The output arrays are held here until then.
+        self.asynchronous = False
+        self._pending = []
+
+    def _stage(self, name, *args, keep=()):
+        """One stage entry point: mpcekf_<name>, or mpcekf_<name>_async in asynchronous mode
+        (its output arrays `keep` held until the synchronisation)."""
+        if self.asynchronous:
+            check(getattr(self.L, f"mpcekf_{name}_async")(self.h, *args))
+            self._pending.append(keep)
+        else:
+            check(getattr(self.L, f"mpcekf_{name}")(self.h, *args))
+            self._pending.clear()
 
     # -- lifetime ---------------------------------------------------------
     def close(self):
@@ -282,8 +307,10 @@ class Context:
         check(self.L.mpcekf_step(self.h, int(nsteps), None, *p, 1))
 
     def sync(self):
-        """Wait for every launch on the context's device (mpcekf_sync)."""
+        """Wait for every launch on the context's device and complete the asynchronous stage
+        calls' host outputs (mpcekf_sync)."""
         check(self.L.mpcekf_sync(self.h))
+        self._pending.clear()
 
     def set_graph(self, enable=True):
         """Replay repeated fused-call shapes from captured hipGraphs (mpcekf_set_graph)."""
@@ -334,7 +361,7 @@ class Context:
         i = self._vec(Iapp)
         t = self._tvec(Tc)
         v = np.empty(self.n)
-        check(self.L.mpcekf_plant_step(self.h, dptr(i), dptr(t), dptr(v)))
+        self._stage("plant_step", dptr(i), dptr(t), dptr(v), keep=(v,))
         return v
 
     def iterEKF(self, vk, ik, Tk=None, bounds=True, xind=True):
@@ -349,7 +376,7 @@ class Context:
         zb = np.empty((self.n, self.nz + 2)) if bounds else None
         xm = np.empty((self.n, 4), dtype=np.int32) if xind else None
         xg = np.empty((self.n, 4)) if xind else None
-        check(self.L.mpcekf_ekf_step(self.h, dptr(v), dptr(i), dptr(t), dptr(zk), dptr(zb), iptr(xm), dptr(xg)))
+        self._stage("ekf_step", dptr(v), dptr(i), dptr(t), dptr(zk), dptr(zb), iptr(xm), dptr(xg), keep=(zk, zb, xm, xg))
         if not xind:
             return zk, zb, None
         return zk, zb, dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
@@ -364,12 +391,12 @@ class Context:
         t = self._tvec(Tk)
         lin = None if keep else np.empty((self.n, LIN_SIZE))
         if zk is None:
-            check(self.L.mpcekf_linearize(self.h, None, None, None, dptr(t), dptr(lin)))
+            self._stage("linearize", None, None, None, dptr(t), dptr(lin), keep=(lin,))
             return lin
         zk = np.ascontiguousarray(zk, dtype=np.float64)
         xm = np.ascontiguousarray(Xind["model"], dtype=np.int32)
         xg = np.ascontiguousarray(Xind["gamma"], dtype=np.float64)
-        check(self.L.mpcekf_linearize(self.h, dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin)))
+        self._stage("linearize", dptr(zk), iptr(xm), dptr(xg), dptr(t), dptr(lin), keep=(lin,))
         return lin
 
     def lin_fields(self, slots, set=None, out=None):
@@ -381,8 +408,13 @@ class Context:
             out = np.empty((self.n, sl.size))
         elif out.shape != (self.n, sl.size) or out.dtype != np.float64 or not out.flags.c_contiguous:
             raise ValueError(f"lin_fields: out must be a C-contiguous float64 array of shape {(self.n, sl.size)}")
-        st = None if set is None else np.ascontiguousarray(set, dtype=np.float64)
-        check(self.L.mpcekf_lin_fields(self.h, iptr(sl), int(sl.size), dptr(st), dptr(out)))
+        st = None
+        if set is not None:
+            st = np.ascontiguousarray(set, dtype=np.float64)
+            if st.size != self.n * sl.size:   # the C side reads n * len(slots) doubles from it
+                raise ValueError(f"lin_fields: set must hold {(self.n, sl.size)} values, got shape {st.shape}")
+            st = st.reshape(self.n, sl.size)
+        self._stage("lin_fields", iptr(sl), int(sl.size), dptr(st), dptr(out), keep=(out,))
         return out
 
     def iterMPC(self, lin, SOCk_1, cost=False):
@@ -394,12 +426,12 @@ class Context:
         uk = np.empty(self.n)
         ne = np.empty(self.n, dtype=np.int32)
         if not cost:
-            check(self.L.mpcekf_mpc_step(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne)))
+            self._stage("mpc_step", dptr(lin), dptr(s), dptr(uk), iptr(ne), keep=(uk, ne))
             return uk, ne
         ju, jf, nd = np.empty(self.n), np.empty(self.n), np.empty(self.n)
         nv = np.empty(self.n, dtype=np.int32)
-        check(self.L.mpcekf_mpc_step_ex(self.h, dptr(lin), dptr(s), dptr(uk), iptr(ne), dptr(ju), dptr(jf),
-                                        dptr(nd), iptr(nv)))
+        self._stage("mpc_step_ex", dptr(lin), dptr(s), dptr(uk), iptr(ne), dptr(ju), dptr(jf), dptr(nd), iptr(nv),
+                    keep=(uk, ne, ju, jf, nd, nv))
         return uk, ne, dict(J_uncon=ju, J_final=jf, norm_DU=nd, viol=nv, nexec=ne)
 
     def mpc_diag(self, lin, uk_1=None):
@@ -409,7 +441,9 @@ class Context:
         u = None if uk_1 is None else self._vec(uk_1)
         p = np.empty((self.n, 7, 2))
         sv = np.empty((self.n, 7))
-        check(self.L.mpcekf_mpc_diag(self.h, dptr(lin), dptr(u), dptr(p), dptr(sv)))
+        self._stage("mpc_diag", dptr(lin), dptr(u), dptr(p), dptr(sv), keep=(p, sv))
+        if self.asynchronous:   # (poles re / im [n, 7, 2], sv): the complex view only after sync
+            return p, sv
         return p[..., 0] + 1j * p[..., 1], sv
 
     # -- state -----------------------------------------------------------
@@ -433,7 +467,7 @@ class Context:
         sc = np.empty((self.n, len(slots)))
         warn = np.empty(self.n, np.int32) if flags else None
         status = np.empty(self.n, np.int32) if flags else None
-        check(self.L.mpcekf_get_scalars(self.h, iptr(slots), len(slots), dptr(sc), iptr(warn), iptr(status)))
+        self._stage("get_scalars", iptr(slots), len(slots), dptr(sc), iptr(warn), iptr(status), keep=(sc, warn, status))
         out = {k: sc[:, j] for j, k in enumerate(names)}
         if flags:
             out.update(warn=warn, status=status)

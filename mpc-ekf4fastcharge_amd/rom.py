@@ -87,6 +87,10 @@ class Electrode:
     Cdleff: np.ndarray         # [ntemp, ntheta] Cdl^(2-nDL) wDL^(nDL-1) (OB_step.m:212-219)
     poly: dict = None          # ABI v3: {"Uocp": [ntemp, ntheta-1, npoly], ..., "Uocp1": [ntheta-1, npoly]}
     Ea: dict = None            # ABI v3: {"k0": J/mol, ...}; missing / 0: no Arrhenius factor
+    # ABI v4: functions on their own theta nodes, {"Uocp": (x [m], coef [ntemp, m-1, npoly]), ...,
+    # "Uocp1": (x, coef [m-1, npoly])}; a function named here is looked up by interp_nodes
+    # instead of its uniform-grid poly (which may then be absent)
+    nodes: dict = None
 
 
 def interp_tab(tab: np.ndarray, x: float) -> float:
@@ -128,6 +132,32 @@ def interp_poly(coef: np.ndarray, x: float) -> float:
     v = float(c[-1])                     # Horner: c0 + s (c1 + s (... + s c_last))
     for k in range(len(c) - 2, -1, -1):
         v = float(c[k] + s * v)
+    return v
+
+
+def node_segment(x: np.ndarray, th: float):
+    """ABI v4 segment of theta on a function's own nodes x [m] (strictly ascending): theta
+    clamped to [0, 1], k = #{j in 1..m-2 : x_j <= theta} (the segment holding it, segments 0
+    and m-2 extended past the end nodes), s = theta - x_k.  The C oracle (node_seg) states
+    the same; the kernels find k through a uniform bucket map (host build_rom) that gives
+    this k exactly."""
+    xc = min(max(th, 0.0), 1.0)
+    k = int(np.searchsorted(x[1:-1], xc, side="right"))
+    return k, xc - float(x[k])
+
+
+def interp_nodes(x: np.ndarray, coef: np.ndarray, th: float) -> float:
+    """ABI v4 row: segment k's polynomial in s = theta - x_k (coef [m-1, npoly]), Horner
+    c0 + s (c1 + s (... + s c_last)) (no contraction; the C oracle and kernels: fma).  An
+    interp1-linear handle's segment is (y_k, slope_k, 0, 0): y_k + s slope_k, np.interp's
+    value to the last bit up to its separate rounding of the product."""
+    if th != th:
+        return float("nan")
+    k, s = node_segment(x, th)
+    c = coef[k]
+    v = float(c[-1])
+    for j in range(len(c) - 2, -1, -1):
+        v = float(c[j] + s * v)
     return v
 
 
@@ -176,12 +206,19 @@ def temp_index(T_K: np.ndarray, T: float):
     return j, float((Tc - T_K[j]) / (T_K[j + 1] - T_K[j]))
 
 
-def eval_tab2(tab2: np.ndarray, theta: float, jg, coef=None) -> float:
+def eval_tab2(tab2: np.ndarray, theta: float, jg, coef=None, nodes=None) -> float:
     """Defined bilinear lookup of a [ntemp, ntheta] table: the theta interpolation of rows
     j and j+1, then a + g (b - a).  coef [ntemp, ntheta-1, 4] (ABI v3): the rows are the
-    piecewise polynomials instead of the linear interpolation of tab2."""
+    piecewise polynomials instead of the linear interpolation of tab2; nodes (x, coef
+    [ntemp, m-1, npoly]) (ABI v4): the rows are polynomials on the function's own nodes."""
     j, g = jg
-    row = (lambda k: interp_tab(tab2[k], theta)) if coef is None else (lambda k: interp_poly(coef[k], theta))
+    if nodes is not None:
+        x, cn = nodes
+        row = lambda k: interp_nodes(x, cn[k], theta)
+    elif coef is None:
+        row = lambda k: interp_tab(tab2[k], theta)
+    else:
+        row = lambda k: interp_poly(coef[k], theta)
     a = row(j)
     if tab2.shape[0] == 1:
         return a
@@ -193,7 +230,8 @@ def eval_fn(e: Electrode, name: str, theta: float, jg, T: float, R: float, Tref:
     """The v3 lookup of one cellData.function handle (include/mpcekf.h): the rows of
     ``name`` at theta (polynomial when ``e.poly`` has them, else linear), linear in T between
     the bracketing rows, times the Arrhenius factor when ``e.Ea[name]`` is non-zero."""
-    v = eval_tab2(getattr(e, name), theta, jg, None if not e.poly else e.poly.get(name))
+    v = eval_tab2(getattr(e, name), theta, jg, None if not e.poly else e.poly.get(name),
+                  None if not e.nodes else e.nodes.get(name))
     ea = 0.0 if not e.Ea else float(e.Ea.get(name, 0.0))
     if ea != 0.0:
         v = v * arrhenius(ea / R, Tref, T)
@@ -226,6 +264,8 @@ class CellFunctions:
 
     def Uocp(self, theta, T=None):            # 1-arg call: its own table (EKFmatsHandler.m:96)
         if T is None:
+            if self.e.nodes and "Uocp1" in self.e.nodes:
+                return interp_nodes(*self.e.nodes["Uocp1"], theta)
             if self.e.poly:
                 return interp_poly(self.e.poly["Uocp1"], theta)
             return interp_tab(self.e.Uocp1, theta)
@@ -298,8 +338,15 @@ class ROM:
     @property
     def npoly(self):
         """ABI v3: coefficients per theta interval of the electrode tables (4 cubic, 6
-        quintic), 0 for v2 linear tables."""
-        return int(np.asarray(self.neg.poly["Uocp1"]).shape[-1]) if self.neg.poly else 0
+        quintic), 0 for v2 linear tables.  With ABI v4 nodes the largest of the uniform-grid
+        and node polynomials (the library pads each to 6)."""
+        n = 0
+        for e in (self.neg, self.pos):
+            for c in (e.poly or {}).values():
+                n = max(n, int(np.asarray(c).shape[-1]))
+            for _, c in (e.nodes or {}).values():
+                n = max(n, int(np.asarray(c).shape[-1]))
+        return n
 
     @property
     def ntheta(self):
@@ -392,10 +439,26 @@ class ROM:
                     raise ValueError(f"electrode table {k}: shape {t.shape}, expected ({tk.size}, ntheta >= 2)")
             if e.Uocp1.shape != (self.ntheta,) or e.soc0.shape != (tk.size,) or e.soc100.shape != (tk.size,):
                 raise ValueError("electrode tables Uocp1 / soc0 / soc100 have the wrong length")
+            nd = e.nodes or {}
+            for k, (x, c) in nd.items():
+                if k not in EL_TABLES + ("Uocp1",):
+                    raise ValueError(f"nodes: {k!r} is not one of {EL_TABLES + ('Uocp1',)}")
+                x = np.asarray(x, dtype=float)
+                if x.ndim != 1 or x.size < 2 or np.any(np.diff(x) <= 0) or not np.all(np.isfinite(x)):
+                    raise ValueError(f"nodes {k}: need >= 2 strictly ascending finite theta nodes")
+                if x.size > 2 and (x[1] <= 0.0 or x[-2] >= 1.0):
+                    raise ValueError(f"nodes {k}: interior nodes must lie in (0, 1)")
+                want = (x.size - 1,) if k == "Uocp1" else (tk.size, x.size - 1)
+                if np.asarray(c).shape[:-1] != want or np.asarray(c).shape[-1] not in (4, 6):
+                    raise ValueError(f"nodes {k}: coefficients {np.asarray(c).shape}, expected {want} x 4 or 6")
+            if nd and not e.poly and set(nd) != set(EL_TABLES) | {"Uocp1"}:
+                raise ValueError("nodes: functions without nodes need the uniform-grid poly tables")
             if e.poly:
-                if set(e.poly) != set(EL_TABLES) | {"Uocp1"}:
-                    raise ValueError(f"poly tables: need all of {EL_TABLES + ('Uocp1',)}, got {sorted(e.poly)}")
-                npoly = np.asarray(e.poly["Uocp1"]).shape[-1]
+                missing = (set(EL_TABLES) | {"Uocp1"}) - set(e.poly) - set(nd)
+                if missing:
+                    raise ValueError(f"poly tables: need all of {EL_TABLES + ('Uocp1',)} (or their nodes), "
+                                     f"missing {sorted(missing)}")
+                npoly = np.asarray(next(iter(e.poly.values()))).shape[-1]
                 if npoly not in (4, 6):
                     raise ValueError(f"poly tables: {npoly} coefficients per interval (4: cubic, 6: quintic)")
                 for k, c in e.poly.items():
@@ -405,7 +468,7 @@ class ROM:
             for k in (e.Ea or {}):
                 if k not in EL_TABLES:
                     raise ValueError(f"Ea: {k!r} is not one of {EL_TABLES}")
-        if bool(self.neg.poly) != bool(self.pos.poly):
+        if bool(self.neg.poly or self.neg.nodes) != bool(self.pos.poly or self.pos.nodes):
             raise ValueError("poly tables must be given for both electrodes or neither")
         if not np.all(self.A[..., -1] == 1):
             raise ValueError("A does not have integrator state (initKF.m:74)")
@@ -468,6 +531,9 @@ class ROM:
                 d[f"{side}_poly_{k}"] = np.asarray(v, dtype=float)
             for k, v in (e.Ea or {}).items():
                 d[f"{side}_Ea_{k}"] = float(v)
+            for k, (x, c) in (e.nodes or {}).items():   # ABI v4 (absent before: hashes unchanged)
+                d[f"{side}_nodex_{k}"] = np.asarray(x, dtype=float)
+                d[f"{side}_nodep_{k}"] = np.asarray(c, dtype=float)
         return d
 
     def save_npz(self, path):
@@ -484,7 +550,10 @@ class ROM:
             cub = {k[len(side) + 6:]: np.array(z[k], dtype=float) for k in z.files
                    if k.startswith(f"{side}_poly_")}
             ea = {k[len(side) + 4:]: float(z[k]) for k in z.files if k.startswith(f"{side}_Ea_")}
-            return Electrode(**kw, poly=cub or None, Ea=ea or None)
+            nd = {k[len(side) + 7:]: (np.array(z[k], dtype=float), np.array(z[f"{side}_nodep_" + k[len(side) + 7:]],
+                                                                           dtype=float))
+                  for k in z.files if k.startswith(f"{side}_nodex_")}
+            return Electrode(**kw, poly=cub or None, Ea=ea or None, nodes=nd or None)
 
         return ROM(T_degC=np.array(z["T_degC"], float), SOC_pct=np.array(z["SOC_pct"], float),
                    Ts=float(z["Ts"]), A=np.array(z["A"], float), C=np.array(z["C"], float),
@@ -497,6 +566,7 @@ class ROM:
     # ---- JSON exchange format (matlab/mpcekf_export_rom.m) ------------------
     JSON_FORMAT = "mpcekf-rom-v2"
     JSON_FORMAT_V3 = "mpcekf-rom-v3"   # + per-table theta polynomials and Arrhenius energies
+    JSON_FORMAT_V4 = "mpcekf-rom-v4"   # + per-function theta nodes (lookup-table handles)
 
     def to_json_dict(self):
         """The dict ``matlab/mpcekf_export_rom.m`` writes: every array as
@@ -513,9 +583,16 @@ class ROM:
                 d["poly"] = {k: arr(v) for k, v in e.poly.items()}
             if e.Ea:
                 d["Ea"] = {k: float(v) for k, v in e.Ea.items()}
+            if e.nodes:   # v4: {"nodes": {"Uocp": {"x": [1, m], "p": [ntemp, m-1, npoly]}, ...}}
+                d["nodes"] = {k: {"x": arr(x), "p": arr(c)} for k, (x, c) in e.nodes.items()}
             return d
 
-        return {"format": self.JSON_FORMAT_V3 if self.npoly or self.neg.Ea or self.pos.Ea else self.JSON_FORMAT, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
+        fmt = self.JSON_FORMAT
+        if self.npoly or self.neg.Ea or self.pos.Ea:
+            fmt = self.JSON_FORMAT_V3
+        if self.neg.nodes or self.pos.nodes:
+            fmt = self.JSON_FORMAT_V4
+        return {"format": fmt, "T_degC": arr(self.T_degC), "SOC_pct": arr(self.SOC_pct),
                 "Ts": float(self.Ts), "A": arr(self.A), "C": arr(self.C), "D": arr(self.D),
                 "names": list(self.names), "xloc": arr(self.xloc), "F": float(self.F), "R": float(self.R),
                 "Q": float(self.Q), "Rc": float(self.Rc), "Tref": float(self.Tref),
@@ -531,9 +608,9 @@ class ROM:
         """Inverse of :meth:`to_json_dict`; accepts what MATLAB's ``jsonencode`` makes of
         the exporter's struct (1-element arrays as bare numbers, NaN as null, a lone
         name as a string).  Raises ValueError on a wrong format tag or shape."""
-        if d.get("format") not in (ROM.JSON_FORMAT, ROM.JSON_FORMAT_V3):
-            raise ValueError(f"ROM json: format {d.get('format')!r}, expected {ROM.JSON_FORMAT!r} "
-                             f"or {ROM.JSON_FORMAT_V3!r}")
+        if d.get("format") not in (ROM.JSON_FORMAT, ROM.JSON_FORMAT_V3, ROM.JSON_FORMAT_V4):
+            raise ValueError(f"ROM json: format {d.get('format')!r}, expected {ROM.JSON_FORMAT!r}, "
+                             f"{ROM.JSON_FORMAT_V3!r} or {ROM.JSON_FORMAT_V4!r}")
 
         def arr(a, ndim):
             if a.get("order", "F") != "F":
@@ -565,8 +642,8 @@ class ROM:
             nth = kw["Uocp1"].size
             cub = {}
             pj = e.get("poly") or {}
-            # coefficients per interval (4 cubic, 6 quintic) from Uocp1's (ntheta-1) x npoly shape
-            npoly = int(np.atleast_1d(pj["Uocp1"]["shape"])[-1]) if "Uocp1" in pj else 0
+            # coefficients per interval (4 cubic, 6 quintic) from any table's trailing dimension
+            npoly = int(np.atleast_1d(next(iter(pj.values()))["shape"])[-1]) if pj else 0
             for k, a in pj.items():
                 if k not in EL_TABLES + ("Uocp1",):
                     raise ValueError(f"ROM json: unknown poly table {k!r}")
@@ -581,7 +658,22 @@ class ROM:
                     raise ValueError(f"ROM json: poly {k}: {x.size} values, expected {want}")
                 cub[k] = x.reshape(want, order="F") if x.shape != want else x
             ea = {k: float(v) for k, v in (e.get("Ea") or {}).items()}
-            return Electrode(**kw, poly=cub or None, Ea=ea or None)
+            nd = {}
+            for k, a in (e.get("nodes") or {}).items():
+                if k not in EL_TABLES + ("Uocp1",):
+                    raise ValueError(f"ROM json: unknown nodes table {k!r}")
+                x = arr(a["x"], 1)
+                pv = np.array([np.nan if v is None else v for v in np.atleast_1d(a["p"]["data"])], dtype=float)
+                shape = [int(v) for v in np.atleast_1d(a["p"]["shape"])]
+                if int(np.prod(shape)) != pv.size:
+                    raise ValueError(f"ROM json: nodes {k}: shape {shape} does not hold {pv.size} values")
+                npn = shape[-1]
+                want = (x.size - 1, npn) if k == "Uocp1" else (ntemp, x.size - 1, npn)
+                if pv.size != int(np.prod(want)):
+                    raise ValueError(f"ROM json: nodes {k}: {pv.size} values, expected {want}")
+                pv = pv.reshape(shape, order="F")
+                nd[k] = (x, pv.reshape(want, order="F") if pv.shape != want else pv)
+            return Electrode(**kw, poly=cub or None, Ea=ea or None, nodes=nd or None)
 
         names = d["names"]
         names = [names] if isinstance(names, str) else [str(s) for s in names]
@@ -904,7 +996,90 @@ def detect_arrhenius(f, T_K, Tref, R, th=None, tol=1e-10):
     return ea
 
 
-def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5):
+NODE_FNS = EL_TABLES + ("Uocp1",)
+
+
+def discover_nodes(ws, lo=-1e-12, hi=1.0 + 1e-12):
+    """The theta breakpoints a lookup-table handle carries (matlab/mpcekf_handle_nodes.m: MATLAB's
+    functions(h).workspace{1}, recursing into captured handles): the union of every captured
+    strictly ascending finite numeric vector of >= 3 values inside [0, 1].  None for a
+    closed-form handle.  A captured vector that is not a breakpoint set only refines the
+    segments, which keeps a piecewise polynomial exact."""
+    found = []
+
+    def walk(v, depth=0):
+        if depth > 8:
+            return
+        if isinstance(v, dict):
+            for x in v.values():
+                walk(x, depth + 1)
+        elif callable(v) and hasattr(v, "workspace"):
+            walk(v.workspace(), depth + 1)
+        elif isinstance(v, (list, tuple, np.ndarray)):
+            a = np.asarray(v)
+            if a.dtype.kind in "fiu" and a.ndim >= 1 and a.squeeze().ndim == 1:
+                a = a.astype(float).ravel()
+                if (a.size >= 3 and np.all(np.isfinite(a)) and np.all(np.diff(a) > 0)
+                        and a[0] >= lo and a[-1] <= hi):
+                    found.append(a)
+    walk(ws)
+    if not found:
+        return None
+    return np.unique(np.clip(np.concatenate(found), 0.0, 1.0))
+
+
+_T4 = np.array([0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0])
+_V4INV = np.linalg.inv(np.vander(_T4, 4, increasing=True))
+
+
+def fit_segments(f, x):
+    """ABI v4 coefficients [m-1, 4] of a piecewise cubic with breakpoints x from handle calls
+    alone: per segment the cubic through f at x_k + h (0, 1/3, 2/3, 1), in s = theta - x_k.
+    Exact (to rounding) for any handle that is a polynomial of degree <= 3 on every segment
+    -- interp1 'linear', pchip, spline, makima.  A segment whose quadratic and cubic terms are
+    rounding noise is stored as interp1's (y_k, (y_k+1 - y_k) / h, 0, 0)."""
+    x = np.asarray(x, dtype=float)
+    c = np.zeros((x.size - 1, 4))
+    for k in range(x.size - 1):
+        a, b = float(x[k]), float(x[k + 1])
+        h = b - a
+        ys = np.array([f(a), f(a + h / 3.0), f(a + 2.0 * h / 3.0), f(b)])
+        q = _V4INV @ ys
+        scale = max(float(np.max(np.abs(ys))), 1e-300)
+        if abs(q[2]) <= 64 * EPS * scale and abs(q[3]) <= 64 * EPS * scale:
+            c[k] = (ys[0], (ys[3] - ys[0]) / h, 0.0, 0.0)
+        else:
+            c[k] = (q[0], q[1] / h, q[2] / (h * h), q[3] / (h * h * h))
+    return c
+
+
+def tabulate_nodes(fh, T_K, Tref=298.15, R=8.3144621, ea=None):
+    """The ABI v4 node tables {name: (x, coef)} of every function of handle object fh whose
+    workspace carries breakpoints (discover_nodes); ea {name: J/mol} as detect_arrhenius
+    found them (the rows of such a function are taken at Tref)."""
+    if not hasattr(fh, "workspace"):
+        return {}
+    T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
+    ea = ea or {}
+    fns = {"Uocp": fh.Uocp, "dUocp": fh.dUocp, "k0": fh.k0, "Rf": fh.Rf, "Cdleff": fh.Cdleff}
+    out = {}
+    for name in NODE_FNS:
+        x = discover_nodes(fh.workspace(name))
+        if x is None or x.size < 2:
+            continue
+        if name == "Uocp1":
+            out[name] = (x, fit_segments(lambda t: fh.Uocp(t), x))
+            continue
+        f = fns[name]
+        rows = []
+        for T in T_K:
+            Tr = Tref if ea.get(name, 0.0) != 0.0 else T
+            rows.append(fit_segments(lambda t, Tr=Tr: f(t, Tr), x))
+        out[name] = (x, np.array(rows))
+    return out
+
+
+def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5, nodes=False):
     """An ABI v3 Electrode from a handle object with the cellData.function interface
     (Uocp(th, T), Uocp(th), dUocp, k0, Rf, Cdleff, soc(z, T), theta0(), theta100()),
     using only handle calls -- the exporter's algorithm (matlab/mpcekf_tabulate_electrode.m):
@@ -913,7 +1088,10 @@ def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5):
       the function at Tref at every table temperature (identical rows: the library reads
       one), else the function at each table temperature;
     * theta-derivatives by fd_derivs; Hermite cubics (order 3) or quintics (order 5) of
-      every row (hermite_coefs); the v2 node tables alongside (the handle's values)."""
+      every row (hermite_coefs); the v2 node tables alongside (the handle's values);
+    * nodes=True (ABI v4): also the node tables of the functions whose handle workspace
+      carries breakpoints (tabulate_nodes); the library then looks those up on their own
+      nodes and the uniform-grid polynomials of the others."""
     th = np.linspace(0.0, 1.0, int(ntheta))
     T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
     h = 1.0 / (th.size - 1)
@@ -933,10 +1111,69 @@ def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5):
         coefs[name] = np.array(cs)
     y, d1, d2 = fd_derivs(lambda t: fh.Uocp(t), th)
     coefs["Uocp1"] = hermite_coefs(y, d1, h, d2 if order == 5 else None)
+    nd = tabulate_nodes(fh, T_K, Tref, R, ea) if nodes else {}
     return Electrode(theta0=float(fh.theta0()), theta100=float(fh.theta100()),
                      soc0=np.array([fh.soc(0.0, T) for T in T_K]), soc100=np.array([fh.soc(1.0, T) for T in T_K]),
                      Uocp=tabs["Uocp"], Uocp1=y, dUocp=tabs["dUocp"], k0=tabs["k0"], Rf=tabs["Rf"],
-                     Cdleff=tabs["Cdleff"], poly=coefs, Ea=ea or None)
+                     Cdleff=tabs["Cdleff"], poly=coefs, Ea=ea or None, nodes=nd or None)
+
+
+def budget_ok(err):
+    return all(err[k] <= TABLE_BUDGET[k] for k in TABLE_BUDGET)
+
+
+class TableBudgetError(ValueError):
+    """The exported lookups miss TABLE_BUDGET (matlab/mpcekf_build_tables.m refuses such a ROM)."""
+
+    def __init__(self, msg, err):
+        super().__init__(msg)
+        self.err = err
+
+
+def export_electrodes(handles, T_K, Tref=298.15, R=8.3144621, T_eval=None, order=5, nodes=True,
+                      ntheta=None, thlim=None, strict=True):
+    """The exporter's whole table step for both electrodes (matlab/mpcekf_build_tables.m, the
+    helper mpcekf_export_rom and the OB_step drop-in share): node tables where a handle's
+    workspace carries breakpoints and they meet the budget, the uniform-grid polynomials for
+    the rest, with ntheta doubled from 257 to 4097 until every function meets TABLE_BUDGET at
+    T_eval (default: the table temperatures and their midpoints) over each electrode's
+    operating theta range.  Returns ({"neg": Electrode, "pos": ...}, ntheta, errors).  When the
+    budget is missed at 4097: TableBudgetError (strict) or the last tables with their errors."""
+    T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
+    sizes = [int(ntheta)] if ntheta else [257, 513, 1025, 2049, 4097]
+    errs = {}
+    els = {}
+    for nth in sizes:
+        ok = True
+        for side, fh in handles.items():
+            e = tabulate_handles(fh, nth, T_K, Tref, R, order, nodes=nodes)
+            lo, hi = thlim[side] if thlim else (0.0, 1.0)
+            err = table_errors(fh, e, T_K, Tref, R, lo, hi, T_eval=T_eval)
+            if e.nodes:   # a node table that misses the budget falls back to the uniform grid
+                bad = [k for k in list(e.nodes) if not _fn_ok(fh, e, k, T_K, Tref, R, lo, hi, T_eval)]
+                for k in bad:
+                    del e.nodes[k]
+                if bad:
+                    err = table_errors(fh, e, T_K, Tref, R, lo, hi, T_eval=T_eval)
+                e.nodes = e.nodes or None
+            els[side], errs[side] = e, err
+            ok = ok and budget_ok(err)
+        if ok:
+            return els, nth, errs
+    if strict:
+        raise TableBudgetError(f"the electrode tables miss the error budget at {sizes[-1]} theta points: {errs}",
+                               errs)
+    return els, sizes[-1], errs
+
+
+_FN_BUDGET = {"Uocp": "Uocp", "Uocp1": "Uocp", "dUocp": "dUocp_rel", "k0": "k0_rel", "Rf": "Rf_rel",
+              "Cdleff": "Cdleff_rel"}
+
+
+def _fn_ok(fh, e, name, T_K, Tref, R, lo, hi, T_eval):
+    """One function's node table against its TABLE_BUDGET entry (table_errors restricted)."""
+    err = table_errors(fh, e, T_K, Tref, R, lo, hi, T_eval=T_eval, only=name)
+    return err[_FN_BUDGET[name]] <= TABLE_BUDGET[_FN_BUDGET[name]]
 
 
 # error budget of the exported tables (matlab/mpcekf_check_tables.m): north_star's 1e-6
@@ -945,26 +1182,32 @@ def tabulate_handles(fh, ntheta, T_K, Tref=298.15, R=8.3144621, order=5):
 TABLE_BUDGET = {"Uocp": 8e-9, "dUocp_rel": 1e-7, "k0_rel": 1e-9, "Rf_rel": 1e-9, "Cdleff_rel": 1e-3, "soc_lin": 1e-12}
 
 
-def table_errors(fh, e: Electrode, T_K, Tref=298.15, R=8.3144621, theta_lo=0.0, theta_hi=1.0, n=997):
-    """Largest differences of the v3 lookups from the handles (matlab/mpcekf_check_tables.m):
-    at n theta points inside [theta_lo, theta_hi] (interval midpoints included) and at
-    every table temperature and the midpoints between them."""
+def table_errors(fh, e: Electrode, T_K, Tref=298.15, R=8.3144621, theta_lo=0.0, theta_hi=1.0, n=997,
+                 T_eval=None, only=None):
+    """Largest differences of the v3 / v4 lookups from the handles (matlab/mpcekf_check_tables.m):
+    at n theta points inside [theta_lo, theta_hi] and at T_eval, by default every table
+    temperature and the midpoints between them (a caller that knows the temperatures the
+    simulation runs at -- the OB_step drop-in's Tc -- passes those).  only: one function
+    (NODE_FNS name; "Uocp1" is the one-argument Uocp)."""
     T_K = np.atleast_1d(np.asarray(T_K, dtype=float))
     cf = CellFunctions(e, T_K, R, Tref)
     xs = np.linspace(theta_lo, theta_hi, n)
-    Ts = np.sort(np.concatenate([T_K, (T_K[1:] + T_K[:-1]) / 2]))
+    Ts = np.sort(np.concatenate([T_K, (T_K[1:] + T_K[:-1]) / 2])) if T_eval is None else np.atleast_1d(T_eval)
     err = {k: 0.0 for k in TABLE_BUDGET}
+    names = ("dUocp", "k0", "Rf", "Cdleff") if only is None else tuple(k for k in (only,) if k in EL_TABLES[1:])
     for T in Ts:
         for x in xs:
-            u = fh.Uocp(x, T)
-            err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x, T) - u))
-            for nm in ("dUocp", "k0", "Rf", "Cdleff"):
+            if only in (None, "Uocp"):
+                err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x, T) - fh.Uocp(x, T)))
+            for nm in names:
                 ref = getattr(fh, nm)(x, T)
                 err[nm + "_rel"] = max(err[nm + "_rel"], abs(getattr(cf, nm)(x, T) - ref) / max(abs(ref), 1e-300))
-            s0, s1 = fh.soc(0.0, T), fh.soc(1.0, T)
-            err["soc_lin"] = max(err["soc_lin"], abs(fh.soc(x, T) - (s0 + x * (s1 - s0))))
-    for x in xs:
-        err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x) - fh.Uocp(x)))
+            if only is None:
+                s0, s1 = fh.soc(0.0, T), fh.soc(1.0, T)
+                err["soc_lin"] = max(err["soc_lin"], abs(fh.soc(x, T) - (s0 + x * (s1 - s0))))
+    if only in (None, "Uocp1"):
+        for x in xs:
+            err["Uocp"] = max(err["Uocp"], abs(cf.Uocp(x) - fh.Uocp(x)))
     return err
 
 
@@ -1059,6 +1302,194 @@ def make_synth_rom(T_degC=(15.0, 25.0, 35.0), SOC_pct=tuple(range(0, 101, 5)), T
               F=F, R=R, Q=Q, Rc=8.0e-4, Tref=Tref, tab_T_K=T_K, neg=neg, pos=pos,
               meta={"kind": "synthetic-NMC30-like", "version": 2 if lookup == "linear" else 3,
                     "lookup": lookup})
+    rom.handles = {"neg": hn, "pos": hp}
+    rom.validate()
+    return rom
+
+
+# ---------------------------------------------------------------------------------------
+# A second synthetic handle family: lookup-table handles (round 6)
+# ---------------------------------------------------------------------------------------
+# A ROM from the Plett-Trimboli toolchain (README.md:61) commonly carries its OCP as measured
+# data interpolated on the data's own, non-uniform breakpoints, e.g.
+#   Uocp = @(x,T) interp1(xU, U0, x) + (T - Tref) * interp1(xS, dS, x)
+# which is neither smooth nor of the closed forms SynthHandles has.  TabHandles is such a cell:
+# the same NMC30-like curves, but sampled ("measured") at breakpoints clustered at the theta
+# ends and interpolated linearly (interp1) or by pchip; an entropic dU/dT table on its own,
+# coarser breakpoints; dUocp from tabulated derivative data; k0 with a tabulated theta factor
+# and a two-term (not pure Arrhenius) temperature dependence.  workspace(name) mirrors
+# MATLAB's functions(h).workspace{1}, where the exporter finds the breakpoints.
+
+def pchip_slopes(x, y):
+    """MATLAB pchip's node slopes (Fritsch-Butland: the weighted harmonic mean of the
+    neighbouring secants inside, zero at a sign change; the shape-preserving three-point
+    formula at the ends)."""
+    x, y = np.asarray(x, float), np.asarray(y, float)
+    h = np.diff(x)
+    dl = np.diff(y) / h
+    n = x.size
+    d = np.zeros(n)
+    for k in range(1, n - 1):
+        if dl[k - 1] * dl[k] > 0:
+            w1, w2 = 2 * h[k] + h[k - 1], h[k] + 2 * h[k - 1]
+            d[k] = (w1 + w2) / (w1 / dl[k - 1] + w2 / dl[k])
+
+    def end(h0, h1, d0, d1):
+        s = ((2 * h0 + h1) * d0 - h0 * d1) / (h0 + h1)
+        if np.sign(s) != np.sign(d0):
+            s = 0.0
+        elif np.sign(d0) != np.sign(d1) and abs(s) > abs(3 * d0):
+            s = 3 * d0
+        return s
+    d[0] = end(h[0], h[1], dl[0], dl[1])
+    d[-1] = end(h[-1], h[-2], dl[-1], dl[-2])
+    return d
+
+
+class _Table:
+    """y(x) on breakpoints x: interp1 'linear' (clamped to the end values outside [x0, x_end],
+    as the library's theta is clamped to [0, 1]) or 'pchip' (ppval: local Horner, end pieces
+    extended)."""
+
+    def __init__(self, x, y, kind="linear"):
+        self.x, self.y, self.kind = np.asarray(x, float), np.asarray(y, float), kind
+        if kind == "pchip":
+            x, y = self.x, self.y
+            h = np.diff(x)
+            dl = np.diff(y) / h
+            d = pchip_slopes(x, y)
+            self.c = np.stack([y[:-1], d[:-1], (3 * dl - 2 * d[:-1] - d[1:]) / h,
+                               (d[:-1] - 2 * dl + d[1:]) / (h * h)], axis=-1)
+
+    def __call__(self, t):
+        t = float(t)
+        if self.kind == "linear":
+            return float(np.interp(t, self.x, self.y))
+        k = int(np.clip(np.searchsorted(self.x, t, side="right") - 1, 0, self.x.size - 2))
+        s = t - self.x[k]
+        c = self.c[k]
+        return float(c[0] + s * (c[1] + s * (c[2] + s * c[3])))
+
+    def deriv_data(self):
+        """Derivative data at the breakpoints, as a toolchain tabulates dU/dx next to U."""
+        return np.gradient(self.y, self.x, edge_order=2) if self.kind == "linear" else pchip_slopes(self.x, self.y)
+
+
+def clustered_nodes(m_mid=72, m_end=12, edge=0.05, seed=0):
+    """Breakpoints as measured OCP data has them: m_end points over each of [0, edge] and
+    [1 - edge, 1], m_mid over the middle, interior ones jittered by up to 20 % of the local
+    spacing (deterministic)."""
+    rng = np.random.Generator(np.random.PCG64(0x7AB + seed))
+    x = np.unique(np.concatenate([np.linspace(0.0, edge, m_end + 1), np.linspace(edge, 1 - edge, m_mid + 1),
+                                  np.linspace(1 - edge, 1.0, m_end + 1)]))
+    h = np.diff(x)
+    j = rng.uniform(-0.2, 0.2, x.size - 2) * np.minimum(h[:-1], h[1:])
+    x[1:-1] += j
+    return x
+
+
+class TabHandles:
+    """Lookup-table ``cellData.function.{neg,pos}`` handles (see the section comment)."""
+
+    def __init__(self, *, theta0, theta100, u, dudt, kth, Ea_k0, Rf, Ea_rf, wDL, Cdl, nDL, R, Tref, kind="linear",
+                 seed=0):
+        self.th0, self.th100, self.R, self.Tref, self.kind = theta0, theta100, R, Tref, kind
+        xU = clustered_nodes(seed=seed)
+        xS = np.linspace(0.0, 1.0, 31)
+        xS[1:-1] += np.random.Generator(np.random.PCG64(0x5A + seed)).uniform(-0.005, 0.005, 29)
+        xk = np.array([0.0, 0.1, 0.22, 0.35, 0.5, 0.63, 0.78, 0.9, 1.0])
+        self.U0 = _Table(xU, u(xU), kind)                    # measured OCP at Tref
+        self.dS = _Table(xS, dudt(xS), "linear")             # entropic coefficient table
+        self.dU0 = _Table(xU, self.U0.deriv_data(), "linear")
+        self.ddS = _Table(xS, self.dS.deriv_data(), "linear")
+        self.kt = _Table(xk, kth(xk), "linear")
+        self.Ea1, self.Ea2 = Ea_k0                           # two-term kinetics
+        self.Rf0, self.Ea_rf = Rf, Ea_rf
+        self.wDL, self.Cdl, self.nDL = wDL, Cdl, nDL
+
+    def workspace(self, name):
+        """What MATLAB's functions(h).workspace{1} would show for the handle ``name``."""
+        U = {"xU": self.U0.x, "U0": self.U0.y, "xS": self.dS.x, "dS": self.dS.y, "Tref": self.Tref}
+        if name == "Uocp":
+            return U
+        if name == "Uocp1":
+            return {"xU": self.U0.x, "U0": self.U0.y}
+        if name == "dUocp":
+            return {"xU": self.dU0.x, "dU0": self.dU0.y, "xS": self.ddS.x, "ddS": self.ddS.y, "Tref": self.Tref}
+        if name == "k0":
+            return {"xk": self.kt.x, "kk": self.kt.y, "Ea1": self.Ea1, "Ea2": self.Ea2, "R": self.R}
+        if name == "Rf":
+            return {"Rf0": self.Rf0, "Ea": self.Ea_rf, "R": self.R}
+        return {"Cdl": self.Cdl, "wDL": self.wDL, "nDL": self.nDL}
+
+    def theta0(self):
+        return self.th0
+
+    def theta100(self):
+        return self.th100
+
+    def soc(self, z, T):
+        return self.th0 + z * (self.th100 - self.th0)
+
+    def Uocp(self, th, T=None):
+        if T is None:
+            return self.U0(th)
+        return self.U0(th) + (T - self.Tref) * self.dS(th)
+
+    def dUocp(self, th, T):
+        return self.dU0(th) + (T - self.Tref) * self.ddS(th)
+
+    def _arr(self, Ea, T):
+        return math.exp(Ea / self.R * (1.0 / self.Tref - 1.0 / T))
+
+    def k0(self, th, T):
+        return self.kt(th) * (0.6 * self._arr(self.Ea1, T) + 0.4 * self._arr(self.Ea2, T))
+
+    def Rf(self, th, T):
+        return float(self.Rf0 * self._arr(-self.Ea_rf, T) * (0.8 + 0.4 * th))
+
+    def Cdleff(self, th, T):
+        cdl = self.Cdl * (1.0 + 2e-3 * (T - self.Tref))
+        return float((cdl ** (2 - self.nDL)) * (self.wDL ** (self.nDL - 1)))
+
+
+def tab_handles(kind="linear", R=8.3144621, Tref=298.15):
+    """(neg, pos) lookup-table handles of the synthetic NMC30-like cell (TabHandles)."""
+    neg = TabHandles(theta0=0.01, theta100=0.80, u=_u_neg, dudt=lambda x: -1.0e-4 * np.exp(-5 * x),
+                     kth=lambda x: 2.0 * (0.9 + 0.4 * x * (1 - x)), Ea_k0=(3.0e4, 5.0e4), Rf=2.0e-3, Ea_rf=1.0e4,
+                     wDL=5.0, Cdl=150.0, nDL=0.95, R=R, Tref=Tref, kind=kind, seed=0)
+    pos = TabHandles(theta0=0.93, theta100=0.40, u=_u_pos, dudt=lambda x: -0.5e-4 * (1 - x),
+                     kth=lambda x: 4.0 * (0.9 + 0.4 * x * (1 - x)), Ea_k0=(4.0e4, 2.0e4), Rf=3.0e-3, Ea_rf=1.0e4,
+                     wDL=5.0, Cdl=120.0, nDL=0.93, R=R, Tref=Tref, kind=kind, seed=1)
+    return neg, pos
+
+
+def operating_theta(h, pad=0.04):
+    """The electrode's theta range over 0-100 % SOC widened by pad (mpcekf_export_rom's lim)."""
+    a, b = h.soc(0.0, h.Tref), h.soc(1.0, h.Tref)
+    return max(0.0, min(a, b) - pad), min(1.0, max(a, b) + pad)
+
+
+def make_tab_rom(kind="linear", tab_T_degC=(-10.0, 25.0, 60.0), nodes=True, T_eval_degC=None, ntheta=None,
+                 strict=True) -> ROM:
+    """The synthetic cell's models (make_synth_rom) with the lookup-table handles of
+    tab_handles(kind), exported by the exporter's algorithm (export_electrodes) from handle
+    calls alone: ABI v4 node tables for the interp1 / pchip functions (nodes=True), the
+    uniform-grid quintics otherwise.  T_eval_degC: the temperatures the budget is checked at
+    (default the table temperatures and midpoints).  rom.handles = the handles (the numpy
+    oracle's handle mode); rom.meta["tab_error"] = the exporter's errors."""
+    base = make_synth_rom(lookup="quintic", ntab=257)
+    hn, hp = tab_handles(kind, base.R, base.Tref)
+    T_K = np.asarray(tab_T_degC, dtype=float) + 273.15
+    T_eval = None if T_eval_degC is None else np.asarray(T_eval_degC, dtype=float) + 273.15
+    els, nth, errs = export_electrodes({"neg": hn, "pos": hp}, T_K, base.Tref, base.R, T_eval=T_eval, nodes=nodes,
+                                       ntheta=ntheta, thlim={"neg": operating_theta(hn), "pos": operating_theta(hp)},
+                                       strict=strict)
+    rom = ROM(T_degC=base.T_degC, SOC_pct=base.SOC_pct, Ts=base.Ts, A=base.A, C=base.C, D=base.D, names=base.names,
+              xloc=base.xloc, F=base.F, R=base.R, Q=base.Q, Rc=base.Rc, Tref=base.Tref, tab_T_K=T_K,
+              neg=els["neg"], pos=els["pos"],
+              meta={"kind": f"synthetic-NMC30-like, {kind} lookup-table handles", "version": 4 if nodes else 3,
+                    "lookup": "nodes" if nodes else "quintic", "ntheta": nth, "tab_error": errs})
     rom.handles = {"neg": hn, "pos": hp}
     rom.validate()
     return rom

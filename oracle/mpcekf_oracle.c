@@ -106,6 +106,10 @@ typedef struct {
   const double *Uocp_p, *dUocp_p, *k0_p, *Rf_p, *Cdleff_p, *Uocp1_p;
   double Ea[5];
   int tconst; /* bit f: every row of function f's polynomials is the same (row 0 blended with itself) */
+  /* ABI v4 (include/mpcekf.h): function f (Uocp, dUocp, k0, Rf, Cdleff, Uocp1) on its own
+   * theta nodes when nnode[f] >= 2: node[f] [m], node_p[f] [ntemp][m-1][6] ([m-1][6]) */
+  int nnode[6];
+  const double *node[6], *node_p[6];
 } orc_electrode;
 
 typedef struct {
@@ -223,6 +227,28 @@ static double tab_poly(const double *c, int n, double x) {
   v = fma(s, v, p[1]);
   return fma(s, v, p[0]);
 }
+/* ABI v4 row (include/mpcekf.h node / node_p): theta clamped to [0, 1], its segment
+ * k = #{j in 1..m-2 : x_j <= theta} (found by bisection here; the kernels read it from a
+ * uniform bucket map built to give this k), then Horner with explicit fma over 6
+ * coefficients in s = theta - x_k (rom.py interp_nodes without fma) */
+static double node_poly(const double *x, int m, const double *c, double th) {
+  if (th != th) return NAN;
+  const double xc = fmin(fmax(th, 0.0), 1.0);
+  int lo = 0, hi = m - 2; /* the largest k in [0, m-2] with k == 0 or x[k] <= xc */
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) / 2;
+    if (x[mid] <= xc) lo = mid;
+    else hi = mid - 1;
+  }
+  const double s = xc - x[lo];
+  const double *p = c + (size_t)lo * NPOLY;
+  double v = p[5];
+  v = fma(s, v, p[4]);
+  v = fma(s, v, p[3]);
+  v = fma(s, v, p[2]);
+  v = fma(s, v, p[1]);
+  return fma(s, v, p[0]);
+}
 /* Defined exp (the v3 Arrhenius factor; rom.py dexp, mpcekf_kernels.hip dexp): fdlibm's
  * reduction x = k ln2 + r (k = floor(x / ln2 + 1/2)) and its rational form for exp(r);
  * +, -, *, /, floor and ldexp only, each exact or correctly rounded on both sides. */
@@ -245,13 +271,23 @@ double orc_exp(double x) {
 /* One handle lookup (include/mpcekf.h): the rows j, j+1 of the T bracket at
  * theta (linear in the node values, or the v3 polynomials), a + g (b - a), then the
  * Arrhenius factor exp(Ea/R (1/Tref - 1/T)) when Ea != 0 (T unclamped). */
-static double tab2(const orc_rom *r, const double *t, const double *tp, double Ea, int one, double th, double T) {
+static double tab2(const orc_rom *r, const orc_electrode *e, int f, const double *t, const double *tp, double th,
+                   double T) {
+  const double Ea = e->Ea[f];
+  const int one = (e->tconst >> f) & 1;
   int j;
   double g;
   tidx(r, T, &j, &g);
   const size_t rp = (size_t)(r->ntheta - 1) * NPOLY;
   double a;
-  if (tp) {
+  if (e->nnode[f] >= 2) { /* v4: the function's own nodes, rows blended as v3's */
+    const int m = e->nnode[f];
+    const size_t np = (size_t)(m - 1) * NPOLY;
+    if (one) j = 0;
+    a = node_poly(e->node[f], m, e->node_p[f] + j * np, th);
+    const double b = (one || r->ntemp == 1) ? a : node_poly(e->node[f], m, e->node_p[f] + (j + 1) * np, th);
+    a = a + g * (b - a);
+  } else if (tp) {
     /* v3: rows j and j + 1 blended; a T-invariant function (all rows equal, `one`) or a
      * single-temperature table blends row 0 with itself, a + g (a - a) (the library's one
      * lookup path, mpcekf_kernels.hip ETab::f) */
@@ -282,22 +318,23 @@ static double fsoc(const orc_rom *r, const orc_electrode *e, double z, double T)
   return s0 + z * (s1 - s0);
 }
 static double fUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Uocp, e->Uocp_p, e->Ea[EF_U], (e->tconst >> EF_U) & 1, th, T);
+  return tab2(r, e, EF_U, e->Uocp, e->Uocp_p, th, T);
 }
 static double fUocp1(const orc_rom *r, const orc_electrode *e, double th) {
+  if (e->nnode[5] >= 2) return node_poly(e->node[5], e->nnode[5], e->node_p[5], th);
   return e->Uocp1_p ? tab_poly(e->Uocp1_p, r->ntheta, th) : tab_interp(e->Uocp1, r->ntheta, th);
 }
 static double fdUocp(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->dUocp, e->dUocp_p, e->Ea[EF_DU], (e->tconst >> EF_DU) & 1, th, T);
+  return tab2(r, e, EF_DU, e->dUocp, e->dUocp_p, th, T);
 }
 static double fk0(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->k0, e->k0_p, e->Ea[EF_K0], (e->tconst >> EF_K0) & 1, th, T);
+  return tab2(r, e, EF_K0, e->k0, e->k0_p, th, T);
 }
 static double fRf(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Rf, e->Rf_p, e->Ea[EF_RF], (e->tconst >> EF_RF) & 1, th, T);
+  return tab2(r, e, EF_RF, e->Rf, e->Rf_p, th, T);
 }
 static double fCdl(const orc_rom *r, const orc_electrode *e, double th, double T) {
-  return tab2(r, e->Cdleff, e->Cdleff_p, e->Ea[EF_CDL], (e->tconst >> EF_CDL) & 1, th, T);
+  return tab2(r, e, EF_CDL, e->Cdleff, e->Cdleff_p, th, T);
 }
 static double msqrt(double x) { return x >= 0 ? sqrt(x) : NAN; }
 
@@ -618,6 +655,23 @@ static double hild_row_t(int Nc, const double *Mi, const double *v, double Ki) {
   return b[0];
 }
 
+/* hildreth.m:35's update w = -(K_i + H(i,:)*lambda - H_ii lambda_i) / H_ii, with t_i =
+ * K_i + H(i,:)*lambda: the defined spelling (round 6) is w = lambda_i - t_i / H_ii as one
+ * fma with the reciprocal, fma(-t_i, 1/H_ii, lambda_i) -- 1/H_ii once per solve and row, so
+ * the per-row chain is t -> w -> max -> d instead of t -> num -> divide (3 ops) -> max -> d.
+ * Outside the reciprocal's normal range (|H_ii| not 0 and outside [2^-1020, 2^1020]: 1/H_ii
+ * would overflow or lose bits) or with a non-finite lambda_i (an inf lambda_i with H_ii = 0
+ * is NaN in MATLAB's H_ii * lambda_i term) the division form fma(H_ii, lambda_i, -t_i) / H_ii.
+ * H_ii = +-0 (the SOC block's first row, predMat G(1,1) = 0): 1/H_ii = +-inf and
+ * fma(-t, +-inf, lambda) is x / +-0's inf / NaN by IEEE, as the division form gives it. */
+static int hild_rok(double h) {
+  const double a = fabs(h);
+  return h == 0.0 || (a >= 0x1p-1020 && a <= 0x1p1020);
+}
+static double hild_w(double t, double h, double rinv, double l) {
+  return (hild_rok(h) && isfinite(l)) ? fma(-t, rinv, l) : fma(h, l, -t) / h;
+}
+
 int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double *M /*nC x Nc*/,
                  const double *gam, double *lam /*in: warm start, out*/, int maxIter, double tol,
                  double *DU) {
@@ -643,7 +697,7 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
    * Defined evaluation (the kernels evaluate the same sequence):
    *  - finite X and M: v recomputed from lambda at the start of every sweep (fma
    *    accumulation from +0 in ascending j), t_i = K_i + M(i,:)*v as hild_row_t,
-   *    w = fma(H_ii, lambda_i, -t_i) / H_ii (= -(K_i + s_i - H_ii lambda_i) / H_ii), and
+   *    w = hild_w(t_i, H_ii, 1/H_ii, lambda_i) (= -(K_i + s_i - H_ii lambda_i) / H_ii), and
    *    after row i v += X(:,i)*(new - old lambda(i)) by fma; when that change is not
    *    finite (a zero-diagonal row going to or from +inf) v is recomputed from lambda
    *    instead, which reproduces the dense form's inf/NaN propagation in kind.
@@ -661,7 +715,7 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
       double w, hii = H[i * HMAX + i];
       if (finite) {
         double t = hild_row_t(Nc, M + i * Nc, v, K[i]);
-        w = fma(hii, lam[i], -t) / hii;
+        w = hild_w(t, hii, 1.0 / hii, lam[i]);
       } else {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];

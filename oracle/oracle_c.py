@@ -28,7 +28,8 @@ class _Electrode(C.Structure):
     _fields_ = [("theta0", C.c_double), ("theta100", C.c_double), ("soc0", _dp), ("soc100", _dp),
                 ("Uocp", _dp), ("dUocp", _dp), ("k0", _dp), ("Rf", _dp), ("Cdleff", _dp), ("Uocp1", _dp),
                 ("Uocp_p", _dp), ("dUocp_p", _dp), ("k0_p", _dp), ("Rf_p", _dp), ("Cdleff_p", _dp),
-                ("Uocp1_p", _dp), ("Ea", C.c_double * 5), ("tconst", C.c_int)]
+                ("Uocp1_p", _dp), ("Ea", C.c_double * 5), ("tconst", C.c_int),
+                ("nnode", C.c_int * 6), ("node", _dp * 6), ("node_p", _dp * 6)]   # ABI v4
 
 
 EL_FNS = ("Uocp", "dUocp", "k0", "Rf", "Cdleff")   # orc_electrode.Ea order (EF_*)
@@ -144,14 +145,21 @@ class PackedRom:
             s.theta0, s.theta100 = e.theta0, e.theta100
             for k in ("soc0", "soc100", "Uocp", "dUocp", "k0", "Rf", "Cdleff", "Uocp1"):
                 setattr(s, k, _p(arr(getattr(e, k))))
+            nd = e.nodes or {}
             for k in EL_FNS + ("Uocp1",):   # ABI v3 polynomials (NULL: linear tables)
-                setattr(s, k + "_p", _p(arr(poly6(e.poly[k]))) if e.poly else _dp())
+                setattr(s, k + "_p", _p(arr(poly6(e.poly[k]))) if e.poly and k in e.poly else _dp())
             for i, k in enumerate(EL_FNS):
                 s.Ea[i] = float((e.Ea or {}).get(k, 0.0))
                 # rows all equal (an exact Arrhenius function): row 0 blended with itself (the library's one path)
-                if e.poly and e.poly[k].shape[0] > 1 and all(np.array_equal(e.poly[k][0], e.poly[k][j])
-                                                             for j in range(1, e.poly[k].shape[0])):
+                rows = np.asarray(nd[k][1]) if k in nd else (np.asarray(e.poly[k]) if e.poly else None)
+                if rows is not None and rows.shape[0] > 1 and all(np.array_equal(rows[0], rows[j])
+                                                                  for j in range(1, rows.shape[0])):
                     s.tconst |= 1 << i
+            for i, k in enumerate(EL_FNS + ("Uocp1",)):   # ABI v4 node tables
+                if k in nd:
+                    s.nnode[i] = int(np.asarray(nd[k][0]).size)
+                    s.node[i] = _p(arr(nd[k][0]))
+                    s.node_p[i] = _p(arr(poly6(nd[k][1])))
         self.s = r
 
 

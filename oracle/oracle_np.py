@@ -9,7 +9,7 @@ PARITY UNPINNED: the reference is MATLAB (no MATLAB/Octave in this image) and
 ships no tests, fixtures or golden vectors; its ROM file ROM_NMC30_HRA.mat is
 missing (.MISSING_LARGE_BLOBS:1).  This restatement therefore runs on the
 synthetic ROM of ``rom.py`` and is pinned only by analytic known-answer tests
-(tests/test_oracle_kat.py) and by agreement with the independent C
+(tests/test_oracle.py, the KATs of its first half) and by agreement with the independent C
 restatement (oracle/mpcekf_oracle.c).  See DESIGN.md "Oracle".
 
 Conventions (identical in the C oracle and the kernels):
@@ -980,8 +980,10 @@ def constraints_mpc(x, MPC, mpc, Phi_s, G_s):
     return np.vstack(Ms), np.concatenate(gs)
 
 
-def hildreth(E, F, M, gamma, lam0, maxIter, tol=1e-6):
-    """hildreth.m:1-46 (dense H, Gauss-Seidel dual coordinate ascent)."""
+def hildreth(E, F, M, gamma, lam0, maxIter, tol=1e-6, recip=False):
+    """hildreth.m:1-46 (dense H, Gauss-Seidel dual coordinate ascent).  recip (test
+    infrastructure, tools/make_golden.py's ulp ensembles): the row update as
+    lambda_i - t_i * (1/H_ii), an ulp-level implementation variant of hildreth.m:35."""
     nC = M.shape[0]
     lam = np.zeros(nC) if lam0 is None else np.array(lam0, dtype=float)
     X = mldivide_spd(E, M.T)                                    # E\M'
@@ -994,7 +996,10 @@ def hildreth(E, F, M, gamma, lam0, maxIter, tol=1e-6):
             s = 0.0
             for j in range(nC):
                 s = s + H[i, j] * lam[j]
-            w = -(K[i] + s - H[i, i] * lam[i]) / H[i, i]
+            if recip:
+                w = lam[i] - (K[i] + s) * (1.0 / H[i, i])
+            else:
+                w = -(K[i] + s - H[i, i] * lam[i]) / H[i, i]
             lam[i] = w if w > 0 else 0.0
         d = lam - lam_old
         conv = True
@@ -1044,7 +1049,7 @@ def iter_mpc(xk, MPC, mpc, smin=None):
     viol = mv(M, DU) - gamma
     nexec = 0
     if np.sum(viol > 0) > 0:
-        DU, lam, nexec = hildreth(E, F, M, gamma, mpc["lam"], mpc["maxHild"])
+        DU, lam, nexec = hildreth(E, F, M, gamma, mpc["lam"], mpc["maxHild"], recip=bool(mpc.get("hild_recip")))
         mpc["lam"] = lam
     uk = DU[0] + mpc["uk_1"]
     mpc["uk_1"] = uk
@@ -1081,6 +1086,7 @@ def _run_cell(rom, SOC0, TC, nsteps, cfg, record_state, tc_traj=None):
     ekf = init_kf(rom, SOC0, TC, SigmaX0, c["SigmaV"], c["SigmaW"], c.get("method", "OB"), hm)
     mpc = init_mpc(rom, SOC0, c["Np"], c["Nc"], c["targetSOC"], c)
     cs = ob_step_init(rom, SOC0, TC, hm)
+    mpc["hild_recip"] = bool(c.get("hild_recip", False))   # test infrastructure (ulp ensembles)
     uk = 0.0
     ob_step(uk, TC, cs)                                         # runMPC.m:74 (state no-op)
     nz = rom.nz

@@ -169,6 +169,11 @@ def rom_struct(rom):
             d["poly"] = {k: np.asarray(v, float) for k, v in e.poly.items()}
         if e.Ea:
             d["Ea"] = np.array([float(e.Ea.get(k, 0.0)) for k in ("Uocp", "dUocp", "k0", "Rf", "Cdleff")])
+        if e.nodes:   # ABI v4 (mpcekf_build_tables.m's nodes): p padded to the poly tables' order
+            def pad(c):
+                c = np.asarray(c, float)
+                return np.concatenate([c, np.zeros(c.shape[:-1] + (rom.npoly - c.shape[-1],))], -1)
+            d["nodes"] = {k: {"x": np.asarray(x, float), "p": pad(c)} for k, (x, c) in e.nodes.items()}
         return d
     el_ = el3
     return dict(T_degC=np.asarray(rom.T_degC, float), SOC_pct=np.asarray(rom.SOC_pct, float), Ts=float(rom.Ts),

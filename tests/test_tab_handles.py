@@ -1,0 +1,221 @@
+"""CPU: lookup-table cellData.function handles and the ABI v4 node tables (round 6).
+
+A ROM from the Plett-Trimboli toolchain (README.md:61) commonly carries its OCP-type
+handles as measured data interpolated on the data's own breakpoints,
+e.g. Uocp = @(x,T) interp1(xU, U0, x) + (T - Tref) * interp1(xS, dS, x), called by the
+reference at OB_step.m:313-314,337-340, iterEKF.m:362-363,404-407,495-500,577-580 and
+EKFmatsHandler.m:84-85,96.  rom.py TabHandles is such a family (interp1-linear and pchip
+variants over 96 breakpoints clustered at the theta ends, an entropic table on 31 other
+breakpoints, derivative tables for dUocp, a k0 with a tabulated theta factor and a two-term,
+not pure Arrhenius, temperature dependence).  These tests show:
+
+* the exporter's algorithm (rom.export_electrodes, mirrored by matlab/mpcekf_build_tables.m)
+  finds the breakpoints in the handles' workspaces and builds ABI v4 node tables that equal
+  the handles to rounding (interp1 and pchip);
+* the v3 uniform-grid quintics cannot follow a slope break: the exporter refuses them at
+  every ntheta up to 4097, and forced through, they miss the handle fixtures by > 1e-6;
+* a non-Arrhenius k0 is exact only at table temperatures: the budget check at the
+  temperatures a drop-in runs at refuses a table that does not hold them (the OB_step
+  drop-in's budget-missing case);
+* the C oracle's v4 lookups follow the numpy handle-mode fixtures
+  (tests/golden/tab_*.npz, pchip_*.npz; tools/make_golden.py make_tab_handles) within 1e-6,
+  and the v4 ROM round-trips JSON (format mpcekf-rom-v4) and npz.
+
+Tolerances: 1e-13 relative (to max(|U|, 1 V)) / 1e-12 relative on the pointwise lookups
+(the handles to rounding: a pchip segment is refitted from 4 handle calls), north_star's
+1e-6 relative on the closed loop.
+"""
+import os
+
+import numpy as np
+import pytest
+
+KEYS = ("u", "v", "soc", "phise")
+RTOL = 1e-6
+
+
+def rel(a, b):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    d = np.abs(a - b) / np.maximum(np.abs(b), 1e-300)
+    d[np.isnan(a) & np.isnan(b)] = 0.0
+    d[np.isnan(d)] = np.inf
+    return d
+
+
+def golden(name):
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+
+
+@pytest.fixture(scope="module")
+def R():
+    from importlib import import_module
+    return import_module("mpc-ekf4fastcharge_amd.rom")
+
+
+def fixture_rom(R, g):
+    return R.make_tab_rom(str(g["kind"]), tab_T_degC=tuple(g["tab_T_degC"]), T_eval_degC=tuple(g["T_eval_degC"]))
+
+
+@pytest.mark.parametrize("kind", ["linear", "pchip"])
+def test_node_tables_equal_the_handles(R, kind):
+    """Every function with breakpoints in its workspace is on its own nodes (Uocp and dUocp
+    on the union of the OCP and entropy breakpoints, k0 on its 9, Uocp1 on the OCP's 96),
+    and every lookup equals the handle to rounding over the whole theta range, at the table
+    temperatures and (Uocp, affine in T) between them."""
+    rom = R.make_tab_rom(kind, T_eval_degC=(25.0,))
+    for side in ("neg", "pos"):
+        e, h = getattr(rom, side), rom.handles[side]
+        assert set(e.nodes) == {"Uocp", "dUocp", "k0", "Uocp1"}
+        assert e.nodes["Uocp1"][0].size == h.U0.x.size
+        assert np.array_equal(e.nodes["Uocp"][0], np.union1d(h.U0.x, h.dS.x))
+        cf = R.CellFunctions(e, rom.tab_T_K, rom.R, rom.Tref)
+        xs = np.concatenate([np.linspace(0, 1, 2001), h.U0.x, h.dS.x, h.U0.x[1:-1] - 1e-13])
+        for T in list(rom.tab_T_K) + [290.0, 305.5]:   # relative to max(|U|, 1 V): the synthetic
+            # positive OCP reaches 2.4e5 V at theta = 0, far outside its operating range
+            u = max(abs(cf.Uocp(x, T) - h.Uocp(x, T)) / max(abs(h.Uocp(x, T)), 1.0) for x in xs)
+            assert u < 1e-13, (side, T, u)
+        T = 298.15
+        for nm in ("dUocp", "k0"):
+            d = max(abs(getattr(cf, nm)(x, T) - getattr(h, nm)(x, T)) / abs(getattr(h, nm)(x, T)) for x in xs)
+            assert d < 1e-12, (side, nm, d)
+        assert max(abs(cf.Uocp(x) - h.Uocp(x)) / max(abs(h.Uocp(x)), 1.0) for x in xs) < 1e-13
+
+
+def test_interp1_linear_segments_are_stored_as_interp1(R):
+    """An interp1-linear handle's segments are (y_k, slope_k, 0, 0): the lookup is y_k +
+    (theta - x_k) slope_k, np.interp's arithmetic up to its separate rounding of the product."""
+    rom = R.make_tab_rom("linear", T_eval_degC=(25.0,))
+    x, c = rom.neg.nodes["Uocp1"]
+    assert np.all(c[:, 2:] == 0.0)
+    h = rom.handles["neg"]
+    assert np.array_equal(c[:, 0], h.U0.y[:-1])
+    xs = np.linspace(0, 1, 5001)
+    err = max(abs(R.interp_nodes(x, c, t) - np.interp(t, h.U0.x, h.U0.y)) for t in xs)
+    assert err <= 4 * np.finfo(float).eps
+
+
+def test_v3_is_refused_on_lookup_table_handles(R):
+    """Without node tables the exporter's budget loop (257 .. 4097 uniform theta points)
+    cannot meet TABLE_BUDGET on an interp1 OCP -- the slope breaks -- and refuses."""
+    hn, hp = R.tab_handles("linear")
+    T_K = np.array([-10.0, 25.0, 60.0]) + 273.15
+    with pytest.raises(R.TableBudgetError) as ei:
+        R.export_electrodes({"neg": hn, "pos": hp}, T_K, T_eval=np.array([298.15]), nodes=False,
+                            thlim={"neg": R.operating_theta(hn), "pos": R.operating_theta(hp)})
+    err = ei.value.err
+    assert err["neg"]["Uocp"] > 1e-6 and err["pos"]["Uocp"] > 1e-6   # vs a budget of 8e-9
+
+
+def test_budget_refuses_a_non_arrhenius_k0_between_table_rows(R):
+    """The drop-in's case (matlab/dropin/OB_step.m -> mpcekf_build_tables): eight cells at
+    eight distinct Tc, tables on a grid that does not hold them (the set-points and the Tc
+    span): the two-term k0 is off between rows, the budget at the Tc refuses the ROM, and
+    with the Tc as table temperatures it passes."""
+    hn, hp = R.tab_handles("linear")
+    tc = np.array([20.4, 21.7, 22.9, 24.2, 25.3, 26.8, 28.1, 29.6])
+    grid = np.array([15.0, 20.4, 25.0, 29.6, 35.0]) + 273.15
+    lim = {"neg": R.operating_theta(hn), "pos": R.operating_theta(hp)}
+    with pytest.raises(R.TableBudgetError) as ei:
+        R.export_electrodes({"neg": hn, "pos": hp}, grid, T_eval=tc + 273.15, ntheta=257, thlim=lim)
+    assert ei.value.err["neg"]["k0_rel"] > 1e-6
+    els, nth, errs = R.export_electrodes({"neg": hn, "pos": hp}, tc + 273.15, T_eval=tc + 273.15, thlim=lim)
+    assert nth == 257 and all(R.budget_ok(e) for e in errs.values())
+    assert errs["neg"]["k0_rel"] < 1e-14
+
+
+def test_discover_nodes_mirrors_the_workspace_scan(R):
+    """MATLAB's functions(h).workspace{1} scan: ascending vectors inside [0, 1] with >= 3
+    entries, recursing into captured handles; scalars, data values outside [0, 1] and
+    non-monotone vectors are ignored; a closed-form handle has none."""
+    class H:
+        def __init__(self, ws):
+            self.ws = ws
+
+        def workspace(self):
+            return self.ws
+
+        def __call__(self, *a):
+            return 0.0
+    inner = H({"xq": np.array([0.0, 0.3, 1.0]), "y": np.array([3.0, 2.0, 1.0])})
+    ws = {"x": np.array([0.0, 0.5, 0.7, 1.0]), "U": np.array([4.1, 3.9, 3.7, 3.5]), "T": 298.15,
+          "g": inner, "bad": np.array([0.2, 0.1, 0.9]), "wide": np.array([0.0, 2.0, 4.0])}
+    assert np.array_equal(R.discover_nodes(ws), [0.0, 0.3, 0.5, 0.7, 1.0])
+    assert R.discover_nodes({"k": 2.0, "Ea": 3e4}) is None
+
+
+def test_v4_rom_round_trips_json_and_npz(R, tmp_path):
+    rom = R.make_tab_rom("pchip", T_eval_degC=(25.0,))
+    d = rom.to_json_dict()
+    assert d["format"] == "mpcekf-rom-v4"
+    rom.save_json(tmp_path / "r.json")
+    rom.save_npz(tmp_path / "r.npz")
+    for back in (R.ROM.load_json(tmp_path / "r.json"), R.ROM.load_npz(tmp_path / "r.npz")):
+        back.validate()
+        for side in ("neg", "pos"):
+            a, b = getattr(rom, side).nodes, getattr(back, side).nodes
+            assert set(a) == set(b)
+            for k in a:
+                assert np.array_equal(a[k][0], b[k][0]) and np.array_equal(a[k][1], b[k][1])
+
+
+def test_c_oracle_v4_matches_numpy_v4_tables(R, oc):
+    """The C oracle's node lookups (bisection) against the numpy restatement reading the same
+    v4 tables (table mode): 1e-12 over 200 steps of 8 cells (same tables, two restatements)."""
+    import oracle_np as O
+    g = golden("tab_batch8_1000")
+    rom = fixture_rom(R, g)
+    out = oc.run(rom, g["soc0"], g["tc"], 200, nthreads=4)
+    for c in range(0, 8, 3):
+        ref = O.run_cell(rom, float(g["soc0"][c]), float(g["tc"][c]), 200)
+        for k in KEYS:
+            assert rel(out[k][:, c], ref[k]).max() < 1e-12, (c, k)
+
+
+@pytest.mark.parametrize("name", ["tab_batch8_1000", "pchip_batch8_300"])
+def test_c_oracle_v4_follows_the_tab_handle_fixtures(R, oc, name):
+    """North_star's 1e-6 on every step of every cell against the numpy restatement calling
+    the lookup-table handles themselves (the reference's semantics)."""
+    g = golden(name)
+    rom = fixture_rom(R, g)
+    assert g["rom_hash"].item() == _hash(rom)
+    out = oc.run(rom, g["soc0"], g["tc"], g["u"].shape[0], nthreads=8)
+    for k in KEYS:
+        d = rel(out[k], g[k])
+        assert d.max() < RTOL, (k, d.max(), np.unravel_index(np.argmax(d), d.shape))
+    assert np.array_equal(out["nexec"], g["nexec"])
+
+
+def test_c_oracle_v4_follows_the_tab_runmpc_fixture(R, oc):
+    """The runMPC.m cell on the lookup-table handles: within 1e-6 on every step where the
+    fixture's ulp ensemble is itself narrower than 1e-6 (tail0 on)."""
+    g = golden("tab_runmpc_3001")
+    rom = fixture_rom(R, g)
+    out = oc.run(rom, g["soc0"], g["tc"], 3001, nthreads=1)
+    t0 = int(g["tail0"])
+    assert t0 > 2000
+    for k in KEYS:
+        d = rel(out[k][:t0], g[k][:t0])
+        assert d.max() < RTOL, (k, d.max(), int(np.argmax(d.max(1))))
+
+
+@pytest.mark.parametrize("name", ["tab_batch8_1000", "pchip_batch8_300"])
+def test_v3_quintic_tables_miss_the_tab_fixtures(R, oc, name):
+    """The same cells on v3 uniform quintics (513 theta, forced past the budget): off the
+    handles' trajectories by far more than 1e-6 -- what the node tables fix."""
+    g = golden(name)
+    rom = R.make_tab_rom(str(g["kind"]), tab_T_degC=tuple(g["tab_T_degC"]), T_eval_degC=tuple(g["T_eval_degC"]),
+                         nodes=False, ntheta=513, strict=False)
+    assert not rom.neg.nodes and not rom.pos.nodes
+    n = min(300, g["u"].shape[0])
+    out = oc.run(rom, g["soc0"], g["tc"], n, nthreads=8)
+    worst = max(rel(out[k], g[k][:n]).max() for k in ("v", "phise"))
+    assert worst > 1e-5, worst
+
+
+def _hash(rom):
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in sorted(rom.to_npz_dict().items()):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(v).tobytes())
+    return h.hexdigest()

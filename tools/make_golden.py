@@ -131,16 +131,23 @@ def make_envelopes(rom, hsh):
     ks17 = list(range(-8, 9))
     ks9 = list(range(-4, 5))
     NK_RUN, NK_NEAR = 32, 16  # members with a 1-ulp random kick of the command every step
+    NK_RECIP, NK_RECIP_NEAR = 32, 8  # + kicked members with the reciprocal row form
     soc0n, tcn = np.array([88.0, 90.5, 93.0, 95.0]), np.array([25.0, 21.0, 29.0, 24.0])
     jobs = [(s, 25.0, 3001, None) for s in _ulp_members(10.0, ks17)]
     jobs += [(10.0, 25.0, 3001, {"ulp_kick": (1000 + i, 1)}) for i in range(NK_RUN)]
+    # round 6: members with hildreth.m:35 spelled lambda_i - t_i (1/H_ii) (the reciprocal
+    # form the C oracle and the kernels now define), kicked as above -- the same ulp-level
+    # implementation freedom, sampled from the other spelling
+    jobs += [(10.0, 25.0, 3001, {"ulp_kick": (5000 + i, 1), "hild_recip": True}) for i in range(NK_RECIP)]
     for ci, (s0, t0) in enumerate(zip(soc0n, tcn)):
         jobs += [(s, float(t0), 200, {"Np": 20, "Nc": 10}) for s in _ulp_members(s0, ks9)]
         jobs += [(float(s0), float(t0), 200, {"Np": 20, "Nc": 10, "ulp_kick": (2000 + 100 * ci + i, 1)})
                  for i in range(NK_NEAR)]
+        jobs += [(float(s0), float(t0), 200, {"Np": 20, "Nc": 10, "ulp_kick": (6000 + 100 * ci + i, 1),
+                                              "hild_recip": True}) for i in range(NK_RECIP_NEAR)]
     with Pool(min(8, os.cpu_count() or 1)) as pool:
         outs = pool.map(_env_cell, jobs)
-    nrun = 17 + NK_RUN
+    nrun = 17 + NK_RUN + NK_RECIP
     run = outs[:nrun]
     env = {}
     for k in ("u", "v", "soc", "phise"):
@@ -151,9 +158,9 @@ def make_envelopes(rom, hsh):
     env["t90"] = np.array([int(np.argmax(soc[:, j] >= 0.90)) if (soc[:, j] >= 0.90).any() else -1
                            for j in range(soc.shape[1])])
     np.savez_compressed(os.path.join(OUT, "env_runmpc_3001.npz"), rom_hash=hsh, soc0=[10.0], tc=[25.0],
-                        ulps=ks17, kicked=NK_RUN, **env)
+                        ulps=ks17, kicked=NK_RUN, kicked_recip=NK_RECIP, **env)
     near = outs[nrun:]
-    per = 9 + NK_NEAR
+    per = 9 + NK_NEAR + NK_RECIP_NEAR
     env = {}
     for k in ("u", "v", "soc", "phise"):
         a = np.stack([np.stack([near[c * per + j][k] for j in range(per)], 1) for c in range(4)], 1)  # [200, 4, m]
@@ -165,7 +172,7 @@ def make_envelopes(rom, hsh):
         env[k + "_wlo"], env[k + "_whi"] = np.percentile(w, 10, axis=0), np.percentile(w, 90, axis=0)
     env["soc_end"] = np.stack([np.stack([near[c * per + j]["soc"][-1] for j in range(per)]) for c in range(4)])
     np.savez_compressed(os.path.join(OUT, "env_wide_near4_200.npz"), rom_hash=hsh, soc0=soc0n, tc=tcn, Np=20, Nc=10,
-                        ulps=ks9, kicked=NK_NEAR, **env)
+                        ulps=ks9, kicked=NK_NEAR, kicked_recip=NK_RECIP_NEAR, **env)
 
 
 def _handle_cell(args):
@@ -246,8 +253,82 @@ def make_handles():
                             **extra, **r)
 
 
+# round 6: the lookup-table handle family (rom.py TabHandles)
+TAB_SOC0_SEED = 0x7AB1
+
+
+def tab_cases():
+    """(name, kind, tab_T_degC, T_eval_degC, soc0, tc, steps) of the lookup-table fixtures; the
+    ROM of each is rom.make_tab_rom(kind, tab_T_degC, T_eval_degC=T_eval_degC)."""
+    rng = np.random.Generator(np.random.PCG64(TAB_SOC0_SEED))
+    soc0, tc = rng.uniform(5, 30, 8), np.round(rng.uniform(20, 30, 8), 2)
+    return [("tab_runmpc_3001", "linear", (-10.0, 25.0, 60.0), (25.0,), np.array([10.0]), np.array([25.0]), 3001),
+            ("tab_batch8_1000", "linear", tuple(np.sort(tc)), tuple(tc), soc0, tc, 1000),
+            ("pchip_batch8_300", "pchip", tuple(np.sort(tc)), tuple(tc), soc0, tc, 300)]
+
+
+def _tab_cell(args):
+    kind, tabT, Tev, soc0, tc, steps, cfg = args
+    R = importlib.import_module("mpc-ekf4fastcharge_amd.rom")
+    rom = R.make_tab_rom(kind, tab_T_degC=tabT, T_eval_degC=Tev)
+    c = {"handles": True}
+    c.update(cfg or {})
+    o = O.run_cell(rom, soc0, tc, steps, c)
+    return {k: o[k] for k in ("u", "v", "soc", "phise", "nexec", "status")}
+
+
+def make_tab_handles():
+    """Handle-mode fixtures of the lookup-table family (round 6): the numpy restatement
+    calling TabHandles (interp1 / pchip over non-uniform breakpoints, a two-term k0) at every
+    call site.  The library's ABI v4 node tables are held to these within 1e-6; v3 uniform
+    quintics cannot be (the exporter refuses them).  The runMPC cell carries a ulp ensemble
+    (SOC0 -4..+4 ulps, 16 kicked members) marking where one trajectory stops being followable."""
+    from multiprocessing import Pool
+    R = importlib.import_module("mpc-ekf4fastcharge_amd.rom")
+    cases = tab_cases()
+    ks = list(range(-4, 5))
+    NK = 16
+    jobs = []
+    name, kind, tabT, Tev, soc0, tc, steps = cases[0]
+    jobs += [(kind, tabT, Tev, s, 25.0, steps, None) for s in _ulp_members(10.0, ks)]
+    jobs += [(kind, tabT, Tev, 10.0, 25.0, steps, {"ulp_kick": (7000 + i, 1)}) for i in range(NK)]
+    for name, kind, tabT, Tev, soc0, tc, steps in cases[1:]:
+        jobs += [(kind, tabT, Tev, float(s), float(t), steps, None) for s, t in zip(soc0, tc)]
+    with Pool(min(8, os.cpu_count() or 1)) as pool:
+        outs = pool.map(_tab_cell, jobs)
+    keys = ("u", "v", "soc", "phise", "nexec")
+    run, outs = outs[:len(ks) + NK], outs[len(ks) + NK:]
+    one = run[ks.index(0)]
+    env = {}
+    for k in ("u", "v", "soc", "phise"):
+        a = np.stack([o[k] for o in run], axis=1)
+        env[k + "_min"], env[k + "_max"] = a.min(1), a.max(1)
+    wide = np.zeros(3001, dtype=bool)
+    for k in ("u", "v", "soc", "phise"):
+        lo, hi = env[k + "_min"], env[k + "_max"]
+        wide |= (hi - lo) > 1e-6 * np.maximum(np.abs(lo), np.abs(hi))
+    env["tail0"] = int(np.argmax(wide)) if wide.any() else 3001
+    name, kind, tabT, Tev, soc0, tc, steps = cases[0]
+    hsh = rom_hash(R.make_tab_rom(kind, tab_T_degC=tabT, T_eval_degC=Tev))
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), rom_hash=hsh, kind=kind, tab_T_degC=tabT, T_eval_degC=Tev,
+                        soc0=soc0, tc=tc, status=np.array([one["status"][-1]]),
+                        **{k: one[k][:, None] for k in keys}, **env)
+    for name, kind, tabT, Tev, soc0, tc, steps in cases[1:]:
+        o, outs = outs[:soc0.size], outs[soc0.size:]
+        r = {k: np.stack([x[k] for x in o], axis=1) for k in keys}
+        r["status"] = np.array([x["status"][-1] for x in o])
+        hsh = rom_hash(R.make_tab_rom(kind, tab_T_degC=tabT, T_eval_degC=Tev))
+        np.savez_compressed(os.path.join(OUT, name + ".npz"), rom_hash=hsh, kind=kind, tab_T_degC=tabT,
+                            T_eval_degC=Tev, soc0=soc0, tc=tc, **r)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
+    if "--tab-only" in sys.argv:
+        t0 = time.time()
+        make_tab_handles()
+        print(f"lookup-table handle fixtures written in {time.time() - t0:.0f} s")
+        return
     if "--handles-only" in sys.argv:
         t0 = time.time()
         make_handles()
