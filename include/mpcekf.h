@@ -241,11 +241,13 @@ int mpcekf_cl_eig(int32_t n, const double *a, double *re, double *im, double *sv
  * per chunk, MPCEKF_COPY_THREADS workers).
  * The temperature argument (Tc of OB_step.m:1, Tk of iterEKF.m:30 / EKFmatsHandler.m:1,
  * degC, [ncells]) sets each cell's temperature for this and later calls; NULL keeps it. */
-/* OB_step: applies iapp[c] to the plant state at tc_degC[c], returns vcell[c]. */
+/* OB_step: applies iapp[c] to the plant state at tc_degC[c], returns vcell[c] (may be NULL:
+ * Vcell also stays on the device for the next mpcekf_ekf_step with vk = NULL). */
 int mpcekf_plant_step(mpcekf_ctx *ctx, const double *iapp, const double *tc_degC, double *vcell);
 /* iterEKF: zk/boundzk [ncells][nz+2], xind_model [ncells][4] (model index t*nZ+z of
  * Xind.theT/theZ), xind_gamma [ncells][4].  Every output may be NULL: zk and Xind also stay
- * on the device for the next mpcekf_linearize (runMPC.m:91 -> :94 without a host round trip). */
+ * on the device for the next mpcekf_linearize (runMPC.m:91 -> :94 without a host round trip).
+ * vk = NULL: the last mpcekf_plant_step's Vcell on the device (MPCEKF_E_STATE without one). */
 int mpcekf_ekf_step(mpcekf_ctx *ctx, const double *vk, const double *ik, const double *tk_degC, double *zk,
                     double *boundzk, int32_t *xind_model, double *xind_gamma);
 /* EKFmatsHandler: lin [ncells][MPCEKF_LIN_SIZE], or NULL (the record stays on the device for
@@ -261,7 +263,8 @@ int mpcekf_linearize(mpcekf_ctx *ctx, const double *zk, const int32_t *xind_mode
 int mpcekf_lin_fields(mpcekf_ctx *ctx, const int32_t *slots, int32_t nslots, const double *set, double *out);
 /* iterMPC (uses and updates the context's uk_1 and lambda warm start):
  * soc_k1 = mpcData.SOCk_1 per cell; outputs uk, nexec.  lin = NULL: the device-resident
- * record of the last mpcekf_linearize. */
+ * record of the last mpcekf_linearize; soc_k1 = NULL: zk(end) of the last mpcekf_ekf_step on
+ * the device (runMPC.m:99's mpcData.SOCk_1 = zk(end)). */
 int mpcekf_mpc_step(mpcekf_ctx *ctx, const double *lin, const double *soc_k1, double *uk, int32_t *nexec);
 /* The same, also returning this call's iterMPC.m:89-95 cost log (mpcData.cost.J_uncon,
  * J_final, norm_DU, viol) per cell; any of the four may be NULL. */

@@ -158,12 +158,14 @@ struct Copier {
   }
 };
 
-int copy_threads() {  // MPCEKF_COPY_THREADS, else half the CPUs this process may use, 1..8
+// MPCEKF_COPY_THREADS, else the CPUs this process may use, 1..16 (the workers sleep on their
+// events; at 65,536 cells 16 beat 8 by 15 % on the drop-in route, profiles/r06b_*)
+int copy_threads() {
   if (const char *e = std::getenv("MPCEKF_COPY_THREADS")) return std::max(0, std::min(64, std::atoi(e)));
   cpu_set_t set;
   int n = 8;
-  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set) / 2;
-  return std::max(1, std::min(8, n));
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  return std::max(1, std::min(16, n));
 }
 
 }  // namespace
@@ -224,9 +226,9 @@ struct mpcekf_ctx {
   size_t h_bytes = 0, bounce_max = (size_t)256 << 20;
   // round 6: the buffer is bump-allocated over the calls up to the next synchronisation
   // (xoff), so _async calls keep their regions until their copies finish; outputs leave it
-  // in chunks of xchunk bytes (MPCEKF_CHUNK, default 4 MiB), one event each (xev, reused
+  // in chunks of xchunk bytes (MPCEKF_CHUNK, default 1 MiB), one event each (xev, reused
   // after the synchronisation), copied out by the worker pool `copier`
-  size_t xoff = 0, xchunk = (size_t)4 << 20;
+  size_t xoff = 0, xchunk = (size_t)1 << 20, xhwm = 0;
   std::vector<hipEvent_t> xev;
   size_t xev_used = 0;
   bool xpending = false;
@@ -301,11 +303,17 @@ struct mpcekf_ctx {
   // the last mpcekf_ekf_step's zk and Xind, the last mpcekf_linearize's records, so the next
   // stage call can take NULL for them instead of a host round trip (valid until a fused step,
   // set_state or init_cells; stage_zk / stage_lin say which are current)
-  double *d_szk = nullptr, *d_sxg = nullptr, *d_slin = nullptr;
-  int *d_sxm = nullptr;
-  bool stage_zk = false, stage_lin = false;
+  double *d_szk = nullptr, *d_sxg = nullptr, *d_slin = nullptr, *d_sv = nullptr;
+  int *d_sxm = nullptr, *d_zslot = nullptr;  // d_zslot: zk(end)'s slot, nz + 1 (mpc_step's NULL soc_k1)
+  bool stage_zk = false, stage_lin = false, stage_v = false;
   int stage_bufs() {
     const size_t nzz = (size_t)nz + 2;
+    if (!d_sv) HIPCHK(hipMalloc((void **)&d_sv, (size_t)n * sizeof(double)));
+    if (!d_zslot) {
+      const int zs = nz + 1;
+      HIPCHK(hipMalloc((void **)&d_zslot, sizeof(int)));
+      HIPCHK(hipMemcpy(d_zslot, &zs, sizeof(int), hipMemcpyHostToDevice));
+    }
     if (!d_szk) HIPCHK(hipMalloc((void **)&d_szk, (size_t)n * nzz * sizeof(double)));
     if (!d_sxg) HIPCHK(hipMalloc((void **)&d_sxg, (size_t)n * 4 * sizeof(double)));
     if (!d_sxm) HIPCHK(hipMalloc((void **)&d_sxm, (size_t)n * 4 * sizeof(int)));
@@ -322,11 +330,16 @@ struct mpcekf_ctx {
   // allocation is not an error: the buffer stays empty and every copy goes direct (Xfer::fits).
   int bounce(size_t bytes) {
     if (xoff + bytes <= h_bytes) return MPCEKF_OK;
+    // grown to the largest epoch seen (a step's _async calls together), so a steady
+    // sequence of calls between synchronisations never drains early
+    const size_t want = std::max(xoff + bytes, xhwm);
+    xhwm = want;
     if (xpending || xoff) {
       int rc = drain();
       if (rc) return rc;
-      if (bytes <= h_bytes) return MPCEKF_OK;
     }
+    bytes = want;
+    if (bytes <= h_bytes) return MPCEKF_OK;
     if (h_bounce) (void)hipHostFree(h_bounce);
     h_bounce = nullptr;
     h_bytes = 0;
@@ -947,7 +960,7 @@ int mpcekf_ctx_destroy(mpcekf_ctx *X) {
   void *ptrs[] = {X->d_prob, X->d_cell_blob, X->d_plant_blob, X->d_bulk, X->d_const, X->d_scal, X->d_int, X->d_zk,
                   X->d_zbk,       X->d_tmp,        X->s.bigx, X->s.ekf,   X->s.lam,   X->d_ts, X->d_hist, X->d_stamps, X->d_bnd, X->d_xm, X->d_xg,
                   X->w.prob, X->w.X, X->w.R, X->w.K, X->w.hii, X->w.it, X->w.smin, X->d_lin, X->d_zsoc, X->d_mb, X->d_uk1p,
-                  X->w.q, X->w.list, X->w.hist, X->d_poly, X->d_szk, X->d_sxg, X->d_sxm, X->d_slin};
+                  X->w.q, X->w.list, X->w.hist, X->d_poly, X->d_szk, X->d_sxg, X->d_sxm, X->d_slin, X->d_sv, X->d_zslot};
   for (void *p : ptrs)
     if (p) (void)hipFree(p);
   for (auto &g : X->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -1000,7 +1013,7 @@ static int set_tc(mpcekf_ctx *X, const double *tc, struct Xfer *xf = nullptr);
 
 // initKF.m:30-136, initMPC.m:29-74 and OB_step.m:39-72 for every cell.
 int mpcekf_init_cells(mpcekf_ctx *X, const double *soc0_pct, const double *tc_degC) {
-  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
+  if (X) X->stage_zk = X->stage_lin = X->stage_v = false;  // the stage route's device hand-offs are stale
   if (!X || ((!soc0_pct || !tc_degC) && X->n)) return fail(MPCEKF_E_ARG, "init_cells: null argument");
   HIPCHK(hipSetDevice(X->device));
   const size_t n = (size_t)X->n;
@@ -1054,7 +1067,7 @@ static int lerr(int rc, const char *what) {
 // update) -> iterEKF measurement update -> EKFmatsHandler -> iterMPC.
 int mpcekf_step_ex(mpcekf_ctx *X, int32_t nsteps, const double *tc_degC, const mpcekf_traj *tr,
                    int32_t outputs_on_device) {
-  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
+  if (X) X->stage_zk = X->stage_lin = X->stage_v = false;  // the stage route's device hand-offs are stale
   int rc = need_init(X);
   if (rc) return rc;
   if (nsteps < 0) return fail(MPCEKF_E_ARG, "nsteps < 0");
@@ -1495,19 +1508,24 @@ extern "C" {
 static int plant_step_impl(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!iapp || !vcell) return fail(MPCEKF_E_ARG, "plant_step: null argument");
+  if (!iapp) return fail(MPCEKF_E_ARG, "plant_step: null argument");
   size_t n = (size_t)X->n;
   Xfer xf{X};
   if ((rc = xf.reserve({n * 8, n * 8, n * 8}))) return rc;
   if ((rc = set_tc(X, tc_degC, &xf))) return rc;
-  if ((rc = X->tmp(2 * n * 8 + 512))) return rc;
+  if ((rc = X->tmp(2 * n * 8 + 512)) || (rc = X->stage_bufs())) return rc;
   Slab sl{(char *)X->d_tmp};
-  double *di = sl.take<double>(n), *dv = sl.take<double>(n);
+  // Vcell also stays on the device for the next mpcekf_ekf_step (vk = NULL there: runMPC.m:88
+  // -> :91 without a host round trip, which an _async plant call needs); vcell may be NULL
+  double *di = sl.take<double>(n), *dv = X->d_sv;
+  X->stage_v = false;
   HIPCHK(xf.in(di, iapp, n * 8));
   if ((rc = lerr(launch_plant(X->r, X->s, di, dv, 0, nullptr, X->stream), "plant"))) return rc;
   if ((rc = lerr(launch_bulk(X->r, X->k, X->s, di, 1, 0, X->stream), "bulk"))) return rc;
-  HIPCHK(xf.out(vcell, dv, n * 8));
-  return xf.end(async);
+  if (vcell) HIPCHK(xf.out(vcell, dv, n * 8));
+  if ((rc = xf.end(async))) return rc;
+  X->stage_v = true;
+  return MPCEKF_OK;
 }
 int mpcekf_plant_step(mpcekf_ctx *X, const double *iapp, const double *tc_degC, double *vcell) {
   return plant_step_impl(X, iapp, tc_degC, vcell, false);
@@ -1520,7 +1538,8 @@ static int ekf_step_impl(mpcekf_ctx *X, const double *vk, const double *ik, cons
                     double *boundzk, int32_t *xind_model, double *xind_gamma, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!vk || !ik) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
+  if (!ik) return fail(MPCEKF_E_ARG, "ekf_step: null argument");
+  if (!vk && !X->stage_v) return fail(MPCEKF_E_STATE, "ekf_step: NULL vk but no mpcekf_plant_step before it");
   size_t n = (size_t)X->n, nzz = (size_t)X->nz + 2;
   Xfer xf{X};
   if ((rc = xf.reserve({n * 8, n * 8, n * 8, n * nzz * 8, n * nzz * 8, 16 * n, 32 * n})))
@@ -1534,7 +1553,8 @@ static int ekf_step_impl(mpcekf_ctx *X, const double *vk, const double *ik, cons
   double *dzk = X->d_szk, *dxg = X->d_sxg;
   int *dxm = X->d_sxm;
   X->stage_zk = X->stage_lin = false;
-  HIPCHK(xf.in(dvk, vk, n * 8));
+  if (vk) HIPCHK(xf.in(dvk, vk, n * 8));
+  else dvk = X->d_sv;  // the last mpcekf_plant_step's Vcell, on the device
   HIPCHK(xf.in(dik, ik, n * 8));
   // iterEKF.m:55 lock-out must see the state before the time update: the bulk
   // update of a locked-out cell is harmless because the cell is stopped.
@@ -1666,8 +1686,9 @@ static int mpc_step_ex_impl(mpcekf_ctx *X, const double *lin, const double *soc_
                        double *J_unc, double *J_fin, double *norm_du, int32_t *nviol, bool async) {
   int rc = need_init(X);
   if (rc) return rc;
-  if (!soc_k1 || !uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
+  if (!uk) return fail(MPCEKF_E_ARG, "mpc_step: null argument");
   if (!lin && !X->stage_lin) return fail(MPCEKF_E_STATE, "mpc_step: NULL lin but no mpcekf_linearize record");
+  if (!soc_k1 && !X->stage_zk) return fail(MPCEKF_E_STATE, "mpc_step: NULL soc_k1 but no mpcekf_ekf_step zk");
   size_t n = (size_t)X->n;
   if ((rc = X->tmp((n * MPCEKF_LIN_SIZE + 5 * n) * 8 + 2 * n * 4 + 4096))) return rc;
   Slab sl{(char *)X->d_tmp};
@@ -1678,7 +1699,9 @@ static int mpc_step_ex_impl(mpcekf_ctx *X, const double *lin, const double *soc_
   if ((rc = xf.reserve({n * MPCEKF_LIN_SIZE * 8, n * 8, n * 8, n * 8, n * 8, n * 8, n * 4, n * 4}))) return rc;
   if (lin) HIPCHK(xf.in(dl, lin, n * MPCEKF_LIN_SIZE * 8));
   else dl = X->d_slin;  // the device-resident record of the last mpcekf_linearize
-  HIPCHK(xf.in(ds, soc_k1, n * 8));
+  if (soc_k1) HIPCHK(xf.in(ds, soc_k1, n * 8));
+  else if ((rc = lerr(launch_cols(X->d_szk, X->n, X->nz + 2, X->d_zslot, 1, ds, false, X->stream), "cols")))
+    return rc;  // runMPC.m:99 mpcData.SOCk_1 = zk(end), from the last mpcekf_ekf_step's device zk
   KIO io{};
   io.mode = MODE_MPC;
   io.lin_in = dl;
@@ -1972,7 +1995,7 @@ int mpcekf_get_scalars_async(mpcekf_ctx *X, const int32_t *slots, int32_t nslots
 }
 
 int mpcekf_set_state(mpcekf_ctx *X, const mpcekf_state *st) {
-  if (X) X->stage_zk = X->stage_lin = false;  // the stage route's device hand-offs are stale
+  if (X) X->stage_zk = X->stage_lin = X->stage_v = false;  // the stage route's device hand-offs are stale
   int rc = need_init(X);
   if (rc) return rc;
   if (!st) return fail(MPCEKF_E_ARG, "set_state: null");

@@ -1083,12 +1083,12 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
       double hii = 0.0;
 #pragma unroll
       for (int k = 0; k < NC; ++k) hii = hii + Mf(i, k) * X[i][k];
-      double s = 0.0, w;
+      double s = 0.0, nl, d;
       if (fin) {
         double t = K[i];
 #pragma unroll
         for (int k = 0; k < NC; ++k) t = __builtin_fma(Mf(i, k), v[k], t);
-        w = hild_w(t, hii, 1.0 / hii, lam[i]);
+        d = hild_step(t, hii, 1.0 / hii, lam[i], nl);
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1099,10 +1099,10 @@ __device__ __forceinline__ int hildreth_core(const MV &Mf, const double E[NC][NC
           p4[j & 3] = p4[j & 3] + h * lam[j];
         }
         s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-        w = -((K[i] + s) - hii * lam[i]) / hii;
+        const double w = -((K[i] + s) - hii * lam[i]) / hii;
+        nl = w > 0 ? w : 0.0;
+        d = nl - lam[i];
       }
-      double nl = w > 0 ? w : 0.0;
-      double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = false;
       lam[i] = nl;
       if (fin) {
@@ -1202,7 +1202,7 @@ __device__ __forceinline__ void hild_x(const Cons &Cn, const double E[NC][NC], X
 // [Cu; -Cu; I; -I] are +-a, +-b, +-c) and the 18 distinct (H_ii, 1/H_ii) pairs (H_ii of
 // a negated row is bit-identical: (-1)(-x) = x, and its 0 * (-x) term only meets
 // a nonzero sum or +0).  Layout [slot][64 lanes] double2: every read is one
-// conflict-free ds_read_b128 per wave.  1/H_ii is the correctly rounded reciprocal of hild_w.
+// conflict-free ds_read_b128 per wave.  1/H_ii is the correctly rounded reciprocal of hild_step.
 constexpr int HS_X = 3 + 3 * NP, HS_SLOTS = 2 * HS_X;
 constexpr int HILD_LDS_PER_WAVE = HS_SLOTS * 64 * 16;  // bytes
 __device__ __forceinline__ constexpr int hslot(int i) {
@@ -1210,8 +1210,8 @@ __device__ __forceinline__ constexpr int hslot(int i) {
 }
 __device__ __forceinline__ constexpr bool hneg(int i) { return i == 2 || i == 3 || i == 6 || i == 7; }
 // The first row of each Toeplitz block is (H(0), 0): all zero when H(0) = 0, as for the
-// SOC block (predMat: G(1,1) = +0), so its H_ii may be 0; 1/H_ii is then +-inf and hild_w's
-// fma gives x / +-0's inf / NaN by IEEE without a select.
+// SOC block (predMat: G(1,1) = +0), so its H_ii may be 0; 1/H_ii is then +-inf and hild_step's
+// product gives x / +-0's inf / NaN by IEEE without a select.
 __device__ __forceinline__ double2 hx(const double2 *hl, int i) {  // X(:,i)
   const double2 x = hl[hslot(i) * 64];
   return hneg(i) ? make_double2(-x.x, -x.y) : x;
@@ -1222,8 +1222,8 @@ __device__ __forceinline__ double2 hh(const double2 *hl, int i) {  // (H_ii, 1/H
 __device__ __forceinline__ double2 *hild_lane_lds(double2 *base) {  // blocks of 256 threads
   return base + (threadIdx.x >> 6) * (HS_SLOTS * 64) + (threadIdx.x & 63);
 }
-// Fills the lane's slots; returns whether every H_ii is in hild_w's reciprocal domain
-// (hild_rok: 0 or [2^-1020, 2^1020]), where a row is the single fma(-t, 1/H_ii, lambda_i).
+// Fills the lane's slots; returns whether every H_ii is in hild_step's reciprocal domain
+// (hild_rok: 0 or [2^-1020, 2^1020]), where a row is min(t (1/H_ii), lambda_i).
 __device__ __forceinline__ bool hild_stage(const Cons &Cn, const XS &Xs, double2 *hl) {
   ConsM Mf{Cn};
   bool yok = true;
@@ -1255,13 +1255,14 @@ __device__ __forceinline__ void hild_unstage(const double2 *hl, XS &Xs) {
 
 // One rank-2 sweep (orc_hildreth, finite X and M): v = X*lambda from +0 at the sweep
 // start (fma, ascending j), t_i = fma(M_i1, v1, fma(M_i0, v0, K_i)),
-// w = fma(-t_i, 1/H_ii, lambda_i) (hild_w with every H_ii in its domain and lambda finite),
-// lambda_i = max(w, 0), v += X(:,i) * d by fma.  A row's dependent chain is t (2 fma) ->
-// w -> max -> d -> v: 6 operations (10 with round 5's division).
+// m = min(t_i (1/H_ii), lambda_i), d = -m, lambda_i -= m (hild_step with every H_ii in its
+// domain and lambda finite), v += X(:,i) * d by fma.  A row's dependent chain is t (2 fma) ->
+// q -> min -> v: 5 operations (10 with round 5's division); the new lambda_i is beside it and
+// can take lambda_i's register (no rotation of the 23 lambdas at the sweep's end).
 // The fast form: straight line, no frozen lanes (the caller keeps a converged lane's
 // lambda aside).  It reports max |d| (the reference's inf-norm test, hildreth.m:39) and
 // whether v ended finite (false once any d was not finite: inf and NaN stay in v; every
-// lambda was finite until then, so each row was hild_w's fma form).
+// lambda was finite until then, so each row was hild_step's reciprocal form).
 // The constant rows 0-7 ([Cu; -Cu; I; -I]) use 3 of the 18 slots (X: +-a, +-b, +-c; their
 // (H_ii, 1/H_ii)): those 6 pairs are held in registers (xr3 / hr3, read back from the
 // lane's LDS slots once per solve), so a sweep reads LDS for the 15 Toeplitz rows only.
@@ -1337,13 +1338,12 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     double t = K[i];
     if (!mzero(i, 0)) t = __builtin_fma(Mf(i, 0), v0, t);
     if (!mzero(i, 1)) t = __builtin_fma(Mf(i, 1), v1, t);
-    const double w = __builtin_fma(-t, hc.y, L[i]);
-    const double nl = w > 0 ? w : 0.0;
-    const double d = nl - L[i];
-    dmax = fmax(dmax, fabs(d));
+    const double m = fmin(t * hc.y, L[i]);
+    const double nl = L[i] - m;
+    dmax = fmax(dmax, fabs(m));
     L[i] = nl;
-    v0 = __builtin_fma(xc.x, d, v0);
-    v1 = __builtin_fma(xc.y, d, v1);
+    v0 = __builtin_fma(-xc.x, m, v0);   // fma(x, d, v) with d = -m: the same value
+    v1 = __builtin_fma(-xc.y, m, v1);
     if (MPCEKF_HILD_NEXTV) {
       u0 = __builtin_fma(xc.x, nl, u0);
       u1 = __builtin_fma(xc.y, nl, u1);
@@ -1380,11 +1380,11 @@ __device__ __forceinline__ void sweep_careful(const Cons &Cn, const double2 *hl,
     double t = __builtin_fma(Mf(i, 0), v0, K[i]);
     t = __builtin_fma(Mf(i, 1), v1, t);
     const double li = L[i];
-    const double w = hild_w(t, hr.x, hr.y, li);
-    const double nl = w > 0 ? w : 0.0;
-    if (!(fabs(nl - li) < tol)) conv = false;
+    double nl;
+    const double ds = hild_step(t, hr.x, hr.y, li, nl);
+    if (!(fabs(ds) < tol)) conv = false;
     const double nli = done ? li : nl;
-    const double d = nli - li;
+    const double d = done ? 0.0 : ds;
     L[i] = nli;
     if (!isfinite(d)) {
       xv(v0, v1);
@@ -1426,7 +1426,7 @@ __device__ __forceinline__ void sweep_dense(const Cons &Cn, const XS &Xs, const 
 // nothing kept).  hl = the lane's LDS slots (HILD_LDS_PER_WAVE per wave).
 //
 // hild_fast (k_hild): the fast rank-2 sweep for lanes with finite X, M, every H_ii in
-// hild_w's reciprocal domain and a finite warm start.  Lanes keep sweeping after they
+// hild_step's reciprocal domain and a finite warm start.  Lanes keep sweeping after they
 // converge; the lambda they converged with goes to L0 (their warm start is no longer
 // needed) and comes back after the loop.  A lane whose sweep ends with a non-finite v,
 // and every lane outside the fast form's
@@ -3958,10 +3958,10 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
     if (fin) xv();
     for (int i = 0; i < nC; ++i) {
       const double hii = Hd[i];
-      double w;
+      double nl, d;
       if (fin) {
         const double t = row_t_rt(Nc, M + i * Nc, v, K[i]);
-        w = hild_w(t, hii, 1.0 / hii, lam[i]);
+        d = hild_step(t, hii, 1.0 / hii, lam[i], nl);
       } else {
         double p4[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = 0; j < nC; ++j) {
@@ -3970,10 +3970,10 @@ __global__ void __launch_bounds__(64) k_hildreth_any(int64_t n, int Nc, int nC, 
           p4[j & 3] = p4[j & 3] + h * lam[j];
         }
         const double s = (p4[0] + p4[1]) + (p4[2] + p4[3]);
-        w = -((K[i] + s) - hii * lam[i]) / hii;
+        const double w = -((K[i] + s) - hii * lam[i]) / hii;
+        nl = w > 0 ? w : 0.0;
+        d = nl - lam[i];
       }
-      const double nl = w > 0 ? w : 0.0;
-      const double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = false;
       lam[i] = nl;
       if (fin) {

@@ -23,18 +23,26 @@ namespace mk {
 // live registers.
 __device__ __forceinline__ void launder(double &x) { asm volatile("" : "+v"(x)); }
 
-// hildreth.m:35's update, w = -(K_i + H(i,:)*lambda - H_ii lambda_i) / H_ii with
-// t_i = K_i + H(i,:)*lambda, spelled as oracle/mpcekf_oracle.c hild_w (round 6):
-// fma(-t_i, 1/H_ii, lambda_i) with the correctly rounded 1/H_ii formed once per solve, when
-// H_ii is 0 or in [2^-1020, 2^1020] (hild_rok) and lambda_i is finite; the division form
-// fma(H_ii, lambda_i, -t_i) / H_ii otherwise.  H_ii = +-0: 1/H_ii = +-inf, and the fma gives
-// x / +-0's inf / NaN by IEEE, as the division does.
+// hildreth.m:35-36's update as oracle/mpcekf_oracle.c hild_step defines it (round 6): the
+// step d = -min(t_i (1/H_ii), lambda_i) and lambda_i <- lambda_i - min(..), with the correctly
+// rounded 1/H_ii formed once per solve, when H_ii is 0 or in [2^-1020, 2^1020] (hild_rok) and
+// lambda_i is finite; the division form (w = fma(H_ii, lambda_i, -t_i) / H_ii, max(w, 0), the
+// difference) otherwise.  fmin is v_min_f64 (a NaN operand yields the other: a NaN q leaves
+// lambda_i = 0, as max(0, NaN) does); H_ii = +-0 gives 1/H_ii = +-inf, and t (+-inf) is x / +-0's
+// inf / NaN by IEEE.  Returns d; nl = the new lambda_i.
 __device__ __forceinline__ bool hild_rok(double h) {
   const double a = fabs(h);
   return h == 0.0 || (a >= 0x1p-1020 && a <= 0x1p1020);
 }
-__device__ __forceinline__ double hild_w(double t, double h, double rinv, double l) {
-  return (hild_rok(h) && isfinite(l)) ? __builtin_fma(-t, rinv, l) : __builtin_fma(h, l, -t) / h;
+__device__ __forceinline__ double hild_step(double t, double h, double rinv, double l, double &nl) {
+  if (hild_rok(h) && isfinite(l)) {
+    const double m = fmin(t * rinv, l);
+    nl = l - m;
+    return -m;
+  }
+  const double w = __builtin_fma(h, l, -t) / h;
+  nl = w > 0 ? w : 0.0;
+  return nl - l;
 }
 
 // predMat.m with A = diag(a), B = ones, evaluated on the structure of Abar:

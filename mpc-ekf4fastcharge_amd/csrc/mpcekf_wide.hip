@@ -602,8 +602,8 @@ __device__ __forceinline__ double row_term8(int i, int k, double v0, double v1, 
 }
 // The I / -I rows (one M entry, +-1 in column j): the tree of hild_row_t adds K_i and +-v_j
 // to zeros only, which is exact, so t = K_i +- v_j in one rounding (the sign of a zero t
-// aside, which cannot reach lambda: hild_w's fma(-t, 1/H_ii, lambda_i) is then lambda_i, +0
-// when lambda_i = +0, or NaN when 1/H_ii is infinite, for either sign).  v_j comes from lane j % 8 of the group (v0 for j < 8,
+// aside, which cannot reach lambda: min(t (1/H_ii), lambda_i) is then +-0 or lambda_i, so
+// lambda_i - min(..) and the step's effect on v are the same for either sign).  v_j comes from lane j % 8 of the group (v0 for j < 8,
 // v1 above) by bcast8; K_i is read in every lane.
 template <int NC>
 __device__ __forceinline__ constexpr bool unit_row(int i) {
@@ -733,7 +733,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       xb[k * NC + m] = x[m];
     }
     const int i = u < NC ? u : u < 2 * NC ? u + NC : u + 2 * NC;  // constraint row (+ NC: its negated copy)
-    ok = ok && hild_rok(h);                          // hild_w's fma form for every row
+    ok = ok && hild_rok(h);                          // hild_step's reciprocal form for every row
     const double2 hh = make_double2(h, 1.0 / h);     // the oracle's 1.0 / hii (IEEE)
     hr[i] = hh;
     if (u < 2 * NC) hr[i + NC] = hh;
@@ -865,18 +865,17 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       const double t = rowT(i, v0, v1, o.kz, o.m0, o.m1);
       const double li = o.li;
       const double2 h = o.h;
-      // w = lambda_i - t / H_ii as hild_w's fma(-t, 1/H_ii, lambda_i): every H_ii is in its
-      // domain (checked at the staging) and lambda_i finite while v is (a zero H(0) row's
-      // 1/H_ii = +-inf gives x / +-0 by IEEE)
-      const double wv = __builtin_fma(-t, h.y, li);
-      const double nl = wv > 0 ? wv : 0.0;
-      const double d = nl - li;
-      convm &= __ballot(fabs(d) < tol);
+      // hild_step's reciprocal form: m = min(t / H_ii, lambda_i) with t (1/H_ii), the step -m,
+      // lambda_i - m: every H_ii is in its domain (checked at the staging) and lambda_i finite
+      // while v is (a zero H(0) row's 1/H_ii = +-inf gives x / +-0 by IEEE)
+      const double m = fmin(t * h.y, li);
+      const double nl = li - m;
+      convm &= __ballot(fabs(m) < tol);
       lst[i] = nl;
       double x0, x1;
       xrow(i, x0, x1);
-      v0 = __builtin_fma(x0, d, v0);
-      v1 = __builtin_fma(x1, d, v1);
+      v0 = __builtin_fma(-x0, m, v0);   // fma(x, d, v) with the step d = -m
+      v1 = __builtin_fma(-x1, m, v1);
       u0 = __builtin_fma(x0, nl, u0);
       u1 = __builtin_fma(x1, nl, u1);
       // every accumulation finishes in its row: left alone, the compiler sank the ones not
@@ -1040,9 +1039,9 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
     for (int i = 0; i < NCON; ++i) {
       const double hii = w.hii[(size_t)c * NCON + i], Ki = w.K[(size_t)c * NCON + i];
       const double li = lam[(size_t)i * n + c];
-      double wv;
+      double nl, d;
       if (fin) {
-        wv = hild_w(row_t_rt<NP, NC>(Hall, i, v, Ki), hii, 1.0 / hii, li);
+        d = hild_step(row_t_rt<NP, NC>(Hall, i, v, Ki), hii, 1.0 / hii, li, nl);
       } else {  // dense H(i,:)*lambda, 4 interleaved partial sums (orc_hildreth)
         double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 1
@@ -1053,10 +1052,10 @@ __global__ void __launch_bounds__(64) k_hild_wide_slow(const KCfg cf, const KSta
           p[j & 3] = p[j & 3] + h * lam[(size_t)j * n + c];
         }
         const double sm = (p[0] + p[1]) + (p[2] + p[3]);
-        wv = -((Ki + sm) - hii * li) / hii;
+        const double wv = -((Ki + sm) - hii * li) / hii;
+        nl = wv > 0 ? wv : 0.0;
+        d = nl - li;
       }
-      const double nl = wv > 0 ? wv : 0.0;
-      const double d = nl - li;
       if (!(fabs(d) < tol)) conv = false;
       lam[(size_t)i * n + c] = nl;
       if (fin) {

@@ -368,8 +368,9 @@ class Context:
         """[zk, boundzk, ekfData, Xind] = iterEKF(vk, ik, Tk, ekfData)  (iterEKF.m:30).
 
         Xind is returned as dict(model=[n,4] model index t*nZ+z, theT, theZ, gamma);
-        xind=False: None (it stays on the device for EKFmatsHandler(None, None))."""
-        v = self._vec(vk)
+        xind=False: None (it stays on the device for EKFmatsHandler(None, None)).  vk = None:
+        the last OB_step's Vcell on the device (the asynchronous route's hand-off)."""
+        v = None if vk is None else self._vec(vk)
         i = self._vec(ik)
         t = self._tvec(Tk)
         zk = np.empty((self.n, self.nz + 2))
@@ -422,7 +423,7 @@ class Context:
         with cost=True also this call's mpcData.cost row (iterMPC.m:89-95) as a dict of
         J_uncon, J_final, norm_DU, viol, nexec per cell."""
         lin = None if lin is None else np.ascontiguousarray(lin, dtype=np.float64)   # None: the device record
-        s = self._vec(SOCk_1)
+        s = None if SOCk_1 is None else self._vec(SOCk_1)   # None: zk(end) of the last iterEKF, on the device
         uk = np.empty(self.n)
         ne = np.empty(self.n, dtype=np.int32)
         if not cost:

@@ -655,21 +655,32 @@ static double hild_row_t(int Nc, const double *Mi, const double *v, double Ki) {
   return b[0];
 }
 
-/* hildreth.m:35's update w = -(K_i + H(i,:)*lambda - H_ii lambda_i) / H_ii, with t_i =
- * K_i + H(i,:)*lambda: the defined spelling (round 6) is w = lambda_i - t_i / H_ii as one
- * fma with the reciprocal, fma(-t_i, 1/H_ii, lambda_i) -- 1/H_ii once per solve and row, so
- * the per-row chain is t -> w -> max -> d instead of t -> num -> divide (3 ops) -> max -> d.
- * Outside the reciprocal's normal range (|H_ii| not 0 and outside [2^-1020, 2^1020]: 1/H_ii
- * would overflow or lose bits) or with a non-finite lambda_i (an inf lambda_i with H_ii = 0
- * is NaN in MATLAB's H_ii * lambda_i term) the division form fma(H_ii, lambda_i, -t_i) / H_ii.
- * H_ii = +-0 (the SOC block's first row, predMat G(1,1) = 0): 1/H_ii = +-inf and
- * fma(-t, +-inf, lambda) is x / +-0's inf / NaN by IEEE, as the division form gives it. */
+/* hildreth.m:35-36's update, lambda_i <- max(0, w) with w = -(K_i + H(i,:)*lambda - H_ii lambda_i)
+ * / H_ii = lambda_i - t_i / H_ii (t_i = K_i + H(i,:)*lambda): the defined spelling (round 6)
+ * takes the step, not the new value, first -- d = max(-lambda_i, -t_i / H_ii) = -min(q, lambda_i)
+ * with q = t_i * (1/H_ii) (1/H_ii once per solve and row), lambda_i <- lambda_i - min(q,
+ * lambda_i).  So the per-row chain is t -> q -> min -> (v += X(:,i) d), the new lambda_i
+ * beside it, and an inactive row (q >= lambda_i) lands on +0 exactly.  fmin(NaN, l) = l: a NaN
+ * q leaves lambda_i = 0, as max(0, NaN) = 0 does.  The step d = -min(q, lambda_i) is what v is
+ * updated with and what the stop test (hildreth.m:39) measures.  Outside the reciprocal's
+ * normal range (|H_ii| not 0 and outside [2^-1020, 2^1020]) or with a non-finite lambda_i (an
+ * inf lambda_i with H_ii = 0 is NaN in MATLAB's H_ii * lambda_i term): the division form,
+ * w = fma(H_ii, lambda_i, -t_i) / H_ii, new = max(w, 0), d = new - lambda_i.  H_ii = +-0 (the
+ * SOC block's first row, predMat G(1,1) = 0): 1/H_ii = +-inf, and q = t * (+-inf) gives x / +-0's
+ * inf / NaN by IEEE, as the division does.  Returns d; *nl = the new lambda_i. */
 static int hild_rok(double h) {
   const double a = fabs(h);
   return h == 0.0 || (a >= 0x1p-1020 && a <= 0x1p1020);
 }
-static double hild_w(double t, double h, double rinv, double l) {
-  return (hild_rok(h) && isfinite(l)) ? fma(-t, rinv, l) : fma(h, l, -t) / h;
+static double hild_step(double t, double h, double rinv, double l, double *nl) {
+  if (hild_rok(h) && isfinite(l)) {
+    const double m = fmin(t * rinv, l);
+    *nl = l - m;
+    return -m;
+  }
+  const double w = fma(h, l, -t) / h;
+  *nl = w > 0 ? w : 0.0;
+  return *nl - l;
 }
 
 int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double *M /*nC x Nc*/,
@@ -697,7 +708,7 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
    * Defined evaluation (the kernels evaluate the same sequence):
    *  - finite X and M: v recomputed from lambda at the start of every sweep (fma
    *    accumulation from +0 in ascending j), t_i = K_i + M(i,:)*v as hild_row_t,
-   *    w = hild_w(t_i, H_ii, 1/H_ii, lambda_i) (= -(K_i + s_i - H_ii lambda_i) / H_ii), and
+   *    the step d and new lambda_i by hild_step (lambda_i - t_i / H_ii clamped at 0), and
    *    after row i v += X(:,i)*(new - old lambda(i)) by fma; when that change is not
    *    finite (a zero-diagonal row going to or from +inf) v is recomputed from lambda
    *    instead, which reproduces the dense form's inf/NaN propagation in kind.
@@ -712,18 +723,18 @@ int orc_hildreth(int Nc, int nC, const double *E, const double *F, const double 
     double v[NCMAX];
     if (finite) hild_v(Nc, nC, X, lam, v);
     for (int i = 0; i < nC; ++i) {
-      double w, hii = H[i * HMAX + i];
+      double nl, d, hii = H[i * HMAX + i];
       if (finite) {
         double t = hild_row_t(Nc, M + i * Nc, v, K[i]);
-        w = hild_w(t, hii, 1.0 / hii, lam[i]);
+        d = hild_step(t, hii, 1.0 / hii, lam[i], &nl);
       } else {
         double p[4] = {0.0, 0.0, 0.0, 0.0};
         for (int j = 0; j < nC; ++j) p[j & 3] = p[j & 3] + H[i * HMAX + j] * lam[j];
         double s = (p[0] + p[1]) + (p[2] + p[3]);
-        w = -((K[i] + s) - hii * lam[i]) / hii;
+        const double w = -((K[i] + s) - hii * lam[i]) / hii;
+        nl = w > 0 ? w : 0.0;
+        d = nl - lam[i];
       }
-      double nl = w > 0 ? w : 0.0;
-      double d = nl - lam[i];
       if (!(fabs(d) < tol)) conv = 0;
       lam[i] = nl;
       if (finite) {

@@ -163,7 +163,8 @@ def stable_two_nearest(d):
 class Cell:
     """Reads the ROM *data*; re-implements the tabulated handle semantics itself
     (include/mpcekf.h mpcekf_electrode): [ntemp, ntheta] tables, theta interpolated
-    on a uniform [0, 1] grid (linearly, or by the v3 piecewise polynomials), then T linearly
+    on a uniform [0, 1] grid (linearly, or by the v3 piecewise polynomials) or, for a
+    function with ABI v4 nodes, by its polynomials on its own theta nodes; then T linearly
     between the two bracketing grid rows, then the v3 Arrhenius factor.
 
     ``handles=True``: calls the ROM's closed-form ``cellData.function`` handles
@@ -216,13 +217,36 @@ class Cell:
             v = float(c[k] + s * v)
         return v
 
+    @staticmethod
+    def _node(x, coef, th):
+        """ABI v4 row (include/mpcekf.h mpcekf_electrode.nnode): the polynomial of segment k on
+        the function's own nodes x [m], k the last of 0..m-2 with k = 0 or x_k <= theta
+        (theta clamped to [0, 1]; a linear scan here, the C oracle bisects), s = theta - x_k."""
+        if th != th:
+            return NAN
+        xc = min(max(th, 0.0), 1.0)
+        k = 0
+        while k + 1 <= len(x) - 2 and x[k + 1] <= xc:
+            k += 1
+        s = xc - float(x[k])
+        c = coef[k]
+        v = float(c[-1])
+        for q in range(len(c) - 2, -1, -1):
+            v = float(c[q] + s * v)
+        return v
+
     def _fn(self, s, name, th, T):
-        """One v3 lookup: rows (polynomial or linear) bilinear in T, times the Arrhenius factor."""
+        """One v3 lookup: rows (polynomial or linear) bilinear in T, times the Arrhenius factor.
+        A function with v4 nodes uses its own node polynomials for the rows instead."""
         e = self.e[s]
-        coef = e.poly.get(name) if e.poly else None
+        nd = e.nodes.get(name) if getattr(e, "nodes", None) else None
+        coef = nd[1] if nd is not None else (e.poly.get(name) if e.poly else None)
         tab = getattr(e, name)
         j, g = self._tj(T)
-        row = (lambda k: self._interp(tab[k], th)) if coef is None else (lambda k: self._poly(coef[k], th))
+        if nd is not None:
+            row = lambda k: self._node(nd[0], coef[k], th)
+        else:
+            row = (lambda k: self._interp(tab[k], th)) if coef is None else (lambda k: self._poly(coef[k], th))
         one = coef is not None and all(np.array_equal(coef[0], coef[k]) for k in range(1, len(coef)))
         v = row(0 if one else j)               # T-invariant rows: row 0, no blend
         if len(self.TK) > 1 and not one:
@@ -260,6 +284,8 @@ class Cell:
             return self.h[s].Uocp(th, T)
         if T is None:                                  # one-argument call (EKFmatsHandler.m:96)
             e = self.e[s]
+            if getattr(e, "nodes", None) and "Uocp1" in e.nodes:
+                return self._node(*e.nodes["Uocp1"], th)
             return self._poly(e.poly["Uocp1"], th) if e.poly else self._interp(e.Uocp1, th)
         return self._fn(s, "Uocp", th, T)
 

@@ -152,3 +152,54 @@ def test_bounce_buffer_and_direct_copies_agree(P, M):
     for a, b in zip(res[0], res[1]):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.parametrize("chunk", [None, "65536"])
+def test_async_stage_route_equals_fused(P, M, monkeypatch, chunk):
+    """The _async stage twins, every call of a step enqueued without a
+    synchronisation until after iterMPC (mpcekf_sync): each step's outputs -- plant V,
+    zk / boundzk, the scalars, lin_fields, poles / sv, uk and the cost log -- are the bits of
+    the synchronous route, and uk is the fused step's.  chunk = 64 KiB splits every output
+    into many chunks (the worker pool's in-order and out-of-order completions)."""
+    if chunk:
+        monkeypatch.setenv("MPCEKF_CHUNK", chunk)
+    rom = P.make_synth_rom(lookup="quintic")
+    n, steps = 4096, 12
+    soc0, tc = batch_inputs(n, seed=101)
+    fused = M.runMPC(rom, soc0, tc, steps)
+    with M.Context(rom, n, M.make_config(bounds=True)) as a, M.Context(rom, n, M.make_config(bounds=True)) as s:
+        for c in (a, s):
+            c.init_cells(soc0, tc)
+        a.asynchronous = True
+        ua = np.zeros(n)
+        us = np.zeros(n)
+        for k in range(steps):
+            outs = []
+            for c, u in ((a, ua), (s, us)):
+                r = {}
+                r["sc0"] = c.get_scalars(("SOCnAvg", "SOCpAvg"))
+                r["v"] = c.OB_step(u, tc)
+                # the async context hands Vcell over on the device (vk = None): its host V is
+                # written only at the synchronisation
+                r["zk"], r["zb"], _ = c.iterEKF(None if c is a else r["v"], u, tc, xind=False)
+                r["sc1"] = c.get_scalars(("x0", "SigmaX0", "priorI"), flags=True)
+                c.EKFmatsHandler(None, None, tc, keep=True)
+                r["f"] = c.lin_fields(SLOTS)
+                r["p"], r["sv"] = c.mpc_diag(None)
+                outs.append(r)
+            a.asynchronous = False
+            ua, nea, ca = a.iterMPC(None, None, cost=True)   # synchronous: completes all; SOCk_1 = device zk(end)
+            a.asynchronous = True
+            us, nes, cs = s.iterMPC(None, outs[1]["zk"][:, -1], cost=True)
+            ra, rs = outs
+            for key in ("v", "zk", "zb", "f", "sv"):
+                np.testing.assert_array_equal(ra[key], rs[key], err_msg=f"step {k} {key}")
+            np.testing.assert_array_equal(ra["p"][..., 0] + 1j * ra["p"][..., 1], rs["p"])
+            for key in ("sc0", "sc1"):
+                for nm in rs[key]:
+                    np.testing.assert_array_equal(ra[key][nm], rs[key][nm], err_msg=f"step {k} {key} {nm}")
+            np.testing.assert_array_equal(ua, us)
+            np.testing.assert_array_equal(nea, nes)
+            for key in cs:
+                np.testing.assert_array_equal(np.asarray(ca[key]), np.asarray(cs[key]))
+            np.testing.assert_array_equal(ua, fused["u"][k])

@@ -201,15 +201,19 @@ def test_c_oracle_v4_follows_the_tab_runmpc_fixture(R, oc):
 @pytest.mark.parametrize("name", ["tab_batch8_1000", "pchip_batch8_300"])
 def test_v3_quintic_tables_miss_the_tab_fixtures(R, oc, name):
     """The same cells on v3 uniform quintics (513 theta, forced past the budget): off the
-    handles' trajectories by far more than 1e-6 -- what the node tables fix."""
+    handles' trajectories by more than north_star's 1e-6 (interp1-linear: 3.5e-5 on phise;
+    pchip, C1 so closer: 2e-6 on soc) -- what the node tables fix (1e-14 on the same cells)."""
     g = golden(name)
     rom = R.make_tab_rom(str(g["kind"]), tab_T_degC=tuple(g["tab_T_degC"]), T_eval_degC=tuple(g["T_eval_degC"]),
                          nodes=False, ntheta=513, strict=False)
     assert not rom.neg.nodes and not rom.pos.nodes
     n = min(300, g["u"].shape[0])
     out = oc.run(rom, g["soc0"], g["tc"], n, nthreads=8)
-    worst = max(rel(out[k], g[k][:n]).max() for k in ("v", "phise"))
-    assert worst > 1e-5, worst
+    worst = max(rel(out[k], g[k][:n]).max() for k in KEYS)
+    assert worst > 1e-6, worst
+    rom4 = R.make_tab_rom(str(g["kind"]), tab_T_degC=tuple(g["tab_T_degC"]), T_eval_degC=tuple(g["T_eval_degC"]))
+    out4 = oc.run(rom4, g["soc0"], g["tc"], n, nthreads=8)
+    assert max(rel(out4[k], g[k][:n]).max() for k in KEYS) < 1e-12
 
 
 def _hash(rom):

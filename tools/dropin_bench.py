@@ -40,14 +40,16 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-diag", action="store_true", help="skip the mpcdiag call (poles / sv)")
-    ap.add_argument("--route", default="device", choices=("device", "host", "capi"),
+    ap.add_argument("--route", default="device", choices=("device", "host", "capi", "capi-async"),
                     help="device: the drop-ins' round-5 sequence (zk / Xind / lin stay on the device, 14 "
                          "doubles of lin read back); host: the round-4 sequence (every array through the "
                          "host); capi: the device sequence through ctypes (mpcekf.py) instead of the MEX "
-                         "gateway, so the shim's marshalling is separated out")
+                         "gateway, so the shim's marshalling is separated out; capi-async: the same with the "
+                         "_async stage twins, Vcell handed to iterEKF on the device, one synchronisation per "
+                         "step (iterMPC)")
     ap.add_argument("--rom-lookup", default="quintic", choices=("linear", "cubic", "quintic"))
     a = ap.parse_args()
-    if a.route == "capi":
+    if a.route in ("capi", "capi-async"):
         return capi(a)
     import importlib
 
@@ -139,6 +141,7 @@ def capi(a):
     slots = np.array(list(range(20, 27)) + [28] + list(range(29, 35)), dtype=np.int32)
     tim = {k: 0.0 for k in ("scalars", "plant", "ekf", "linearize", "lin_fields", "mpcdiag", "mpc")}
     nb = {k: 0 for k in tim}
+    asy = a.route == "capi-async"
     with M.Context(rom, n, M.make_config(bounds=True)) as ctx:
         ctx.init_cells(soc0, tc)
         uk = np.zeros(n)
@@ -151,15 +154,19 @@ def capi(a):
 
         def step(count):
             nonlocal uk
+            ctx.asynchronous = asy
             timed("scalars", ctx.get_scalars, ("SOCnAvg", "SOCpAvg"))          # OB_step.m:226-228
             v = timed("plant", ctx.OB_step, uk, tc)
-            zk, zb, xi = timed("ekf", ctx.iterEKF, v, uk, tc)
+            # async: Vcell reaches iterEKF on the device (vk = None), its host copy at the sync
+            zk, zb, xi = timed("ekf", ctx.iterEKF, None if asy else v, uk, tc)
             timed("scalars", ctx.get_scalars, ("x0", "SigmaX0", "priorI"), flags=True)   # ekfData fields
             timed("linearize", ctx.EKFmatsHandler, None, None, tc, keep=True)
             f = timed("lin_fields", ctx.lin_fields, slots)
             if not a.no_diag:
                 timed("mpcdiag", ctx.mpc_diag, None)
-            uk, ne, cost = timed("mpc", ctx.iterMPC, None, zk[:, -1], cost=True)
+            ctx.asynchronous = False   # iterMPC synchronises: every earlier output is written
+            # async: SOCk_1 = zk(end) from the device zk (runMPC.m:99), the host zk not yet written
+            uk, ne, cost = timed("mpc", ctx.iterMPC, None, None if asy else zk[:, -1], cost=True)
             if count:
                 nb["scalars"] += (16 + 24 + 8) * n
                 nb["plant"] += 3 * 8 * n
@@ -183,7 +190,9 @@ def capi(a):
     same = bool(np.array_equal(u_last, ref))
     line = {"what": "the drop-ins' device-route stage sequence through the C-ABI (ctypes, host buffers): "
                     "plant -> ekf -> linearize (kept on device) -> lin_fields (14 doubles) -> mpc_diag -> mpc",
-            "route": "capi", "rom_lookup": a.rom_lookup, "cells": n, "steps": a.steps, "warmup": a.warmup,
+            "route": a.route, "rom_lookup": a.rom_lookup, "cells": n, "steps": a.steps, "warmup": a.warmup,
+            "copy_threads": os.environ.get("MPCEKF_COPY_THREADS", "default"),
+            "chunk": os.environ.get("MPCEKF_CHUNK", "default"),
             "mpcdiag": not a.no_diag, "cell_steps_per_s": n * a.steps / dt, "ms_per_step": dt / a.steps * 1e3,
             "ms_per_step_by_stage": {k: v / a.steps * 1e3 for k, v in tim.items()},
             "host_bytes_per_cell_step": {k: v / (n * a.steps) for k, v in nb.items()},
