@@ -226,9 +226,9 @@ struct mpcekf_ctx {
   size_t h_bytes = 0, bounce_max = (size_t)256 << 20;
   // round 6: the buffer is bump-allocated over the calls up to the next synchronisation
   // (xoff), so _async calls keep their regions until their copies finish; outputs leave it
-  // in chunks of xchunk bytes (MPCEKF_CHUNK, default 1 MiB), one event each (xev, reused
+  // in chunks of xchunk bytes (MPCEKF_CHUNK, default 4 MiB), one event each (xev, reused
   // after the synchronisation), copied out by the worker pool `copier`
-  size_t xoff = 0, xchunk = (size_t)1 << 20, xhwm = 0;
+  size_t xoff = 0, xchunk = (size_t)4 << 20, xhwm = 0;
   std::vector<hipEvent_t> xev;
   size_t xev_used = 0;
   bool xpending = false;

@@ -1338,9 +1338,9 @@ __device__ __forceinline__ void sweep_fast(const Cons &Cn, const double2 *hl, co
     double t = K[i];
     if (!mzero(i, 0)) t = __builtin_fma(Mf(i, 0), v0, t);
     if (!mzero(i, 1)) t = __builtin_fma(Mf(i, 1), v1, t);
-    const double m = fmin(t * hc.y, L[i]);
+    const double m = fmin_q(t * hc.y, L[i]);   // fmin / fmax(., fabs) without the canonicalising maxes
     const double nl = L[i] - m;
-    dmax = fmax(dmax, fabs(m));
+    dmax = fmax_abs_q(dmax, m);
     L[i] = nl;
     v0 = __builtin_fma(-xc.x, m, v0);   // fma(x, d, v) with d = -m: the same value
     v1 = __builtin_fma(-xc.y, m, v1);

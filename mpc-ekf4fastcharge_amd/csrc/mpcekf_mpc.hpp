@@ -34,6 +34,22 @@ __device__ __forceinline__ bool hild_rok(double h) {
   const double a = fabs(h);
   return h == 0.0 || (a >= 0x1p-1020 && a <= 0x1p1020);
 }
+// fmin(q, l) for operands that are not signalling NaNs (q a product, l an arithmetic result
+// or a finite load): v_min_f64 itself.  fmin's lowering first quiets l with a v_max_f64
+// (l, l) on every row of a sweep, which is pure issue cost there.
+__device__ __forceinline__ double fmin_q(double q, double l) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(q), "v"(l));
+  return r;
+}
+// fmax(a, |m|) for operands that are not signalling NaNs (a running max, m a min of a
+// product): v_max_f64 with the abs source modifier, one instruction.  fmax(a, fabs(m))
+// lowers to a canonicalising v_max_f64 (|m|, |m|) first when m comes from inline asm.
+__device__ __forceinline__ double fmax_abs_q(double a, double m) {
+  double r;
+  asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(m));
+  return r;
+}
 __device__ __forceinline__ double hild_step(double t, double h, double rinv, double l, double &nl) {
   if (hild_rok(h) && isfinite(l)) {
     const double m = fmin(t * rinv, l);

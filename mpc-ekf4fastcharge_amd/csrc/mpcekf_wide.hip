@@ -868,7 +868,7 @@ __global__ void __launch_bounds__(128, 1) k_hild_wide(const KCfg cf, const KStat
       // hild_step's reciprocal form: m = min(t / H_ii, lambda_i) with t (1/H_ii), the step -m,
       // lambda_i - m: every H_ii is in its domain (checked at the staging) and lambda_i finite
       // while v is (a zero H(0) row's 1/H_ii = +-inf gives x / +-0 by IEEE)
-      const double m = fmin(t * h.y, li);
+      const double m = fmin_q(t * h.y, li);   // fmin without the canonicalising max of lambda_i
       const double nl = li - m;
       convm &= __ballot(fabs(m) < tol);
       lst[i] = nl;
