@@ -297,7 +297,7 @@ class Context:
         check(self.L.mpcekf_step_ex(self.h, int(nsteps), tcs.ctypes.data_as(C.c_void_p) if tcs is not None else None,
                                     C.byref(tr), 0))
         if "poles" in out:
-            out["poles"] = out["poles"][..., 0] + 1j * out["poles"][..., 1]
+            out["poles"] = _complex(out["poles"])
         return out
 
     def step_device(self, nsteps, u=0, v=0, soc=0, phise=0, nexec=0):
@@ -380,7 +380,7 @@ class Context:
         self._stage("ekf_step", dptr(v), dptr(i), dptr(t), dptr(zk), dptr(zb), iptr(xm), dptr(xg), keep=(zk, zb, xm, xg))
         if not xind:
             return zk, zb, None
-        return zk, zb, dict(model=xm, gamma=xg, theT=xm // self.rom.nZ, theZ=xm % self.rom.nZ)
+        return zk, zb, _Xind(model=xm, gamma=xg, nZ=self.rom.nZ)
 
     def EKFmatsHandler(self, zk, Xind, Tk=None, keep=False):
         """[MPC, xhat] = EKFmatsHandler(ekfData, Xind, zk, Tk)  (EKFmatsHandler.m:1).
@@ -443,9 +443,7 @@ class Context:
         p = np.empty((self.n, 7, 2))
         sv = np.empty((self.n, 7))
         self._stage("mpc_diag", dptr(lin), dptr(u), dptr(p), dptr(sv), keep=(p, sv))
-        if self.asynchronous:   # (poles re / im [n, 7, 2], sv): the complex view only after sync
-            return p, sv
-        return p[..., 0] + 1j * p[..., 1], sv
+        return _complex(p), sv   # a view of p: asynchronously, its values arrive at the sync
 
     # -- state -----------------------------------------------------------
     def get_state(self):
@@ -480,6 +478,32 @@ class Context:
         s = _lib.State(dptr(a.get("bigX")), dptr(a.get("ekf")), dptr(a.get("scal")), dptr(a.get("lam")),
                        iptr(a.get("warn")), iptr(a.get("status")), dptr(a.get("mb")))
         check(self.L.mpcekf_set_state(self.h, C.byref(s)))
+
+
+def _complex(p):
+    """[..., 2] re / im float64 pairs as a complex128 [...] view (no copy, the exact pairs:
+    re + 1j * im would turn a -0 real part into +0 and an infinite imaginary part's real
+    part into NaN)."""
+    return p.view(np.complex128)[..., 0]
+
+
+class _Xind(dict):
+    """iterEKF's Xind: model / gamma, and theT / theZ (model // nZ, model % nZ) formed when
+    first read -- after an asynchronous iterEKF, model holds its values only after the sync."""
+
+    def __init__(self, model, gamma, nZ):
+        super().__init__(model=model, gamma=gamma)
+        self._nZ = nZ
+
+    def __missing__(self, key):
+        if key == "theT":
+            v = self["model"] // self._nZ
+        elif key == "theZ":
+            v = self["model"] % self._nZ
+        else:
+            raise KeyError(key)
+        self[key] = v
+        return v
 
 
 # ---------------------------------------------------------------------------

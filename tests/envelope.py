@@ -23,9 +23,19 @@ def load(name):
     return np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
 
 
-def outside(x, lo, hi, rtol=RTOL):
-    """Boolean mask of entries of x outside [lo, hi] widened by rtol * max(|lo|, |hi|)."""
-    tol = rtol * np.maximum(np.abs(lo), np.abs(hi))
+# Window statistics (check_near, check_tail_stats) are held to the members' range widened by
+# this fraction of its width on each side.  One more trajectory drawn like the N members
+# lands outside their raw [min, max] with probability 2 / (N + 1) per statistic, and the
+# checks make 12 per cell (48 for the near-limit cells): at N = 73 a fair sample fails some
+# raw range most of the time.  A quarter of the range still separates another attractor or a
+# biased implementation (the cells' statistics differ between cells by several ranges).
+STAT_MARGIN = 0.25
+
+
+def outside(x, lo, hi, rtol=RTOL, margin=0.0):
+    """Boolean mask of entries of x outside [lo, hi] widened by rtol * max(|lo|, |hi|) and
+    by margin * (hi - lo)."""
+    tol = rtol * np.maximum(np.abs(lo), np.abs(hi)) + margin * (hi - lo)
     return (x < lo - tol) | (x > hi + tol)
 
 
@@ -49,7 +59,7 @@ def check_near(out, e, window=NEAR_TAIL):
     given step), so no per-step band from a finite ensemble holds an independent
     trajectory.  What is held is the trajectory's distribution over the window: its mean,
     10th and 90th percentile of u, v, soc and phise, and its final SOC, each inside the
-    range the members' own statistics span (widened by 1e-6 relative)."""
+    range the members' own statistics span (widened by 1e-6 relative and STAT_MARGIN)."""
     a, b = window
     stats = {"wmean": lambda x: x.mean(0), "wlo": lambda x: np.percentile(x, 10, axis=0),
              "whi": lambda x: np.percentile(x, 90, axis=0)}
@@ -57,10 +67,11 @@ def check_near(out, e, window=NEAR_TAIL):
         x = np.asarray(out[k])[a:b]
         for nm, f in stats.items():
             m = e[f"{k}_{nm}"]                      # [4 cells, members]
-            bad = outside(f(x), m.min(1), m.max(1))
-            assert not bad.any(), f"{k} {nm}: cells {np.nonzero(bad)[0].tolist()} outside the members' range"
+            bad = outside(f(x), m.min(1), m.max(1), margin=STAT_MARGIN)
+            assert not bad.any(), (f"{k} {nm}: cells {np.nonzero(bad)[0].tolist()} outside the members' range: "
+                                   f"{f(x)[bad]} vs [{m.min(1)[bad]}, {m.max(1)[bad]}]")
     end = np.asarray(out["soc"])[-1]
-    bad = outside(end, e["soc_end"].min(1), e["soc_end"].max(1))
+    bad = outside(end, e["soc_end"].min(1), e["soc_end"].max(1), margin=STAT_MARGIN)
     assert not bad.any(), f"final SOC of cells {np.nonzero(bad)[0].tolist()} outside the members' range"
 
 
@@ -68,7 +79,7 @@ def check_tail_stats(out, e):
     """One cell's trajectories [steps] (or [steps, 1]) over its chaotic tail [tail0, end)
     against the members of a ulp ensemble (tests/golden/handles_runmpc_3001): the window
     mean, 10th and 90th percentile of u, v, soc and phise each inside the range the
-    members' own statistics span (widened by 1e-6 relative), and the step to 90 % SOC
+    members' own statistics span (widened by 1e-6 relative and STAT_MARGIN), and the step to 90 % SOC
     one of the members' (check_near's rule for a single cell)."""
     a = int(e["tail0"])
     stats = {"wmean": lambda x: x.mean(), "wlo": lambda x: np.percentile(x, 10), "whi": lambda x: np.percentile(x, 90)}
@@ -76,7 +87,7 @@ def check_tail_stats(out, e):
         x = np.asarray(out[k]).reshape(-1)[a:]
         for nm, f in stats.items():
             m = e[f"{k}_{nm}"]
-            assert not outside(np.array([f(x)]), m.min(), m.max()).any(), \
+            assert not outside(np.array([f(x)]), m.min(), m.max(), margin=STAT_MARGIN).any(), \
                 f"{k} {nm} over steps {a}-: {f(x)!r} outside the members' [{m.min()!r}, {m.max()!r}]"
     soc = np.asarray(out["soc"]).reshape(-1)
     t90 = int(np.argmax(soc >= 0.90)) if (soc >= 0.90).any() else -1

@@ -358,3 +358,15 @@ def test_ulp_envelopes_are_not_vacuous():
     w = envelope.load("env_wide_near4_200")
     assert (w["u_wmean"].max(1) - w["u_wmean"].min(1) >= 0).all()
     assert np.ptp(w["soc_wmean"].mean(1)) > 0.01
+    # the widened window-mean ranges (envelope.STAT_MARGIN) tell the cells apart as well as the
+    # raw ranges do: no other cell's members' median window mean of u, soc or phise that a
+    # cell's raw range excludes is let in by the margin (v sits at the voltage limit in all
+    # four cells, and the 95 % cell's members spread widely, so v's and the percentiles'
+    # ranges discriminate less, with or without it)
+    for k in ("u", "soc", "phise"):
+        m = w[f"{k}_wmean"]
+        for i in range(m.shape[0]):
+            others = np.median(np.delete(m, i, axis=0), axis=1)
+            raw = envelope.outside(others, m[i].min(), m[i].max())
+            wide = envelope.outside(others, m[i].min(), m[i].max(), margin=envelope.STAT_MARGIN)
+            assert raw.sum() >= 1 and (wide == raw).all(), (k, i, raw, wide)
