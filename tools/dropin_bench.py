@@ -40,17 +40,23 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-diag", action="store_true", help="skip the mpcdiag call (poles / sv)")
-    ap.add_argument("--route", default="device", choices=("device", "host", "capi", "capi-async"),
+    ap.add_argument("--route", default="device",
+                    choices=("device", "host", "capi", "capi-async", "c", "c-async", "c-reuse", "c-async-reuse"),
                     help="device: the drop-ins' round-5 sequence (zk / Xind / lin stay on the device, 14 "
                          "doubles of lin read back); host: the round-4 sequence (every array through the "
                          "host); capi: the device sequence through ctypes (mpcekf.py) instead of the MEX "
                          "gateway, so the shim's marshalling is separated out; capi-async: the same with the "
                          "_async stage twins, Vcell handed to iterEKF on the device, one synchronisation per "
-                         "step (iterMPC)")
+                         "step (iterMPC); c / c-async: the capi sequences driven from C "
+                         "(tools/dropin_loop.c: fresh malloc'ed outputs every call, as mxArrays), so the "
+                         "Python binding's per-call work is separated out as well; -reuse: output arrays "
+                         "allocated once, so the caller's allocator is separated out too")
     ap.add_argument("--rom-lookup", default="quintic", choices=("linear", "cubic", "quintic"))
     a = ap.parse_args()
     if a.route in ("capi", "capi-async"):
         return capi(a)
+    if a.route.startswith("c-") or a.route == "c":
+        return c_loop(a)
     import importlib
 
     import mexshim
@@ -201,6 +207,61 @@ def capi(a):
     print(json.dumps(line), flush=True)
     if not same:
         sys.exit("dropin_bench: the C-ABI stage route's u differs from the fused step")
+
+
+def c_loop(a):
+    """The capi stage sequence driven from C (tools/dropin_loop.c) on a context made here."""
+    import ctypes as C
+    import importlib
+    import subprocess
+
+    import bench
+    P = importlib.import_module("mpc-ekf4fastcharge_amd")
+    M = importlib.import_module("mpc-ekf4fastcharge_amd.mpcekf")
+    bdir = os.path.join(ROOT, "mpc-ekf4fastcharge_amd", "_build")
+    so = os.path.join(bdir, "libdropin_loop.so")
+    src = os.path.join(ROOT, "tools", "dropin_loop.c")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.run(["gcc", "-O2", "-std=c11", "-shared", "-fPIC", "-I" + os.path.join(ROOT, "include"), src,
+                        "-L" + bdir, "-lmpcekf", "-Wl,-rpath,$ORIGIN", "-o", so], check=True)
+    lib = C.CDLL(so)
+    rom = P.make_synth_rom(lookup=a.rom_lookup)
+    n = a.cells
+    soc0, tc = bench.batch_inputs(n)
+    sc = M.Context.SCALARS
+    sa = np.array([sc.index(k) for k in ("SOCnAvg", "SOCpAvg")], dtype=np.int32)
+    sb = np.array([sc.index(k) for k in ("x0", "SigmaX0", "priorI")], dtype=np.int32)
+    fields = np.array(list(range(20, 27)) + [28] + list(range(29, 35)), dtype=np.int32)
+    uk = np.zeros(n)
+    ms = np.zeros(7)
+    tot, byt = C.c_double(), C.c_double()
+    ip = lambda x: x.ctypes.data_as(C.POINTER(C.c_int32))
+    dp = lambda x: x.ctypes.data_as(C.POINTER(C.c_double))
+    with M.Context(rom, n, M.make_config(bounds=True)) as ctx:
+        ctx.init_cells(soc0, tc)
+        lib.dropin_loop.restype = C.c_int
+        rc = lib.dropin_loop(ctx.h, C.c_int64(n), C.c_int32(ctx.nz), C.c_int32(a.steps),
+                             C.c_int32(a.warmup), C.c_int32(("async" in a.route) + 2 * ("reuse" in a.route)), dp(tc), ip(sa), len(sa), ip(sb),
+                             len(sb), ip(fields), len(fields), dp(uk), dp(ms), C.byref(tot), C.byref(byt))
+        if rc:
+            sys.exit(f"dropin_loop failed: {rc} {M._lib.load().mpcekf_last_error().decode()}")
+    ref = M.runMPC(rom, soc0, tc, a.warmup + a.steps)["u"][-1]
+    same = bool(np.array_equal(uk, ref))
+    names = ("scalars", "plant", "ekf", "linearize", "lin_fields", "mpcdiag", "mpc")
+    line = {"what": "the drop-ins' device-route stage sequence through the C-ABI, driven from C (tools/dropin_loop.c, "
+                    + ("host output arrays allocated once" if "reuse" in a.route else
+                       "fresh malloc'ed host outputs every call") +
+                    "): plant -> ekf -> linearize (kept on device) -> lin_fields (14 doubles) -> mpc_diag -> mpc",
+            "route": a.route, "rom_lookup": a.rom_lookup, "cells": n, "steps": a.steps, "warmup": a.warmup,
+            "copy_threads": os.environ.get("MPCEKF_COPY_THREADS", "default"),
+            "chunk": os.environ.get("MPCEKF_CHUNK", "default"), "mpcdiag": True,
+            "cell_steps_per_s": n * a.steps / (tot.value * 1e-3), "ms_per_step": tot.value / a.steps,
+            "ms_per_step_by_stage": {k: float(ms[i]) / a.steps for i, k in enumerate(names)},
+            "host_bytes_per_cell_step_total": byt.value,
+            "u_last_equals_fused": same, "build_id": M._lib.load().mpcekf_build_id().decode()}
+    print(json.dumps(line), flush=True)
+    if not same:
+        sys.exit("dropin_bench: the C-driven stage route's u differs from the fused step")
 
 
 if __name__ == "__main__":

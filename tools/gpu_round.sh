@@ -48,7 +48,7 @@ do_pmc() {
   timeout -k 10 300 python bench.py --pmc gpurun_out/prof_$TAG/pmc_traffic.json > $O/bench_pmc.json 2> $O/bench_pmc.err
 }
 do_dropin() {
-  for rt in capi capi-async; do
+  for rt in capi capi-async c c-async; do
     timeout -k 10 300 python tools/dropin_bench.py --route $rt --cells 65536 --steps 20 > $O/dropin_${rt}_65536.json \
       2> $O/dropin_${rt}_65536.err && \
     timeout -k 10 300 python tools/dropin_bench.py --route $rt --cells 1024 --steps 40 > $O/dropin_${rt}_1024.json \
