@@ -9,8 +9,10 @@
 #            configs[4], the 131,072-cell per-GPU load of configs[3], the v2-table line
 #   trace    rocprofv3 kernel trace + stats of the default bench and of configs[1] / [4]
 #   pmc      PMC traffic (tools/profile.sh) and SQ counters (tools/cell_pmc.sh) of the
-#            default bench, then the bench line with that traffic attached
-#   dropin   the C-ABI stage route at 65,536 and 1,024 cells (tools/dropin_bench.py)
+#            default bench, then the bench line with that traffic attached; the same traffic
+#            pass and line at Np = 20 / Nc = 10
+#   dropin   the C-ABI stage route at 65,536 and 1,024 cells (tools/dropin_bench.py: through
+#            mpcekf.py, and driven from C with fresh or reused host buffers; sync and _async)
 #   closing  tests + smoke + bench + trace + pmc + dropin on one build (the round's record)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -45,10 +47,13 @@ do_trace() {
 do_pmc() {
   bash tools/profile.sh $TAG && \
   bash tools/cell_pmc.sh $TAG && \
-  timeout -k 10 300 python bench.py --pmc gpurun_out/prof_$TAG/pmc_traffic.json > $O/bench_pmc.json 2> $O/bench_pmc.err
+  timeout -k 10 300 python bench.py --pmc gpurun_out/prof_$TAG/pmc_traffic.json > $O/bench_pmc.json 2> $O/bench_pmc.err && \
+  PMCARGS="--np 20" bash tools/profile.sh ${TAG}_np20 --np 20 --nc 10 && \
+  timeout -k 10 300 python bench.py --no-cpu --np 20 --nc 10 --pmc gpurun_out/prof_${TAG}_np20/pmc_traffic.json \
+    > $O/bench_pmc_wide.json 2> $O/bench_pmc_wide.err
 }
 do_dropin() {
-  for rt in capi capi-async c c-async; do
+  for rt in capi capi-async c c-async c-reuse c-async-reuse; do
     timeout -k 10 300 python tools/dropin_bench.py --route $rt --cells 65536 --steps 20 > $O/dropin_${rt}_65536.json \
       2> $O/dropin_${rt}_65536.err && \
     timeout -k 10 300 python tools/dropin_bench.py --route $rt --cells 1024 --steps 40 > $O/dropin_${rt}_1024.json \
