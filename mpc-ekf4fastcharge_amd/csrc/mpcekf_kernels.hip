@@ -34,6 +34,12 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 // read; the others read Sigma at their update.  1: corner 0's Sigma is what the gains
 // use first; 2..4 hold more Sigma in registers and spill (measured no faster).
 // MPCEKF_CELL_OUTLINE: the Jacobi symmetrisation as a call instead of inline.
+#ifndef MPCEKF_S_AHEAD  // k_cell: corner j+1's Sigma loaded before corner j's record store (§4.2)
+#define MPCEKF_S_AHEAD 1
+#endif
+#ifndef MPCEKF_RING_LATE  // k_cell: the plant's ring stores after the cell's last load (§4.2)
+#define MPCEKF_RING_LATE 1
+#endif
 #ifndef MPCEKF_REC_ONCE
 #define MPCEKF_REC_ONCE 1
 #endif
@@ -2164,7 +2170,7 @@ __device__ __forceinline__ void replay_S(double S[NPK], const double *a, int ts,
 
 template <int NZ>
 __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc, int NM, const int m[4], int64_t c,
-                                              int t, double W) {
+                                              int t, double W, double pt) {
   // all timestamps, then all lagging records, in flight together (latency, not bytes,
   // is the cost here); a model named by several corners is advanced once
   int ts[4];
@@ -2178,7 +2184,7 @@ __device__ __forceinline__ void ekf_catch_up4(const KState &s, const CellCtx &cc
     for (int i = 0; i < j; ++i) need[j] = need[j] && m[i] != m[j];
   }
   if (!(need[0] || need[1] || need[2] || need[3])) return;
-  const double pt = s.hist_p[(size_t)(t % LAZY_H) * s.n + c];  // the usual (lag-1) input
+  // pt: step t's input (the ring's slot t, which k_cell may not have stored yet: MPCEKF_RING_LATE)
   double x[4][NX], S[4][NPK];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -2403,13 +2409,17 @@ __device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]
 template <int NZ, bool PL>
 __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, const double *L, const double *tb,
                                              const double *Tp, const double *Zp, int64_t c, int lazy_t, double Iapp,
-                                             double tcs, int st) {
+                                             double tcs, int st, double *ring_p = nullptr) {
   constexpr int OA = NZ * NX + NZ, OR0 = NZ * NX + NZ + NX + NPK, OD = NZ * NX;
   const int stride = r.cell_stride;
   if (lazy_t) {  // this step's inputs, for the deferred updates of every model
-    const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
-    s.hist_u[slot] = Iapp;
-    s.hist_p[slot] = s.priorI[c];
+    if (ring_p) {  // stored by the caller after its last load (MPCEKF_RING_LATE)
+      *ring_p = s.priorI[c];
+    } else {
+      const size_t slot = (size_t)(lazy_t % LAZY_H) * s.n + c;
+      s.hist_u[slot] = Iapp;
+      s.hist_p[slot] = s.priorI[c];
+    }
   }
   if (st & ST_ERROR) return __builtin_nan("");
   const double T = tcs + 273.15;  // OB_step.m:75
@@ -2619,6 +2629,10 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   const double *Tp = tb + r.cell_tab + r.cell_tablen;
   const double *Zp = Tp + MAXT;
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the plant's ring inputs for this step (MPCEKF_RING_LATE: stored after the cell's last
+  // load, below, so that no load of the step waits for their stores)
+  double ring_u = 0.0, ring_p = 0.0;
+  bool ring_late = false;
   // the per-cell work as a lambda: its early exits return here, so every lane of the block
   // reaches the barrier of the fused Hildreth below
   auto body = [&]() {
@@ -2682,7 +2696,10 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     if constexpr ((PARTS & P_EKF) && !MB) {
       if (fplant && !planted) {
         if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
-        vplant = cell_plant<NZ, PL>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, s.uk[c], Tc, st);
+        ring_u = s.uk[c];
+        vplant = cell_plant<NZ, PL>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, ring_u, Tc, st,
+                                    MPCEKF_RING_LATE ? &ring_p : nullptr);
+        ring_late = MPCEKF_RING_LATE && io.lazy_t;
         s.vk[c] = vplant;
         planted = true;
       }
@@ -2933,6 +2950,16 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     __builtin_amdgcn_sched_barrier(0);
     STAMP(5);
     double xu[4][NX];  // corner j's xhat after its update
+    // MPCEKF_S_AHEAD: corner j+1's Sigma is loaded before corner j's record is stored.  On
+    // gfx950 one counter (vmcnt) covers loads and stores in issue order, so a load issued
+    // after a store cannot be waited for without waiting for the store as well; loaded one
+    // corner ahead, the wait for Sigma_{j+1} no longer includes corner j's store.  A corner
+    // that repeats an earlier model (dup) reads its record after that store, as before.
+    double Sn[NPK];
+    auto s_ahead = [&](int j) {
+      return MPCEKF_S_AHEAD && j < 4 && j >= MPCEKF_REC_ONCE && !dup[j];
+    };
+    if (s_ahead(1)) load_S(cc.erec + (size_t)xi.m[1] * REC, Sn);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       double *rec = cc.erec + (size_t)xi.m[j] * REC;
@@ -2945,12 +2972,16 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
         if (j < MPCEKF_REC_ONCE) {
 #pragma unroll
           for (int k = 0; k < NPK; ++k) Sj[k] = Sr[j][k];
+        } else if (s_ahead(j)) {
+#pragma unroll
+          for (int k = 0; k < NPK; ++k) Sj[k] = Sn[k];
         } else {
           load_S(rec, Sj);
         }
         if (t && j > 0) replay_S(Sj, cc.L + xi.m[j] * cc.stride + NZ * NX + NZ, tsj[j], t, cf.SigmaW);
       }
       meas_update_regs<MPCEKF_CELL_OUTLINE>(xj, Sj, Lg[j], St[j], res);
+      if (j + 1 < 4 && s_ahead(j + 1)) load_S(cc.erec + (size_t)xi.m[j + 1] * REC, Sn);
       store_rec(rec, xj, Sj);
       if (t) s.ts_ekf[c * r.NM + xi.m[j]] = t;
 #pragma unroll
@@ -2970,7 +3001,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     const bool same = m1[0] == xi.m[0] && m1[1] == xi.m[1] && m1[2] == xi.m[2] && m1[3] == xi.m[3] &&
                       !(dup[1] || dup[2] || dup[3]);
     if (!same) {
-      if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW);
+      if (io.lazy_t) ekf_catch_up4<NZ>(s, cc, r.NM, xi.m, c, io.lazy_t, cf.SigmaW, pt);
 #pragma unroll
       for (int j = 0; j < 4; ++j) load_x(cc.erec + (size_t)xi.m[j] * REC, xu[j]);
     }
@@ -3133,6 +3164,11 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #endif
   };
   body();
+  if (ring_late) {  // every path of body ran the plant; the ring's slot t is read by no load of this step
+    const size_t slot = (size_t)(io.lazy_t % LAZY_H) * s.n + c;
+    s.hist_u[slot] = ring_u;
+    s.hist_p[slot] = ring_p;
+  }
   if constexpr (MPCEKF_CELL_HILD && (PARTS & P_MPC) != 0) {
     if (io.hild) {  // hildreth.m in the same kernel (no k_hild launch): the blob's LDS becomes the
       __syncthreads();  // per-lane Hildreth slots once every wave of the block is done with it
