@@ -40,6 +40,9 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_RING_LATE  // k_cell: the plant's ring stores after the cell's last load (§4.2)
 #define MPCEKF_RING_LATE 1
 #endif
+#ifndef MPCEKF_PLANT_STORE_LATE  // k_cell: the plant's state stores after the cell's last load
+#define MPCEKF_PLANT_STORE_LATE 0
+#endif
 #ifndef MPCEKF_REC_ONCE
 #define MPCEKF_REC_ONCE 1
 #endif
@@ -2401,15 +2404,39 @@ __device__ __forceinline__ double qform(const double T[NPK], const double rw[NX]
   return q;
 }
 
+// The plant's per-cell stores, held for the caller to issue after its last load
+// (MPCEKF_PLANT_STORE_LATE): SOCn / SOCp and the advanced corner states.
+struct PlantOut {
+  double socn, socp;
+  double x[4][6];
+  int mm[4];
+  bool adv[4], on;
+};
+__device__ __forceinline__ void plant_store(const KRom &r, const KState &s, int64_t c, int lazy_t, const PlantOut &o) {
+  s.SOCn[c] = o.socn;
+  s.SOCp[c] = o.socp;
+  double *bx = s.bigx + (size_t)c * r.NM * 6;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!o.adv[j]) continue;
+    double2 *p = reinterpret_cast<double2 *>(bx + (size_t)o.mm[j] * 6);
+    p[0] = make_double2(o.x[j][0], o.x[j][1]);
+    p[1] = make_double2(o.x[j][2], o.x[j][3]);
+    p[2] = make_double2(o.x[j][4], o.x[j][5]);
+    s.ts_plant[c * r.NM + o.mm[j]] = lazy_t;
+  }
+}
 // OB_step's simStep (OB_step.m:188-357) for one cell at the start of k_cell's fused step:
 // k_plant's arithmetic, read from the cell blob (the plant's 9 role rows are the blob's
 // first C rows, D at nzp*5, diag(A) after them -- the integrator's a = 1 exactly, checked
 // by build_rom -- and the res0 column after the Sigma coefficients).  Returns Vcell; the
 // plant state, averages, ring inputs and timestamps are stored as k_plant stores them.
+// (ring_p / po: the ring input and the state stores handed back for the caller to issue
+// after its last load, MPCEKF_RING_LATE / MPCEKF_PLANT_STORE_LATE.)
 template <int NZ, bool PL>
 __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, const double *L, const double *tb,
                                              const double *Tp, const double *Zp, int64_t c, int lazy_t, double Iapp,
-                                             double tcs, int st, double *ring_p = nullptr) {
+                                             double tcs, int st, double *ring_p = nullptr, PlantOut *po = nullptr) {
   constexpr int OA = NZ * NX + NZ, OR0 = NZ * NX + NZ + NX + NPK, OD = NZ * NX;
   const int stride = r.cell_stride;
   if (lazy_t) {  // this step's inputs, for the deferred updates of every model
@@ -2515,6 +2542,21 @@ __device__ __forceinline__ double cell_plant(const KRom &r, const KState &s, con
   const double Rfn = et.f(0, EF_RF, negSOC), Rfp = et.f(1, EF_RF, posSOC);  // OB_step.m:339-340
   double V = posEta3 - negEta0 + yk[R_PHIE] + Uocpp3 - Uocpn0 + (Rfp * yk[R_IFDL3] - Rfn * yk[R_IFDL0]);
   V = V - r.Rc * Iapp;
+  if (po) {  // the caller stores them after its last load
+    po->on = true;
+    po->socn = SOCnAvg;
+    po->socp = SOCpAvg;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      po->mm[j] = mm[j];
+      po->adv[j] = lazy_t && tsj[j] < lazy_t;
+      const double *a = L + mm[j] * stride + OA;
+#pragma unroll
+      for (int e = 0; e < NX; ++e) po->x[j][e] = __builtin_fma(a[e], xs[j][e], Iapp);
+      po->x[j][NX] = __builtin_fma(1.0, xs[j][NX], Iapp);
+    }
+    return V;
+  }
   s.SOCn[c] = SOCnAvg;
   s.SOCp[c] = SOCpAvg;
   if (lazy_t) {  // advance the corners through step t in place
@@ -2633,6 +2675,8 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
   // load, below, so that no load of the step waits for their stores)
   double ring_u = 0.0, ring_p = 0.0;
   bool ring_late = false;
+  PlantOut pout;  // MPCEKF_PLANT_STORE_LATE: the plant's stores, issued after body
+  pout.on = false;
   // the per-cell work as a lambda: its early exits return here, so every lane of the block
   // reaches the barrier of the fused Hildreth below
   auto body = [&]() {
@@ -2698,7 +2742,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
         if (c == 0 && io.lazy_t) *s.hslow = 0;  // k_hild_slow of the previous step has finished
         ring_u = s.uk[c];
         vplant = cell_plant<NZ, PL>(r, s, cc.L, tb, Tp, Zp, c, io.lazy_t, ring_u, Tc, st,
-                                    MPCEKF_RING_LATE ? &ring_p : nullptr);
+                                    MPCEKF_RING_LATE ? &ring_p : nullptr, MPCEKF_PLANT_STORE_LATE ? &pout : nullptr);
         ring_late = MPCEKF_RING_LATE && io.lazy_t;
         s.vk[c] = vplant;
         planted = true;
@@ -3164,6 +3208,7 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
 #endif
   };
   body();
+  if (MPCEKF_PLANT_STORE_LATE && pout.on) plant_store(r, s, c, io.lazy_t, pout);
   if (ring_late) {  // every path of body ran the plant; the ring's slot t is read by no load of this step
     const size_t slot = (size_t)(io.lazy_t % LAZY_H) * s.n + c;
     s.hist_u[slot] = ring_u;
