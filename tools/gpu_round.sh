@@ -9,8 +9,9 @@
 #            configs[4], the 131,072-cell per-GPU load of configs[3], the v2-table line
 #   trace    rocprofv3 kernel trace + stats of the default bench and of configs[1] / [4]
 #   pmc      PMC traffic (tools/profile.sh) and SQ counters (tools/cell_pmc.sh) of the
-#            default bench, then the bench line with that traffic attached; the same traffic
-#            pass and line at Np = 20 / Nc = 10
+#            default bench, then the bench line with that traffic attached (the Np = 20 pass:
+#            PMCARGS="--np 20" bash tools/profile.sh TAG_np20 --np 20 --nc 10, in a call of its
+#            own: its counter passes print nothing for minutes)
 #   dropin   the C-ABI stage route at 65,536 and 1,024 cells (tools/dropin_bench.py: through
 #            mpcekf.py, and driven from C with fresh or reused host buffers; sync and _async)
 #   closing  tests + smoke + bench + trace + pmc + dropin on one build (the round's record)
@@ -47,10 +48,7 @@ do_trace() {
 do_pmc() {
   bash tools/profile.sh $TAG && \
   bash tools/cell_pmc.sh $TAG && \
-  timeout -k 10 300 python bench.py --pmc gpurun_out/prof_$TAG/pmc_traffic.json > $O/bench_pmc.json 2> $O/bench_pmc.err && \
-  PMCARGS="--np 20" bash tools/profile.sh ${TAG}_np20 --np 20 --nc 10 && \
-  timeout -k 10 300 python bench.py --no-cpu --np 20 --nc 10 --pmc gpurun_out/prof_${TAG}_np20/pmc_traffic.json \
-    > $O/bench_pmc_wide.json 2> $O/bench_pmc_wide.err
+  timeout -k 10 300 python bench.py --pmc gpurun_out/prof_$TAG/pmc_traffic.json > $O/bench_pmc.json 2> $O/bench_pmc.err
 }
 do_dropin() {
   for rt in capi capi-async c c-async c-reuse c-async-reuse; do
