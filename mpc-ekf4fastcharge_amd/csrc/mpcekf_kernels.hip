@@ -40,8 +40,8 @@ constexpr int NCON = 4 * NC + 3 * NP;  // constraint rows (constraintsMPC.m)
 #ifndef MPCEKF_RING_LATE  // k_cell: the plant's ring stores after the cell's last load (§4.2)
 #define MPCEKF_RING_LATE 1
 #endif
-#ifndef MPCEKF_PLANT_STORE_LATE  // k_cell: the plant's state stores after the cell's last load (1)
-#define MPCEKF_PLANT_STORE_LATE 0     // or after iterEKF's first record loads are issued (2)
+#ifndef MPCEKF_PLANT_STORE_LATE  // k_cell: the plant's state stores after the cell's last load
+#define MPCEKF_PLANT_STORE_LATE 0
 #endif
 #ifndef MPCEKF_REC_ONCE
 #define MPCEKF_REC_ONCE 1
@@ -2934,10 +2934,6 @@ __global__ void __launch_bounds__(256) k_cell(const KRom r, const KCfg cf, const
     // step t's ring input: the plant stores this cell's priorI there (k_plant, or cell_plant
     // below, which may not have run yet)
     const double pt = t ? (fplant ? s.priorI[c] : s.hist_p[(size_t)(t % LAZY_H) * s.n + c]) : 0.0;
-    if (MPCEKF_PLANT_STORE_LATE == 2 && pout.on) {  // the plant's stores after the EKF's first loads
-      plant_store(r, s, c, io.lazy_t, pout);
-      pout.on = false;
-    }
     run_plant();  // the records above are in flight while the plant's chain runs
     if (planted) vk = vplant;
     if (t) {
