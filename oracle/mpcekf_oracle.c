@@ -640,7 +640,8 @@ static void hild_v(int Nc, int nC, const double *X, const double *lam, double *v
  * b_k = fma(M_i,k+8, v_k+8, a_k) when k + 8 < Nc, else a_k; summed as the pairwise tree
  * ((b0+b1)+(b2+b3)) + ((b4+b5)+(b6+b7)) (the 3-level lane butterfly).  For Nc <= 8 this is
  * round 2's 16-slot tree up to the sign of a zero t (its extra slots only added +0), which
- * cannot reach lambda: num = fma(H_ii, lambda_i, -t) and max(w, 0) absorb it. */
+ * cannot reach lambda: min(t (1/H_ii), lambda_i) is then +-0 or lambda_i, and lambda_i - m and
+ * the step's effect on v are the same for either sign (hild_step). */
 static double hild_row_t(int Nc, const double *Mi, const double *v, double Ki) {
   if (Nc <= 2) {
     double t = Ki;
