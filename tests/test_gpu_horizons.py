@@ -101,6 +101,17 @@ def test_bench_workloads_on_the_v3_rom_sampled(rom_v3, oc, M, Np, Nc, stride):
     _check(out, ref)
 
 
+def test_configs2_every_cell_on_the_v3_rom(rom_v3, oc, M):
+    """configs[2] as bench.py runs it (65,536 cells, Np = 5, the v3 quintic ROM) over the full
+    1,010-step window, every cell, bitwise against the C oracle (the sampled tests above hold
+    1 in 64; this holds all of them: ~30 s of C oracle on the box's 16 host threads)."""
+    soc0, tc = batch_inputs(65536)
+    steps = 1010
+    out = _gpu_sampled(M, rom_v3, soc0, tc, steps, 1)
+    ref = oc.run(rom_v3, soc0, tc, steps, nthreads=NTHREADS)
+    _check(out, ref)
+
+
 def test_configs4_wide_65536_cells_1010_steps_sampled(rom, oc, M):
     soc0, tc = batch_inputs(65536)
     steps, stride = 1010, 256
