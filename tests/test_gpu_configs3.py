@@ -6,7 +6,7 @@ the library in turn, over the 1,010-step window that holds the maxIter regime, a
 whole 1,048,576-cell input also runs as ONE context (≈17 GB of state, well inside one
 MI355X's 288 GB).  Checks:
 
-  * each shard's 1/512 sample of cells is bitwise equal to the C oracle;
+  * each shard's 1/64 sample of cells (16,384 of the million over the eight) is bitwise equal to the C oracle;
   * the concatenation of the eight shards' samples equals the single-context run's
     sample, bit for bit (runMPC.m:83-112 has no cross-cell term, so the shard boundaries
     cannot change any cell's bits).
@@ -24,7 +24,7 @@ from conftest import batch_inputs
 pytestmark = pytest.mark.gpu
 
 NTHREADS = min(16, os.cpu_count() or 1)
-TOTAL, WORLD, STEPS, STRIDE, CHUNK = 1048576, 8, 1010, 512, 101
+TOTAL, WORLD, STEPS, STRIDE, CHUNK = 1048576, 8, 1010, 64, 101
 KEYS = ("u", "v", "soc", "phise", "nexec")
 
 
