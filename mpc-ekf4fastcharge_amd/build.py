@@ -51,16 +51,17 @@ def source_hash():
     return h.hexdigest()[:16]
 
 
-def build(force=False, verbose=False, variant="", defines=()):
+def build(force=False, verbose=False, variant="", defines=(), flags=()):
     """variant "stamps": profiling build _build/libmpcekf_stamps.so (-DMPCEKF_STAMPS);
     any other variant name with ``defines`` (["NAME=VAL", ..]) builds an A/B library
-    _build/libmpcekf_<variant>.so that bench.py loads through MPCEKF_LIB."""
+    _build/libmpcekf_<variant>.so that bench.py loads through MPCEKF_LIB; ``flags`` are extra
+    hipcc arguments for such a variant (e.g. ["-mllvm", "-amdgpu-sched-strategy=max-ilp"])."""
     os.makedirs(OUT, exist_ok=True)
     jobs = []
     objs = []
     sfx = f"_{variant}" if variant else ""
     extra = ["-DMPCEKF_STAMPS"] if variant == "stamps" else []
-    extra += [f"-D{d}" for d in defines]
+    extra += [f"-D{d}" for d in defines] + list(flags)
     extra.append(f'-DMPCEKF_SRC_HASH="{source_hash()}"')
     lib = os.path.join(OUT, f"libmpcekf{sfx}.so")
     for s in SOURCES:
@@ -92,5 +93,7 @@ if __name__ == "__main__":
     ap.add_argument("--stamps", action="store_true")
     ap.add_argument("--variant", default="")
     ap.add_argument("-D", dest="defines", action="append", default=[])
+    ap.add_argument("--flag", dest="flags", action="append", default=[], help="extra hipcc argument (variants)")
     a = ap.parse_args()
-    print(build(force=a.force, verbose=True, variant="stamps" if a.stamps else a.variant, defines=a.defines))
+    print(build(force=a.force, verbose=True, variant="stamps" if a.stamps else a.variant, defines=a.defines,
+                flags=a.flags))
