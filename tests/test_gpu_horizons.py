@@ -6,7 +6,7 @@ included, so any difference is a bug).
   configs[2]  65 536 cells x 1 000 steps, a 1/64 strided sample of cells checked
               (cells are independent, runMPC.m:83-112, so the oracle runs the sample alone)
   configs[4]  65 536 cells x 1 000 steps at Np = 20 / Nc = 10, a 1/256 sample
-  and configs[2] / configs[4] again on the v3 (quintic) ROM the bench runs
+  and configs[1] / configs[2] / configs[4] again on the v3 (quintic) ROM the bench runs
 
 The 1 000-step window covers the part of the charge where ~2 % of cells run
 hildreth.m into maxIter (steps ~350-800).  The GPU runs in chunks of
@@ -134,3 +134,16 @@ def test_configs3_rank7_shard_131072_cells_sampled(rom, oc, M):
     out = _gpu_sampled(M, rom, soc0[a:b], tc[a:b], steps, stride)
     ref = oc.run(rom, soc0[a:b:stride], tc[a:b:stride], steps, nthreads=NTHREADS)
     _check(out, ref)
+
+
+def test_configs1_every_cell_on_the_v3_rom(rom_v3, oc, M):
+    """configs[1] as bench.py --cells-per-gpu 1024 runs it: 1,024 cells on the small-batch
+    mappings (k_ekf4's lane quads, k_cell<P_MPC>, k_bounds beside k_hild on the side stream)
+    with the v3 quintic ROM, every cell over the 1,010-step window, bitwise against the C
+    oracle (test_configs1_1024_cells_1010_steps runs the v2 linear tables)."""
+    soc0, tc = batch_inputs(1024)
+    steps = 1010
+    out = _gpu_sampled(M, rom_v3, soc0, tc, steps, 1)
+    ref = oc.run(rom_v3, soc0, tc, steps, nthreads=NTHREADS)
+    _check(out, ref)
+    assert (out["nexec"] == 100).any()
