@@ -5,7 +5,7 @@ included, so any difference is a bug).
   configs[1]  1 024 cells x 1 000 steps (+ warm-up 10), every cell
   configs[2]  65 536 cells x 1 000 steps, a 1/64 strided sample of cells checked
               (cells are independent, runMPC.m:83-112, so the oracle runs the sample alone)
-  configs[4]  65 536 cells x 1 000 steps at Np = 20 / Nc = 10, a 1/256 sample
+  configs[4]  65 536 cells x 1 000 steps at Np = 20 / Nc = 10, a 1/32 sample (2 048 cells)
   and configs[1] / configs[2] / configs[4] again on the v3 (quintic) ROM the bench runs
 
 The 1 000-step window covers the part of the charge where ~2 % of cells run
@@ -114,7 +114,7 @@ def test_configs2_every_cell_on_the_v3_rom(rom_v3, oc, M):
 
 def test_configs4_wide_65536_cells_1010_steps_sampled(rom, oc, M):
     soc0, tc = batch_inputs(65536)
-    steps, stride = 1010, 256
+    steps, stride = 1010, 32
     cfg = M.make_config(Np=20, Nc=10)
     out = _gpu_sampled(M, rom, soc0, tc, steps, stride, cfg=cfg)
     ref = oc.run(rom, soc0[::stride], tc[::stride], steps, nthreads=NTHREADS, Np=20, Nc=10)
