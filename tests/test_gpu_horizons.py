@@ -124,13 +124,13 @@ def test_configs4_wide_65536_cells_1010_steps_sampled(rom, oc, M):
 def test_configs3_rank7_shard_131072_cells_sampled(rom, oc, M):
     """configs[3] (1,048,576 cells on 8 GPUs): the last rank's 131,072-cell shard of the
     global input sequence, as bench.py --gpus 8 --total-cells 1048576 assigns it, through
-    one context on this GPU over the full 1,010-step window; a 1/512 sample bitwise."""
+    one context on this GPU over the full 1,010-step window; a 1/64 sample (2,048 cells) bitwise."""
     import bench
     total, world, rank = 1048576, 8, 7
     soc0, tc = batch_inputs(total)
     a, b = bench.shard_range(total, world, rank)
     assert b - a == 131072
-    steps, stride = 1010, 512
+    steps, stride = 1010, 64
     out = _gpu_sampled(M, rom, soc0[a:b], tc[a:b], steps, stride)
     ref = oc.run(rom, soc0[a:b:stride], tc[a:b:stride], steps, nthreads=NTHREADS)
     _check(out, ref)
