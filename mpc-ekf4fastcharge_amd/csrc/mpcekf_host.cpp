@@ -211,9 +211,11 @@ struct mpcekf_ctx {
   bool flush_roll = false;
   hipStream_t fstream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  // small batches (ncells <= MPCEKF_BOUNDS_SIDE, default 16384): k_bounds on fstream beside
-  // Hildreth.  Both read only what k_cell wrote and neither writes what the other reads;
-  // at 1,024 cells each is one wave's chain on a few CUs, so they overlap instead of adding.
+  // batches of ncells <= MPCEKF_BOUNDS_SIDE (default 0: off): k_bounds on fstream beside
+  // Hildreth.  Both read only what k_cell wrote and neither writes what the other reads.
+  // On by default up to 16,384 cells in rounds 4-5 (+1-3 %); with round 6's shorter k_hild the
+  // cross-stream fork and join cost more than the overlap at every size (256-16,384 cells,
+  // profiles/r06ab_bounds_side_small.txt), so it is an option.
   bool bounds_side = false;
   hipEvent_t ev_bfork = nullptr, ev_bjoin = nullptr;
   // staging for host trajectories / stage IO (grown on demand)
@@ -868,7 +870,7 @@ int mpcekf_ctx_create(const mpcekf_rom *rom, const mpcekf_config *cfg, int devic
   // MPCEKF_FLUSH_ROLL=1: the rolling flush schedule (results identical)
   if (const char *e = std::getenv("MPCEKF_FLUSH_ROLL")) X->flush_roll = std::atoi(e) != 0;
   {
-    int64_t side_max = 16384;
+    int64_t side_max = 0;
     if (const char *e = std::getenv("MPCEKF_BOUNDS_SIDE")) side_max = std::atoll(e);
     if (const char *e = std::getenv("MPCEKF_BOUNCE_MAX")) X->bounce_max = (size_t)std::atoll(e);
     if (const char *e = std::getenv("MPCEKF_CHUNK")) X->xchunk = std::max<size_t>((size_t)std::atoll(e), 4096);

@@ -335,8 +335,8 @@ def test_mpc_stage_edge_records(rom, oc, M):
 
 
 def test_bounds_side_stream_is_exact(rom, M):
-    """Small batches run k_bounds on a second stream beside Hildreth (MPCEKF_BOUNDS_SIDE:
-    up to 16,384 cells by default) and join it before k_flush / the next k_cell rewrite the
+    """k_bounds on a second stream beside Hildreth (MPCEKF_BOUNDS_SIDE, an option since
+    round 6; up to 16,384 cells by default before) joins it before k_flush / the next k_cell rewrite the
     records it reads: boundzk and the loop give the bits of k_bounds on the step's stream,
     over two flush windows, with per-kernel timing on (its events straddle the streams)."""
     import os
